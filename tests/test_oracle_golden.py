@@ -1,0 +1,138 @@
+"""Pin the CPU oracle against the reference's own outputs (golden vectors).
+
+Every fixture under tests/golden/ was produced by driving the reference
+(mapf_gym.FixedMapfGym, astar_4, makeBfsMap, Runner.run) in the build
+container (tests/golden/make_golden.py).  Bit-exact comparisons throughout.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from golden_io import G1_NAMES, Fuzz, load, unpack_obs
+
+
+def replay_g1(z):
+    """Replay a g1 episode in the oracle; yield (t, oracle outputs, fixture)."""
+    n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
+    world = z["map"]
+    H, W = world.shape
+    hmode = int(z["human_mode"])
+    cfg = O.make_config(H, W, n, fov, nch, use_da=int(z["use_da"]), use_hp=int(z["use_hp"]),
+                        human_mode=hmode, max_seq=z["seq"].shape[1], max_human_seq=len(z["hseq"]))
+    env = O.OracleEnv(cfg)
+    seqs = [z["seq"][i, :z["seq_len"][i]] for i in range(n)]
+    env.reset_fixed(world, seqs, z["hstart"], z["hgoal"], z["hseq"] if hmode == 2 else None)
+    return env
+
+
+@pytest.mark.parametrize("name", G1_NAMES)
+def test_g1_episode_bit_exact(name):
+    z = load(name)
+    n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
+    env = replay_g1(z)
+    p0, g0 = env.agents()
+    np.testing.assert_array_equal(p0, z["pos0"])
+    np.testing.assert_array_equal(g0, z["goal0"])
+    np.testing.assert_array_equal(env.human_path(), z["hpath0"])
+    np.testing.assert_array_equal(env.bfs(), z["bfs0"])
+    obs, vec = env.observe()
+    np.testing.assert_array_equal(obs, unpack_obs(z["obs0"], (n, nch, fov, fov)))
+    np.testing.assert_array_equal(vec, z["vec0"][0])
+    for t in range(int(z["steps"])):
+        o = env.step(z["actions"][t])
+        for k, ref in [("status", z["status"][t]), ("reward", z["reward"][t]), ("cost", z["cost"][t]),
+                       ("valid", z["valid"][t]), ("fixed", z["fixed"][t]), ("goals", z["goals"][t]),
+                       ("constr", z["constr"][t])]:
+            np.testing.assert_array_equal(o[k], ref.astype(o[k].dtype), err_msg=f"{name} t={t} {k}")
+        assert o["shadow"] == int(z["shadow"][t]), (name, t)
+        p, g = env.agents()
+        np.testing.assert_array_equal(p, z["pos"][t], err_msg=f"{name} t={t} pos")
+        np.testing.assert_array_equal(g, z["goal"][t], err_msg=f"{name} t={t} goal")
+        h = env.human()
+        np.testing.assert_array_equal(h["pos"], z["hpos"][t])
+        np.testing.assert_array_equal(h["next"], z["hnext"][t])
+        obs, vec = env.observe()
+        np.testing.assert_array_equal(obs, unpack_obs(z["obs"][t], (n, nch, fov, fov)), err_msg=f"{name} t={t} obs")
+        np.testing.assert_array_equal(vec, z["vec"][t], err_msg=f"{name} t={t} vec")
+    np.testing.assert_array_equal(env.bfs(), z["bfs_final"])
+    assert env.errors() == 0
+
+
+def run_fuzz_case(c):
+    H, W, n, fov = int(c["H"]), int(c["W"]), int(c["n"]), int(c["fov"])
+    world = c["map"].reshape(H, W)
+    cfg = O.make_config(H, W, n, fov, 6, use_da=int(c["use_da"]), use_hp=int(c["use_hp"]), max_seq=3)
+    env = O.OracleEnv(cfg)
+    hpath = c["hpath"]
+    # LoopingHuman path = start -> goal -> start, so start = path[0], goal = path[len//2]
+    env.reset_fixed(world, list(c["seq"]), hpath[0], hpath[len(hpath) // 2])
+    prev = c["prev"] if c["prev"].size == n else np.full(n, -1)
+    env.debug_set(int(c["hstep0"]), prev)
+    return env
+
+
+def test_g2_fuzz_one_step_bit_exact():
+    fz = Fuzz()
+    assert fz.count > 2000
+    bad = []
+    for i in range(fz.count):
+        c = fz.case(i)
+        n, fov = int(c["n"]), int(c["fov"])
+        env = run_fuzz_case(c)
+        np.testing.assert_array_equal(env.human_path(), c["hpath"])
+        p, g = env.agents()
+        np.testing.assert_array_equal(p, c["pos0"])
+        obs, vec = env.observe()
+        if not (np.array_equal(obs, unpack_obs(c["obs0"], (n, 6, fov, fov))) and np.array_equal(vec, c["vec0"])):
+            bad.append((i, "obs0"))
+            continue
+        o = env.step(c["actions"])
+        for k in ["status", "reward", "cost", "valid", "fixed", "goals", "constr"]:
+            if not np.array_equal(o[k], c[k].astype(o[k].dtype)):
+                bad.append((i, k))
+        if o["shadow"] != int(c["shadow"]):
+            bad.append((i, "shadow"))
+        p, g = env.agents()
+        if not (np.array_equal(p, c["pos1"]) and np.array_equal(g, c["goal1"])):
+            bad.append((i, "pos1"))
+        obs, vec = env.observe()
+        if not (np.array_equal(obs, unpack_obs(c["obs1"], (n, 6, fov, fov))) and np.array_equal(vec, c["vec1"])):
+            bad.append((i, "obs1"))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:10]}"
+
+
+def test_g3_astar_and_bfs_bit_exact():
+    z = load("g3_search")
+    offs = np.concatenate([[0], np.cumsum(z["path_len"])])
+    boff = 0
+    for k in range(len(z["mi"])):
+        world = z[f"map{int(z['mi'][k])}"]
+        s, g = z["s"][k], z["g"][k]
+        ref_path = z["path"][offs[k]:offs[k + 1]]
+        got = O.astar(world, s, g)
+        if not z["ok"][k]:
+            assert got is None
+        else:
+            np.testing.assert_array_equal(got, ref_path, err_msg=f"case {k}")
+        bfs = O.bfs_map(world, g)
+        ref = z["bfs"][boff:boff + world.size].reshape(world.shape)
+        boff += world.size
+        np.testing.assert_array_equal(bfs, ref, err_msg=f"bfs case {k}")
+
+
+def test_g4_gae_bit_exact():
+    z = load("g4_gae")
+    adv, ret = O.gae(z["rewards"], z["values"], z["last_v"], float(z["gamma"]), float(z["lam"]))
+    np.testing.assert_array_equal(ret, z["returns"])
+    cadv, cret = O.gae(z["cost_rewards"], z["cost_values"], z["last_cv"], float(z["gamma"]), float(z["lam"]))
+    np.testing.assert_array_equal(cret, z["cost_returns"])
+
+
+def test_runner_buffer_contract():
+    """BatchValues shapes from runner.py:104-115 (T=256, N=2, C=6, F=9)."""
+    z = load("g4_gae")
+    assert tuple(z["obs_shape"]) == (256, 2, 6, 9, 9)
+    assert tuple(z["hidden_shape"]) == (256, 2, 2, 512)
+    assert tuple(z["valid_shape"]) == (256, 2, 5)
+    assert tuple(z["ps_shape"]) == (256, 2, 5)
+    assert str(z["actions_dtype"]) == "int64"
