@@ -1,0 +1,161 @@
+"""Benchmark: lockstep agent-steps/sec for (env.step + observe), BASELINE.json's metric.
+
+A "step" = one lockstep step of every env on the GPU: the random policy's
+actions (Philox, on device) -> mapf_step (getActionStatus ... jointStep,
+human replans, BFS maps on goal changes) -> mapf_observe (all agents' FOV
+observations + vectors), i.e. runner.py:64-100 with a random policy.
+
+Default workload (N=1): BASELINE config c2 -- 4096 envs x 8 agents, 20x20
+generalised warehouse, FOV 11, 6 channels, Human with random goals,
+lifelong random goals.  Multi-GPU: one process per GPU (torch.distributed
+launcher); every rank owns its own 4096 envs (weak scaling, no data-path
+collective); value = all agent-steps / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "primal-ppo_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def observe_bytes_per_agent(C, F, H, W, N):
+    """C*F^2*4 + 16 (obs + vec writes) + (ceil(H*W/8) + 8N + 8)/N (reads)."""
+    return C * F * F * 4 + 16 + (-(-H * W // 8) + 8 * N + 8) / N
+
+
+def cpu_baseline(H, W, N, F, C, seconds):
+    """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host, one thread."""
+    from oracle import oracle as O
+    from mapf_amd.maps import generate_warehouse
+    world = generate_warehouse(H, W)
+    B = 32
+    cfg = O.make_config(H, W, N, F, C, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
+    batch = O.OracleBatch(cfg, world, B)
+    batch.run(5)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        batch.run(10)
+        steps += 10
+    dt = time.perf_counter() - t0
+    return {"value": round(B * N * steps / dt, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{B} envs x {N} agents, {H}x{W}, FOV {F}, random policy, {steps} lockstep steps "
+                      f"(step+observe) in {dt:.1f}s, single thread; reference Python measured 3,442 "
+                      f"agent-steps/s/core on this shape (BASELINE.md)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--size", type=int, default=20)
+    ap.add_argument("--fov", type=int, default=11)
+    ap.add_argument("--channels", type=int, default=6)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mapf_amd.config import make_config
+    from mapf_amd.env import BatchedMapfGym
+    from mapf_amd.maps import generate_warehouse
+
+    B, N, H, W, F, C = args.envs, args.agents, args.size, args.size, args.fov, args.channels
+    world = generate_warehouse(H, W)
+    env = BatchedMapfGym(make_config(B, H, W, num_agents=N, fov=F, num_channel=C, human_mode="random",
+                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B), device=dev)
+    env.reset_seeded(world)
+    obs, vec, acts = env.obs, env.vec, env.actions
+
+    def one_step():
+        env.random_actions(acts)
+        env.step(acts)
+        env.observe(obs, vec)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+
+    K = args.steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        e0, e1, e2 = ev[k]
+        e0.record()
+        env.random_actions(acts)
+        env.step(acts)
+        e1.record()
+        env.observe(obs, vec)
+        e2.record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(K)]))
+    obs_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(K)]))
+    counters = env.counters()
+
+    if rank == 0:
+        total_agent_steps = world_size * B * N * K
+        value = total_agent_steps / elapsed
+        bpa = observe_bytes_per_agent(C, F, H, W, N)
+        achieved = bpa * B * N / (obs_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (seeded warehouse episodes on device, uniform random policy)",
+            "config": {"workload": f"c2: {B} envs x {N} agents per GPU, {H}x{W} warehouse, FOV {F}, {C} channels, "
+                                   f"random policy, env.step+observe",
+                       "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
+                       "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
+                       "parallelism": f"env-shards x{world_size}"},
+            "breakdown_ms": {"actions+step+replan+bfs": round(step_ms, 4), "observe": round(obs_ms, 4)},
+            "roofline": {"kernel": "observe_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_agent": bpa, "agents_per_launch": B * N},
+            "device_counters": [int(x) for x in counters[:8]],
+        }
+        if world_size == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(H, W, N, F, C, args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    env.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

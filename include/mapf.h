@@ -1,0 +1,177 @@
+/*
+ * include/mapf.h -- C ABI of libmapf.so, the MI355X-native batched MAPF env.
+ *
+ * Drop-in boundary for the reference's per-step env API.
+ * The reference (Nielsencu/primal-ppo) has no FFI layer: its boundary is the
+ * Python method API of mapf_gym.MapfGym, called by runner.py:30-100 and
+ * evaluate.py:218-269 in this fixed order:
+ *
+ *   MapfGym() / FixedMapfGym(...)   mapf_gym.py:164-173 / :648-669  -> mapf_reset
+ *   getAllObservations()            mapf_gym.py:327-336             -> mapf_observe
+ *   getActionStatus(a)              mapf_gym.py:434-480             -> mapf_step (status)
+ *   calculateActionReward(a, st)    mapf_gym.py:483-511             -> mapf_step (reward, shadow_goals)
+ *   calculateCostReward(a)          mapf_gym.py:528-533             -> mapf_step (cost)
+ *   getTrainValid(a)                mapf_gym.py:535-550             -> mapf_step (train_valid)
+ *   jointStep(a, st)                mapf_gym.py:614-637             -> mapf_step (MAPF_STEP_COMMIT)
+ *   agent.bfsMap / makeBfsMap       mapf_gym.py:211-244             -> mapf_bfs
+ *   Runner.run GAE                  runner.py:117-149               -> mapf_gae
+ *   Model.train normalisation       model.py:106-113                -> mapf_normalize_advantages
+ *   Model.step sampling             model.py:38-40                  -> mapf_sample_actions
+ *
+ * Conventions
+ *  - One handle = B lockstep environments resident on one GPU (Structure of
+ *    Arrays in HBM).  The handle owns its device state; the caller owns every
+ *    output buffer (device pointers, e.g. torch tensors' data_ptr()).
+ *  - Calls are asynchronous on the caller's HIP stream (`stream` is a
+ *    hipStream_t passed as void*; NULL = the null stream).  A handle is not
+ *    thread-safe: one handle per GPU / process.
+ *  - Errors: 0 = OK, negative = error code (MAPF_E*); mapf_last_error() gives
+ *    a message (thread-local).  Impossible states the reference raises on
+ *    (mapf_gym.py:456,508,588,610; astar_4.py:109) are counted on the device
+ *    (mapf_get_counters) instead of raised.
+ *  - No C++ exceptions cross this boundary.
+ */
+#ifndef MAPF_H
+#define MAPF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAPF_ABI_VERSION 1
+
+#define MAPF_OK 0
+#define MAPF_EINVAL (-1)
+#define MAPF_EDEVICE (-2)
+#define MAPF_ENOMEM (-3)
+#define MAPF_ESTATE (-4)
+
+/* Environment configuration.  Field names follow alg_parameters.py
+ * (EnvParameters :27-48, TrainingParameters :76-78, NetParameters :103-104). */
+typedef struct mapf_config {
+    int32_t num_envs;        /* B: environments on this device                     */
+    int32_t num_agents;      /* N: EnvParameters.N_AGENTS, 1..64                    */
+    int32_t height, width;   /* H, W: grid, 1..128 each                             */
+    int32_t fov;             /* F: EnvParameters.FOV_SIZE, 1..16                    */
+    int32_t num_channel;     /* C: 5, 6 (NetParameters.NUM_CHANNEL) or 7 (+BFS ch) */
+    int32_t use_da, use_hp;  /* FixedMapfGym(useDA, useHP), mapf_gym.py:662-663    */
+    int32_t lifelong;        /* EnvParameters.LIFELONG                              */
+    int32_t human_mode;      /* 0 LoopingHuman, 1 Human (random goals), 2 FixedPathHuman */
+    int32_t goal_mode;       /* 0 agentsSequence (FixedMapfGym), 1 getFreeCell (MapfGym) */
+    int32_t fix_choice;      /* fixActions random.choice: 0 rotating rule, 1 Philox */
+    int32_t shared_map;      /* 1: one H x W map for all envs, 0: one map per env    */
+    int32_t keep_bfs;        /* maintain agent.bfsMap (makeBfsMap) for every agent   */
+    int32_t max_seq;         /* S: agentsSequence capacity per agent (goal_mode 0)  */
+    int32_t max_human_seq;   /* human pose sequence capacity (human_mode 2)          */
+    int32_t k_predict;       /* TrainingParameters.K_TIMESTEP_PREDICT                */
+    int32_t penalty_radius;  /* EnvParameters.PENALTY_RADIUS                         */
+    float action_cost;       /* EnvParameters.ACTION_COST                            */
+    float collision_cost;    /* EnvParameters.COLLISION_COST                         */
+    float human_collision_cost; /* EnvParameters.HUMAN_COLLISION_COST                */
+    float repeat_cost;       /* EnvParameters.REPEAT_POS                             */
+    float goal_reward;       /* EnvParameters.GOAL_REWARD (runner.py:89-91)          */
+    int32_t env_offset;      /* global index of env 0 (RNG counters; sharding)       */
+    uint32_t reserved;
+    uint64_t seed;           /* Philox key (SetupParameters.SEED)                    */
+} mapf_config;
+
+typedef struct mapf_env mapf_env;
+
+/* Reset specification.  All pointers are HOST pointers.
+ * mode 0 (FixedMapfGym, mapf_gym.py:648-669): maps + agent sequences +
+ *   human start/goal (LoopingHuman) or human pose sequence (FixedPathHuman).
+ * mode 1 (MapfGym, mapf_gym.py:164-184): maps + Philox draws for the human
+ *   entrance/goal and agent starts/goals (getFreeCell semantics). */
+typedef struct mapf_reset_spec {
+    int32_t mode;
+    int32_t reserved;
+    const int8_t *maps;          /* [shared_map ? 1 : B][H][W], values 0 (free) / -1 (obstacle) */
+    const int32_t *seq;          /* [B][N][S][2] (row, col)                    mode 0 */
+    const int32_t *seq_len;      /* [B][N], 1..S                               mode 0 */
+    const int32_t *human_start;  /* [B][2]                                     mode 0, human_mode 0 */
+    const int32_t *human_goal;   /* [B][2]                                     mode 0, human_mode 0 */
+    const int32_t *human_seq;    /* [B][max_human_seq][2]                      human_mode 2 */
+    const int32_t *human_seq_len;/* [B], 2..max_human_seq                      human_mode 2 */
+    uint64_t seed;               /* mode 1: overrides config.seed when non-zero */
+} mapf_reset_spec;
+
+/* Per-step outputs: DEVICE pointers owned by the caller; NULL = not written. */
+typedef struct mapf_step_out {
+    int8_t *status;          /* [B][N]  getActionStatus: 1, -1, -2, -3, -4          */
+    float *reward;           /* [B][N]  calculateActionReward (before GOAL_REWARD)   */
+    int32_t *shadow_goals;   /* [B]     calculateActionReward's shadowGoal           */
+    float *cost;             /* [B][N]  calculateCostReward                          */
+    float *train_valid;      /* [B][N][5] getTrainValid                              */
+    int32_t *actions_fixed;  /* [B][N]  actions after fixActions                      */
+    float *goals_reached;    /* [B][N]  jointStep's goalsReached                      */
+    float *constraints;      /* [B][N]  jointStep's constraintsViolated               */
+    float *reward_total;     /* [B][N]  reward + GOAL_REWARD where goal reached (runner.py:89-91) */
+} mapf_step_out;
+
+#define MAPF_STEP_COMMIT 1u  /* apply jointStep (move, goals, human, counters).  Without it
+                                only the pre-step outputs are produced and no state changes. */
+
+/* Host-side snapshot of the env state (checkpoint / test hook).  Any pointer
+ * may be NULL (skipped).  Cells are (row, col). */
+typedef struct mapf_state {
+    int32_t *pos;            /* [B][N][2]                                  */
+    int32_t *goal;           /* [B][N][2]                                  */
+    int32_t *last_action;    /* [B][N]   -1 = none (reset)                 */
+    int32_t *seq_cursor;     /* [B][N]   util.Sequence.curIdx              */
+    int32_t *human;          /* [B][10]  pos r,c; next r,c; goal r,c; step; path len; entrance r,c */
+    int32_t *human_path;     /* [B][path_capacity][2]                      */
+    uint32_t *clock;         /* [B]      steps since reset                 */
+} mapf_state;
+
+const char *mapf_last_error(void);
+int mapf_abi_version(void);
+
+int mapf_create(const mapf_config *cfg, int device, mapf_env **out);
+int mapf_destroy(mapf_env *env);
+int mapf_path_capacity(const mapf_env *env);       /* human path capacity per env */
+
+int mapf_reset(mapf_env *env, const mapf_reset_spec *spec, void *stream);
+
+/* One lockstep step for all B envs: actions are DEVICE int32 [B][N] in 0..4. */
+int mapf_step(mapf_env *env, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream);
+
+/* getAllObservations for all envs: obs DEVICE float [B][N][C][F][F], vec [B][N][4]. */
+int mapf_observe(mapf_env *env, float *obs, float *vec, void *stream);
+
+/* Uniform random policy (Philox, counter = env clock): DEVICE int32 [B][N]. */
+int mapf_random_actions(mapf_env *env, int32_t *actions, void *stream);
+
+/* Copy agent.bfsMap for every agent: DEVICE int16 [B][N][H][W] (requires keep_bfs). */
+int mapf_bfs(mapf_env *env, int16_t *dist, void *stream);
+
+/* Counters of impossible states / clamped events (host uint32[16]); synchronises the stream. */
+int mapf_get_counters(mapf_env *env, uint32_t *host16, void *stream);
+
+int mapf_get_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
+int mapf_set_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
+
+/* GAE over a [T][M] buffer (runner.py:117-149, numpy float32 semantics:
+ * f32(gamma) and f32(gamma*lam) constants, separate multiply and add).
+ * All pointers DEVICE float; v_last [M]. */
+int mapf_gae(const float *rewards, const float *values, const float *v_last, float *adv, float *ret,
+             int32_t T, int32_t M, double gamma, double lam, void *stream);
+
+/* model.py:106-113: adv = norm(ret - v); cadv = norm(cret - cv);
+ * norm(x) = (x - mean) / (std_unbiased + 1e-6); if mix: adv = (adv - lam*cadv)/(lam+1).
+ * DEVICE float [M] each; adv_out / cadv_out [M]. */
+int mapf_normalize_advantages(const float *ret, const float *v, const float *cret, const float *cv,
+                              float *adv_out, float *cadv_out, int32_t M, double lagrange, int32_t mix,
+                              void *stream);
+
+/* Model.step sampling (model.py:38-40): per row, inverse CDF of ps[M][5]
+ * with a Philox uniform (key seed, counter (row, step)).  DEVICE. */
+int mapf_sample_actions(const float *ps, int32_t ps_stride, int32_t *actions, int64_t *actions64, int32_t M,
+                        uint64_t seed, uint32_t step, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAPF_H */

@@ -1,0 +1,482 @@
+// primal-ppo_amd/csrc/mapf_api.cpp -- the C ABI (include/mapf.h) over the HIP kernels.
+//
+// Host responsibilities: validate configs and reset inputs (the reference
+// raises Python exceptions where this returns MAPF_EINVAL), own the device
+// SoA state, build the padded obstacle bitmaps and the fp64-derived lookup
+// tables, and order the kernels of one step on the caller's stream:
+//   step_kernel -> replan_kernel (human paths, if the human can replan)
+//               -> bfs_kernel (agent.bfsMap on goal changes, if keep_bfs)
+// No allocation, copy or synchronisation happens inside mapf_step /
+// mapf_observe, so both can be captured into a hipGraph by the caller.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mapf.h"
+#include "mapf_kernels.h"
+
+using namespace mapf;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t _e = (x);                                                                       \
+        if (_e != hipSuccess) return fail(MAPF_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+int next_pow2(int n) {
+    int g = 1;
+    while (g < n) g <<= 1;
+    return g;
+}
+}  // namespace
+
+struct mapf_env {
+    mapf_config cfg;
+    int device = 0;
+    DevEnv d{};
+    int parity = 1;
+    bool ready = false;
+    std::vector<void *> allocs;
+    template <class T>
+    int alloc(T *&p, size_t n) {
+        void *q = nullptr;
+        if (n == 0) n = 1;
+        if (hipMalloc(&q, n * sizeof(T)) != hipSuccess) return fail(MAPF_ENOMEM, "hipMalloc failed");
+        allocs.push_back(q);
+        p = reinterpret_cast<T *>(q);
+        return 0;
+    }
+};
+
+extern "C" {
+
+const char *mapf_last_error(void) { return g_err.c_str(); }
+int mapf_abi_version(void) { return MAPF_ABI_VERSION; }
+
+int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
+    if (!cfg || !out) return fail(MAPF_EINVAL, "null argument");
+    const mapf_config &c = *cfg;
+    if (c.num_envs < 1) return fail(MAPF_EINVAL, "num_envs must be >= 1");
+    if (c.num_agents < 1 || c.num_agents > 64) return fail(MAPF_EINVAL, "num_agents must be in 1..64");
+    if (c.height < 1 || c.height > 128 || c.width < 1 || c.width > 128) return fail(MAPF_EINVAL, "height/width must be in 1..128");
+    if (c.fov < 1 || c.fov > 16) return fail(MAPF_EINVAL, "fov must be in 1..16");
+    if (c.num_channel < 5 || c.num_channel > 7) return fail(MAPF_EINVAL, "num_channel must be 5, 6 or 7");
+    if (c.num_channel == 7 && !c.keep_bfs) return fail(MAPF_EINVAL, "num_channel 7 (BFS channel) needs keep_bfs");
+    if (c.human_mode < 0 || c.human_mode > 2) return fail(MAPF_EINVAL, "human_mode must be 0, 1 or 2");
+    if (c.goal_mode < 0 || c.goal_mode > 1) return fail(MAPF_EINVAL, "goal_mode must be 0 or 1");
+    if (c.fix_choice < 0 || c.fix_choice > 1) return fail(MAPF_EINVAL, "fix_choice must be 0 or 1");
+    if (c.max_seq < 1) return fail(MAPF_EINVAL, "max_seq must be >= 1");
+    if (c.human_mode == 2 && c.max_human_seq < 2) return fail(MAPF_EINVAL, "max_human_seq must be >= 2");
+    if (c.penalty_radius < 1 || c.penalty_radius > 64) return fail(MAPF_EINVAL, "penalty_radius must be in 1..64");
+    if (c.k_predict < 0 || c.k_predict > 64) return fail(MAPF_EINVAL, "k_predict must be in 0..64");
+    if (hipSetDevice(device) != hipSuccess) return fail(MAPF_EDEVICE, "hipSetDevice failed");
+
+    auto *e = new mapf_env();
+    e->cfg = c;
+    e->device = device;
+    DevEnv &d = e->d;
+    d.B = c.num_envs; d.N = c.num_agents; d.H = c.height; d.W = c.width; d.F = c.fov; d.C = c.num_channel;
+    d.P = c.fov / 2 > 1 ? c.fov / 2 : 1;
+    d.Hp = d.H + 2 * d.P;
+    d.WW = (d.W + 2 * d.P + 31) / 32;
+    d.G = next_pow2(d.N);
+    d.S = c.max_seq;
+    d.HS = c.max_human_seq > 2 ? c.max_human_seq : 2;
+    d.Lmax = 2 * d.H * d.W + 1;
+    d.use_da = c.use_da; d.use_hp = c.use_hp; d.lifelong = c.lifelong; d.human_mode = c.human_mode;
+    d.goal_mode = c.goal_mode; d.fix_choice = c.fix_choice; d.shared_map = c.shared_map ? 1 : 0;
+    d.keep_bfs = c.keep_bfs ? 1 : 0; d.k_predict = c.k_predict; d.R = c.penalty_radius;
+    d.action_cost = c.action_cost; d.collision_cost = c.collision_cost; d.human_collision_cost = c.human_collision_cost;
+    d.repeat_cost = c.repeat_cost; d.goal_reward = c.goal_reward;
+    d.env_offset = (uint32_t)c.env_offset;
+    d.seed = c.seed;
+    d.maxd2 = (d.H - 1) * (d.H - 1) + (d.W - 1) * (d.W - 1);
+    d.obs_envs = 64 / d.N > 1 ? 64 / d.N : 1;
+    if (d.obs_envs > d.B) d.obs_envs = d.B;
+
+    // fp64 lookup tables, computed exactly like the reference (numpy sqrt / python pow)
+    const double R = (double)c.penalty_radius;
+    std::vector<float> cost_lut(d.R * d.R + 1);
+    d.constr_d2 = -1;
+    for (int k = 0; k <= d.R * d.R; ++k) {
+        double v = R - std::sqrt((double)k);      // np.linalg.norm -> sqrt (mapf_gym.py:519)
+        if (!(v > 0.0)) v = 0.0;
+        cost_lut[k] = (float)(v / R);
+        if (v / R >= 0.01) d.constr_d2 = k;       // monotone in k (mapf_gym.py:633)
+    }
+    std::vector<double> dist_lut(d.maxd2 + 1);
+    for (int k = 0; k <= d.maxd2; ++k) dist_lut[k] = std::pow((double)k, 0.5);   // (...) ** .5 (:320)
+
+    const size_t BN = (size_t)d.B * d.N;
+    const size_t nmaps = d.shared_map ? 1 : (size_t)d.B;
+    int rc = 0;
+    uint32_t *map_bits = nullptr;
+    float *cl = nullptr;
+    double *dl = nullptr;
+    rc |= e->alloc(map_bits, nmaps * d.Hp * d.WW);
+    rc |= e->alloc(d.pos, BN); rc |= e->alloc(d.goal, BN); rc |= e->alloc(d.last_act, BN);
+    rc |= e->alloc(d.seq, BN * d.S); rc |= e->alloc(d.seq_len, BN); rc |= e->alloc(d.seq_cur, BN);
+    rc |= e->alloc(d.hpath, (size_t)d.B * d.Lmax);
+    rc |= e->alloc(d.hlen, d.B); rc |= e->alloc(d.hstep, d.B);
+    rc |= e->alloc(d.hpos, d.B); rc |= e->alloc(d.hgoal, d.B); rc |= e->alloc(d.hentr, d.B);
+    rc |= e->alloc(d.hseq, (size_t)d.B * d.HS); rc |= e->alloc(d.hseq_len, d.B); rc |= e->alloc(d.hseq_idx, d.B);
+    rc |= e->alloc(d.hreplans, d.B); rc |= e->alloc(d.clock, d.B);
+    if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * d.H * d.W);
+    rc |= e->alloc(d.counters, C_NUM);
+    rc |= e->alloc(d.replan_list, 2 * (size_t)d.B);
+    rc |= e->alloc(d.bfs_list, 2 * BN);
+    rc |= e->alloc(cl, cost_lut.size());
+    rc |= e->alloc(dl, dist_lut.size());
+    if (rc) {
+        std::string m = g_err;
+        mapf_destroy(e);
+        return fail(MAPF_ENOMEM, m);
+    }
+    d.map_bits = map_bits;
+    d.cost_lut = cl;
+    d.dist_lut = dl;
+    if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dl, dist_lut.data(), dist_lut.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d.counters, 0, C_NUM * sizeof(uint32_t)) != hipSuccess) {
+        mapf_destroy(e);
+        return fail(MAPF_EDEVICE, "initial upload failed");
+    }
+    *out = e;
+    return MAPF_OK;
+}
+
+int mapf_destroy(mapf_env *e) {
+    if (!e) return MAPF_OK;
+    (void)hipSetDevice(e->device);
+    for (void *p : e->allocs) (void)hipFree(p);
+    delete e;
+    return MAPF_OK;
+}
+
+int mapf_path_capacity(const mapf_env *e) { return e ? e->d.Lmax : 0; }
+
+int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
+    if (!e || !spec || !spec->maps) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    DevEnv &d = e->d;
+    const int B = d.B, N = d.N, H = d.H, W = d.W;
+    const size_t nmaps = d.shared_map ? 1 : (size_t)B;
+    if (spec->mode != 0 && spec->mode != 1) return fail(MAPF_EINVAL, "reset mode must be 0 or 1");
+    if (spec->mode == 1 && d.human_mode == 2) return fail(MAPF_EINVAL, "seeded reset needs human_mode 0 or 1");
+    if (spec->mode == 1 && spec->seed) d.seed = spec->seed;
+
+    // padded obstacle bitmaps
+    std::vector<uint32_t> bits(nmaps * d.Hp * d.WW, 0u);
+    for (size_t m = 0; m < nmaps; ++m) {
+        uint32_t *mb = bits.data() + m * d.Hp * d.WW;
+        for (int r = 0; r < d.Hp; ++r)
+            for (int c = 0; c < d.WW * 32; ++c) {
+                const int mr = r - d.P, mc = c - d.P;
+                bool ob;
+                if (mr < 0 || mr >= H || mc < 0 || mc >= W) ob = true;
+                else {
+                    const int8_t v = spec->maps[m * H * W + mr * W + mc];
+                    if (v != 0 && v != -1) return fail(MAPF_EINVAL, "map values must be 0 (free) or -1 (obstacle)");
+                    ob = v == -1;
+                }
+                if (ob) mb[r * d.WW + (c >> 5)] |= 1u << (c & 31);
+            }
+    }
+    auto free_at = [&](int b, int r, int c) {
+        if (r < 0 || r >= H || c < 0 || c >= W) return false;
+        const size_t m = d.shared_map ? 0 : (size_t)b;
+        return spec->maps[m * H * W + r * W + c] == 0;
+    };
+
+    std::vector<uint32_t> seq, hpos, hgoal, hseq;
+    std::vector<int32_t> seq_len, hseq_len;
+    if (spec->mode == 0) {
+        if (!spec->seq || !spec->seq_len) return fail(MAPF_EINVAL, "mode 0 needs seq and seq_len");
+        seq.assign((size_t)B * N * d.S, 0u);
+        seq_len.assign((size_t)B * N, 0);
+        for (int b = 0; b < B; ++b) {
+            std::vector<uint32_t> starts;
+            for (int i = 0; i < N; ++i) {
+                const size_t ai = (size_t)b * N + i;
+                const int len = spec->seq_len[ai];
+                if (len < 1 || len > d.S) return fail(MAPF_EINVAL, "seq_len out of range");
+                seq_len[ai] = len;
+                for (int k = 0; k < len; ++k) {
+                    const int r = spec->seq[(ai * d.S + k) * 2], c = spec->seq[(ai * d.S + k) * 2 + 1];
+                    if (r < 0 || r >= H || c < 0 || c >= W) return fail(MAPF_EINVAL, "sequence cell out of the map");
+                    seq[ai * d.S + k] = pack(r, c);
+                }
+                const int r0 = spec->seq[(ai * d.S) * 2], c0 = spec->seq[(ai * d.S) * 2 + 1];
+                if (!free_at(b, r0, c0)) return fail(MAPF_EINVAL, "agent start on an obstacle");
+                for (uint32_t s2 : starts)
+                    if (s2 == pack(r0, c0)) return fail(MAPF_EINVAL, "two agents start on the same cell");
+                starts.push_back(pack(r0, c0));
+            }
+        }
+        hpos.assign(B, 0u); hgoal.assign(B, 0u);
+        if (d.human_mode == 2) {
+            if (!spec->human_seq || !spec->human_seq_len) return fail(MAPF_EINVAL, "human_mode 2 needs human_seq");
+            hseq.assign((size_t)B * d.HS, 0u);
+            hseq_len.assign(B, 0);
+            for (int b = 0; b < B; ++b) {
+                const int len = spec->human_seq_len[b];
+                if (len < 2 || len > d.HS) return fail(MAPF_EINVAL, "human_seq_len out of range");
+                hseq_len[b] = len;
+                for (int k = 0; k < len; ++k) {
+                    const int r = spec->human_seq[((size_t)b * d.HS + k) * 2], c = spec->human_seq[((size_t)b * d.HS + k) * 2 + 1];
+                    if (!free_at(b, r, c)) return fail(MAPF_EINVAL, "human pose not on a free cell");
+                    hseq[(size_t)b * d.HS + k] = pack(r, c);
+                }
+            }
+        } else {
+            if (!spec->human_start || !spec->human_goal) return fail(MAPF_EINVAL, "mode 0 needs human_start/goal");
+            for (int b = 0; b < B; ++b) {
+                const int sr = spec->human_start[2 * b], sc = spec->human_start[2 * b + 1];
+                const int gr = spec->human_goal[2 * b], gc = spec->human_goal[2 * b + 1];
+                if (!free_at(b, sr, sc) || !free_at(b, gr, gc)) return fail(MAPF_EINVAL, "human start/goal not free");
+                if (sr == gr && sc == gc) return fail(MAPF_EINVAL, "human start == goal (astar_4 returns [])");
+                hpos[b] = pack(sr, sc);
+                hgoal[b] = pack(gr, gc);
+            }
+        }
+    }
+
+    HIPCHK(hipMemcpyAsync((void *)d.map_bits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d.counters, 0, C_NUM * sizeof(uint32_t), s));
+    if (spec->mode == 0) {
+        HIPCHK(hipMemcpyAsync(d.seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d.seq_len, seq_len.data(), seq_len.size() * 4, hipMemcpyHostToDevice, s));
+        if (d.human_mode == 2) {
+            HIPCHK(hipMemcpyAsync(d.hseq, hseq.data(), hseq.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d.hseq_len, hseq_len.data(), hseq_len.size() * 4, hipMemcpyHostToDevice, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(d.hpos, hpos.data(), hpos.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d.hgoal, hgoal.data(), hgoal.size() * 4, hipMemcpyHostToDevice, s));
+        }
+        launch_reset_fixed(d, s);
+    } else {
+        launch_reset_seeded(d, s);
+    }
+    launch_replan(d, 0, true, s);
+    if (d.keep_bfs) launch_bfs(d, 0, true, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // host staging buffers die at return
+    e->parity = 1;
+    e->ready = true;
+    return MAPF_OK;
+}
+
+int mapf_step(mapf_env *e, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream) {
+    if (!e || !actions) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_step before mapf_reset");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    StepOut o{};
+    if (out) {
+        o.status = out->status; o.reward = out->reward; o.shadow_goals = out->shadow_goals; o.cost = out->cost;
+        o.train_valid = out->train_valid; o.actions_fixed = out->actions_fixed; o.goals_reached = out->goals_reached;
+        o.constraints = out->constraints; o.reward_total = out->reward_total;
+    }
+    const int parity = e->parity;
+    launch_step(e->d, actions, o, flags, parity, s);
+    if (flags & MAPF_STEP_COMMIT) {
+        if (e->d.human_mode != 0) launch_replan(e->d, parity, false, s);
+        if (e->d.keep_bfs) launch_bfs(e->d, parity, false, s);
+        e->parity ^= 1;
+    }
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
+    if (!e || !obs || !vec) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_observe before mapf_reset");
+    HIPCHK(hipSetDevice(e->device));
+    launch_observe(e->d, obs, vec, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_random_actions(mapf_env *e, int32_t *actions, void *stream) {
+    if (!e || !actions) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_random_actions before mapf_reset");
+    HIPCHK(hipSetDevice(e->device));
+    launch_random_actions(e->d, actions, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_bfs(mapf_env *e, int16_t *dist, void *stream) {
+    if (!e || !dist) return fail(MAPF_EINVAL, "null argument");
+    if (!e->d.keep_bfs) return fail(MAPF_ESTATE, "keep_bfs is off");
+    HIPCHK(hipSetDevice(e->device));
+    const size_t n = (size_t)e->d.B * e->d.N * e->d.H * e->d.W * sizeof(int16_t);
+    HIPCHK(hipMemcpyAsync(dist, e->d.bfs, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return MAPF_OK;
+}
+
+int mapf_get_counters(mapf_env *e, uint32_t *host16, void *stream) {
+    if (!e || !host16) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(host16, e->d.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MAPF_OK;
+}
+
+int mapf_get_state(mapf_env *e, const mapf_state *h, void *stream) {
+    if (!e || !h) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    const DevEnv &d = e->d;
+    const size_t BN = (size_t)d.B * d.N;
+    std::vector<uint32_t> pos(BN), goal(BN), hpath((size_t)d.B * d.Lmax), hp(d.B), hg(d.B), he(d.B), clk(d.B);
+    std::vector<int8_t> la(BN);
+    std::vector<int32_t> cur(BN), hl(d.B), hs(d.B);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(pos.data(), d.pos, BN * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(goal.data(), d.goal, BN * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(la.data(), d.last_act, BN, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cur.data(), d.seq_cur, BN * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hpath.data(), d.hpath, hpath.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hl.data(), d.hlen, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hs.data(), d.hstep, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hp.data(), d.hpos, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hg.data(), d.hgoal, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(he.data(), d.hentr, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(clk.data(), d.clock, d.B * 4, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < BN; ++k) {
+        if (h->pos) { h->pos[2 * k] = prow(pos[k]); h->pos[2 * k + 1] = pcol(pos[k]); }
+        if (h->goal) { h->goal[2 * k] = prow(goal[k]); h->goal[2 * k + 1] = pcol(goal[k]); }
+        if (h->last_action) h->last_action[k] = la[k];
+        if (h->seq_cursor) h->seq_cursor[k] = cur[k];
+    }
+    for (int b = 0; b < d.B; ++b) {
+        const uint32_t *path = hpath.data() + (size_t)b * d.Lmax;
+        const int st = hs[b], len = hl[b];
+        const uint32_t nx = (len <= 0) ? hp[b] : (st >= len - 1 ? path[len - 1] : path[st + 1]);
+        if (h->human) {
+            int32_t *o = h->human + 10 * b;
+            o[0] = prow(hp[b]); o[1] = pcol(hp[b]); o[2] = prow(nx); o[3] = pcol(nx);
+            o[4] = prow(hg[b]); o[5] = pcol(hg[b]); o[6] = st; o[7] = len; o[8] = prow(he[b]); o[9] = pcol(he[b]);
+        }
+        if (h->human_path)
+            for (int k = 0; k < d.Lmax; ++k) {
+                h->human_path[((size_t)b * d.Lmax + k) * 2] = k < len ? prow(path[k]) : -1;
+                h->human_path[((size_t)b * d.Lmax + k) * 2 + 1] = k < len ? pcol(path[k]) : -1;
+            }
+        if (h->clock) h->clock[b] = clk[b];
+    }
+    return MAPF_OK;
+}
+
+int mapf_set_state(mapf_env *e, const mapf_state *h, void *stream) {
+    if (!e || !h) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_set_state before mapf_reset");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    DevEnv &d = e->d;
+    const size_t BN = (size_t)d.B * d.N;
+    HIPCHK(hipStreamSynchronize(s));
+    if (h->pos) {
+        std::vector<uint32_t> v(BN);
+        for (size_t k = 0; k < BN; ++k) {
+            const int r = h->pos[2 * k], c = h->pos[2 * k + 1];
+            if (r < 0 || r >= d.H || c < 0 || c >= d.W) return fail(MAPF_EINVAL, "pos out of the map");
+            v[k] = pack(r, c);
+        }
+        HIPCHK(hipMemcpy(d.pos, v.data(), BN * 4, hipMemcpyHostToDevice));
+    }
+    if (h->goal) {
+        std::vector<uint32_t> v(BN);
+        for (size_t k = 0; k < BN; ++k) {
+            const int r = h->goal[2 * k], c = h->goal[2 * k + 1];
+            if (r < 0 || r >= d.H || c < 0 || c >= d.W) return fail(MAPF_EINVAL, "goal out of the map");
+            v[k] = pack(r, c);
+        }
+        HIPCHK(hipMemcpy(d.goal, v.data(), BN * 4, hipMemcpyHostToDevice));
+    }
+    if (h->last_action) {
+        std::vector<int8_t> v(BN);
+        for (size_t k = 0; k < BN; ++k) {
+            if (h->last_action[k] < -1 || h->last_action[k] > 4) return fail(MAPF_EINVAL, "last_action out of range");
+            v[k] = (int8_t)h->last_action[k];
+        }
+        HIPCHK(hipMemcpy(d.last_act, v.data(), BN, hipMemcpyHostToDevice));
+    }
+    if (h->seq_cursor) HIPCHK(hipMemcpy(d.seq_cur, h->seq_cursor, BN * 4, hipMemcpyHostToDevice));
+    if (h->human_path && h->human) {
+        std::vector<uint32_t> path((size_t)d.B * d.Lmax, 0u);
+        std::vector<int32_t> hl(d.B);
+        for (int b = 0; b < d.B; ++b) {
+            const int len = h->human[10 * b + 7];
+            if (len < 1 || len > d.Lmax) return fail(MAPF_EINVAL, "human path length out of range");
+            hl[b] = len;
+            for (int k = 0; k < len; ++k)
+                path[(size_t)b * d.Lmax + k] = pack(h->human_path[((size_t)b * d.Lmax + k) * 2],
+                                                    h->human_path[((size_t)b * d.Lmax + k) * 2 + 1]);
+        }
+        HIPCHK(hipMemcpy(d.hpath, path.data(), path.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hlen, hl.data(), d.B * 4, hipMemcpyHostToDevice));
+    }
+    if (h->human) {
+        std::vector<uint32_t> hp(d.B), hg(d.B), he(d.B);
+        std::vector<int32_t> hs(d.B);
+        for (int b = 0; b < d.B; ++b) {
+            const int32_t *o = h->human + 10 * b;
+            hp[b] = pack(o[0], o[1]); hg[b] = pack(o[4], o[5]); hs[b] = o[6]; he[b] = pack(o[8], o[9]);
+        }
+        HIPCHK(hipMemcpy(d.hpos, hp.data(), d.B * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hgoal, hg.data(), d.B * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hstep, hs.data(), d.B * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hentr, he.data(), d.B * 4, hipMemcpyHostToDevice));
+    }
+    if (h->clock) HIPCHK(hipMemcpy(d.clock, h->clock, d.B * 4, hipMemcpyHostToDevice));
+    return MAPF_OK;
+}
+
+int mapf_gae(const float *rewards, const float *values, const float *v_last, float *adv, float *ret, int32_t T,
+             int32_t M, double gamma, double lam, void *stream) {
+    if (!rewards || !values || !v_last || !adv || !ret) return fail(MAPF_EINVAL, "null argument");
+    if (T < 1 || M < 1) return fail(MAPF_EINVAL, "T and M must be >= 1");
+    // numpy: GAMMA * next_nonterminal (python floats) then * f32 array -> f32(gamma);
+    //        GAMMA * LAM * next_nonterminal -> f32(gamma * lam)   (runner.py:134-140)
+    launch_gae(rewards, values, v_last, adv, ret, T, M, (float)(gamma * 1.0), (float)(gamma * lam * 1.0),
+               (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_normalize_advantages(const float *ret, const float *v, const float *cret, const float *cv, float *adv_out,
+                              float *cadv_out, int32_t M, double lagrange, int32_t mix, void *stream) {
+    if (!ret || !v || !cret || !cv || !adv_out || !cadv_out) return fail(MAPF_EINVAL, "null argument");
+    if (M < 1) return fail(MAPF_EINVAL, "M must be >= 1");
+    launch_normalize(ret, v, cret, cv, adv_out, cadv_out, M, (float)lagrange, (float)(lagrange + 1.0), mix,
+                     (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_sample_actions(const float *ps, int32_t ps_stride, int32_t *actions, int64_t *actions64, int32_t M,
+                        uint64_t seed, uint32_t step, void *stream) {
+    if (!ps || (!actions && !actions64)) return fail(MAPF_EINVAL, "null argument");
+    if (M < 1 || ps_stride < 5) return fail(MAPF_EINVAL, "bad M / stride");
+    launch_sample(ps, ps_stride, actions, actions64, M, seed, step, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+}  // extern "C"

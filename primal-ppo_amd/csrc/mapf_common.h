@@ -1,0 +1,112 @@
+// primal-ppo_amd/csrc/mapf_common.h -- device-side layout and helpers shared by
+// the MAPF kernels (gfx950, wave64).
+//
+// HBM layout (Structure of Arrays, one handle = B lockstep envs):
+//   map_bits  [nmaps][Hp][WW] u32   obstacle bitmap padded by P=max(F/2,1) cells
+//                                   of 1s on every side (off-map == obstacle)
+//   pos, goal [B*N] u32             packed cell (row | col << 16)
+//   last_act  [B*N] i8              -1 = none (Agent.invalidActions[2] empty)
+//   seq       [B*N*S] u32, seq_len/seq_cur [B*N]   agentsSequence
+//   hpath     [B*Lmax] u32, hlen/hstep [B], hpos/hgoal/hentr [B]   human
+//   bfs       [B*N*H*W] i16         agent.bfsMap (keep_bfs)
+//   counters  [32] u32              error counters + work-list counts
+//   replan_list [2][B], bfs_list [2][B*N]  per-step work lists (step parity)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mapf {
+
+constexpr int NA = 5;           // EnvParameters.N_ACTIONS
+constexpr int FREECELL_TRIES = 64;
+
+// Agent.dirDict / oppositeAction (mapf_gym.py:97-100); x = row, y = col.
+__host__ __device__ constexpr int dr(int a) { return a == 2 ? 1 : (a == 4 ? -1 : 0); }
+__host__ __device__ constexpr int dc(int a) { return a == 1 ? 1 : (a == 3 ? -1 : 0); }
+__host__ __device__ constexpr int opp(int a) { return a == 0 ? 0 : (a == 1 ? 3 : (a == 2 ? 4 : (a == 3 ? 1 : 2))); }
+
+// Philox purposes (shared spec with oracle/mapf_oracle.c).
+enum : uint32_t { P_ENTRANCE = 1, P_HGOAL0 = 2, P_START = 3, P_GOAL0 = 4, P_GOAL = 5,
+                  P_HGOAL = 6, P_FIX = 7, P_ACT = 8, P_SAMPLE = 9 };
+
+// counters[] slots
+enum : int { C_BAD_ACTION = 0, C_FIX_BOUND = 1, C_EMPTY_VIABLE = 2, C_FREECELL = 3,
+             C_UNREACHABLE = 4, C_BAD_STATUS = 5, C_PATH_OVERFLOW = 6,
+             C_REPLAN_COUNT = 8,   // [8],[9]  by step parity
+             C_BFS_COUNT = 10,     // [10],[11]
+             C_NUM = 32 };
+
+struct DevEnv {
+    int B, N, H, W, F, C, P, Hp, WW, G, S, HS, Lmax;
+    int use_da, use_hp, lifelong, human_mode, goal_mode, fix_choice, shared_map, keep_bfs, k_predict, R;
+    float action_cost, collision_cost, human_collision_cost, repeat_cost, goal_reward;
+    uint32_t env_offset;
+    uint64_t seed;
+    int maxd2;
+    int constr_d2;            // largest d2 with (R - sqrt(d2)) / R >= 0.01 in fp64 (mapf_gym.py:633)
+    int obs_envs;             // envs per observe workgroup
+    const uint32_t *map_bits;
+    uint32_t *pos, *goal;
+    int8_t *last_act;
+    uint32_t *seq;
+    int32_t *seq_len, *seq_cur;
+    uint32_t *hpath;
+    int32_t *hlen, *hstep;
+    uint32_t *hpos, *hgoal, *hentr;
+    uint32_t *hseq;
+    int32_t *hseq_len, *hseq_idx;
+    uint32_t *hreplans, *clock;
+    int16_t *bfs;
+    uint32_t *counters, *replan_list, *bfs_list;
+    const float *cost_lut;    // [R*R+1]: float32(max(R - sqrt(d2), 0) / R) (fp64 like the reference)
+    const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
+};
+
+__host__ __device__ inline uint32_t pack(int r, int c) { return (uint32_t)(r & 0xFFFF) | ((uint32_t)c << 16); }
+__host__ __device__ inline int prow(uint32_t p) { return (int)(p & 0xFFFF); }
+__host__ __device__ inline int pcol(uint32_t p) { return (int)(p >> 16); }
+
+// Philox4x32-10 (same constants/rounds as oracle/mapf_oracle.c: philox()).
+struct u32x4 { uint32_t x, y, z, w; };
+__device__ inline u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t seed) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+
+// Obstacle test on the padded bitmap (off-map cells read as 1 within P cells).
+__device__ inline bool obstacle_at(const DevEnv &e, const uint32_t *bits, int r, int c) {
+    if (r < -e.P || r >= e.H + e.P || c < -e.P || c >= e.W + e.P) return true;
+    int rr = r + e.P, cc = c + e.P;
+    return (bits[rr * e.WW + (cc >> 5)] >> (cc & 31)) & 1u;
+}
+__device__ inline bool in_map(const DevEnv &e, int r, int c) { return r >= 0 && r < e.H && c >= 0 && c < e.W; }
+
+__device__ inline const uint32_t *env_map(const DevEnv &e, int b) {
+    return e.map_bits + (e.shared_map ? 0 : (size_t)b * e.Hp * e.WW);
+}
+
+// Human.getNextPos (mapf_gym.py:46-50).
+__device__ inline uint32_t human_next(const DevEnv &e, int b) {
+    int st = e.hstep[b], len = e.hlen[b];
+    const uint32_t *path = e.hpath + (size_t)b * e.Lmax;
+    return st >= len - 1 ? path[len - 1] : path[st + 1];
+}
+
+// Wave-level helpers ---------------------------------------------------------
+__device__ inline int lane_id() { return threadIdx.x & 63; }
+__device__ inline uint64_t ballot(bool p) { return __ballot(p); }
+__device__ inline uint32_t shfl32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+__device__ inline uint64_t shfl64(uint64_t v, int src) {
+    uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+}  // namespace mapf

@@ -1,0 +1,71 @@
+// primal-ppo_amd/csrc/mapf_group.h -- lane-group primitives.
+//
+// One environment = one group of G lanes (G = next pow2 >= N, G <= 64), lane
+// i of the group = agent i, so a wave holds 64/G environments.  Every piece of
+// the reference that is sequential over agents (getActionStatus's scan,
+// fixActions' worklist, jointStep's goal draws) runs as a GROUP-UNIFORM loop:
+// every lane of the group executes the same iterations, exchanging per-agent
+// values with ds_bpermute (shfl) and 64-bit ballots restricted to the group.
+#pragma once
+#include "mapf_common.h"
+
+namespace mapf {
+
+struct Group {
+    int G, base, i;          // group width, first lane of the group, agent slot
+    uint64_t wmask;          // group's lanes within the wave ballot
+    __device__ Group(int G_) : G(G_) {
+        int lane = lane_id();
+        base = lane & ~(G_ - 1);
+        i = lane & (G_ - 1);
+        wmask = (G_ == 64) ? ~0ull : (((1ull << G_) - 1ull) << base);
+    }
+    // bit j = predicate of agent j of this group
+    __device__ uint64_t ballot(bool p) const { return (__ballot(p) & wmask) >> base; }
+    __device__ uint32_t shfl(uint32_t v, int j) const { return shfl32(v, base + j); }
+    __device__ int shfl_i(int v, int j) const { return (int)shfl32((uint32_t)v, base + j); }
+    __device__ uint64_t shfl64(uint64_t v, int j) const { return mapf::shfl64(v, base + j); }
+};
+
+__device__ inline int ctz64(uint64_t x) { return __builtin_ctzll(x); }
+__device__ inline int popc64(uint64_t x) { return __popcll(x); }
+__device__ inline uint64_t below(int i) { return i >= 64 ? ~0ull : ((1ull << i) - 1ull); }
+__device__ inline int nth_bit(unsigned m, int n) {  // position of the n-th set bit (n >= 0)
+    for (int t = 0; t < 32; ++t)
+        if ((m >> t) & 1u) { if (n == 0) return t; --n; }
+    return -1;
+}
+
+// util.getFreeCell (util.py:67-76) as a specified Philox stream -- identical
+// to oracle/mapf_oracle.c free_cell(): draw k uses counter
+// (env, purpose | agent << 8, epoch, k); row = mulhi(w0, H), col = mulhi(w1, W);
+// after FREECELL_TRIES rejections the last draw's w2 picks uniformly among
+// the admissible cells in row-major order.  `ok(r, c)` must be group-uniform
+// (it may ballot).  Returns false when no cell is admissible.
+template <class Ok>
+__device__ bool group_free_cell(const DevEnv &e, uint32_t env_id, uint32_t purpose, int agent, uint32_t epoch,
+                                Ok ok, int &r, int &c) {
+    u32x4 o = {0, 0, 0, 0};
+    const uint32_t c1 = purpose | ((uint32_t)agent << 8);
+    for (int k = 0; k < FREECELL_TRIES; ++k) {
+        o = philox(env_id, c1, epoch, (uint32_t)k, e.seed);
+        r = (int)__umulhi(o.x, (uint32_t)e.H);
+        c = (int)__umulhi(o.y, (uint32_t)e.W);
+        if (ok(r, c)) return true;
+    }
+    int cnt = 0;
+    for (int rr = 0; rr < e.H; ++rr)
+        for (int cc = 0; cc < e.W; ++cc)
+            if (ok(rr, cc)) ++cnt;
+    if (cnt == 0) return false;
+    int pick = (int)__umulhi(o.z, (uint32_t)cnt);
+    for (int rr = 0; rr < e.H; ++rr)
+        for (int cc = 0; cc < e.W; ++cc)
+            if (ok(rr, cc)) {
+                if (pick == 0) { r = rr; c = cc; return true; }
+                --pick;
+            }
+    return false;
+}
+
+}  // namespace mapf

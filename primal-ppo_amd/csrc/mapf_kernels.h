@@ -1,0 +1,36 @@
+// primal-ppo_amd/csrc/mapf_kernels.h -- host-side launchers of the MAPF kernels.
+#pragma once
+#include "mapf_common.h"
+
+namespace mapf {
+
+struct StepOut {          // device pointers (mapf_step_out)
+    int8_t *status;
+    float *reward;
+    int32_t *shadow_goals;
+    float *cost;
+    float *train_valid;
+    int32_t *actions_fixed;
+    float *goals_reached;
+    float *constraints;
+    float *reward_total;
+};
+
+void launch_step(const DevEnv &e, const int32_t *actions, const StepOut &out, uint32_t flags, int parity,
+                 hipStream_t s);
+void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s);
+// human path (re)planning for the envs in replan_list[parity] (or all envs when all = true)
+void launch_replan(const DevEnv &e, int parity, bool all, hipStream_t s);
+// agent BFS maps for bfs_list[parity] (or all agents when all = true)
+void launch_bfs(const DevEnv &e, int parity, bool all, hipStream_t s);
+void launch_observe(const DevEnv &e, float *obs, float *vec, hipStream_t s);
+void launch_reset_fixed(const DevEnv &e, hipStream_t s);
+void launch_reset_seeded(const DevEnv &e, hipStream_t s);
+void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,
+                float gl, hipStream_t s);
+void launch_normalize(const float *ret, const float *v, const float *cret, const float *cv, float *adv,
+                      float *cadv, int M, float lam, float lam1, int mix, hipStream_t s);
+void launch_sample(const float *ps, int stride, int32_t *a32, int64_t *a64, int M, uint64_t seed, uint32_t step,
+                   hipStream_t s);
+
+}  // namespace mapf

@@ -1,0 +1,330 @@
+// primal-ppo_amd/csrc/mapf_step.hip -- one lockstep env step for B envs.
+//
+// Reference semantics (Nielsencu/primal-ppo mapf_gym.py), in runner.py:64-100
+// order: getActionStatus (:434-480) -> calculateActionReward (:483-511) ->
+// calculateCostReward (:528-533) -> getTrainValid (:535-550) -> jointStep
+// (:614-637: fixActions :552-612, takeStep :158-161, lifelong goals :623-627,
+// human.nextStep :25-31, constraintsViolated :631-633).  The masks that the
+// reference recomputes at the END of jointStep (getUnconditionallyGoodActions
+// :404-430) are a pure function of the state, so this kernel recomputes them
+// at the START of the next step instead of storing them.
+//
+// Mapping: lane = agent, G lanes per env (mapf_group.h).  Conflicts are never
+// materialised as the reference's restrictedAction dict: for distinct agent
+// positions (guaranteed: starts are validated distinct and resolved moves
+// never collide), the dict's content is exactly
+//   (j, b) in R_i[a]  <=>  p_i+d(a) == p_j+d(b)  or  (p_i+d(a) == p_j and p_j+d(b) == p_i)
+// and its key set is  a in keys(i) <=> exists j != i: |p_i+d(a) - p_j|_1 <= 1.
+// (The reference's pruning test, mapf_gym.py:387, never removes a true
+// conflict when positions differ.)
+//
+// HBM traffic per agent-step: ~16 B state read, ~50 B outputs (+ rare BFS /
+// replan work lists) -- latency bound, not bandwidth bound.
+#include "mapf_group.h"
+#include "mapf_kernels.h"
+
+namespace mapf {
+
+__global__ __launch_bounds__(256) void step_kernel(DevEnv e, const int32_t *__restrict__ actions, StepOut out,
+                                                   uint32_t flags, int parity) {
+    const int G = e.G, N = e.N;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = gt / G;
+    if (gt == 0 && (flags & 1u)) {       // zero the other parity's work-list counts (consumed last step)
+        e.counters[C_REPLAN_COUNT + (parity ^ 1)] = 0;
+        e.counters[C_BFS_COUNT + (parity ^ 1)] = 0;
+    }
+    if (b >= e.B) return;                 // whole group leaves together
+    Group g(G);
+    const int i = g.i;
+    const bool act = i < N;
+    const size_t ai = (size_t)b * N + i;
+    const uint32_t env_id = e.env_offset + (uint32_t)b;
+    const uint32_t clock = e.clock[b];
+
+    // ---- state -----------------------------------------------------------
+    const uint32_t pp = act ? e.pos[ai] : 0xFFFFFFFFu;
+    const int pr = act ? prow(pp) : -100, pc = act ? pcol(pp) : -100;
+    const uint32_t gg = act ? e.goal[ai] : 0u;
+    const int la = act ? (int)e.last_act[ai] : -1;
+    int a = act ? actions[ai] : 0;
+    if (act && (a < 0 || a >= NA)) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
+    const uint32_t *bits = env_map(e, b);
+    const uint32_t hp = e.hpos[b], hn = human_next(e, b);
+
+    // ---- getInvalidActions (mapf_gym.py:339-360) ---------------------------
+    unsigned st_mask = 0, hu_mask = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const int r = pr + dr(k), c = pc + dc(k);
+        if (!in_map(e, r, c) || obstacle_at(e, bits, r, c)) st_mask |= 1u << k;
+        else if (pack(r, c) == hn) hu_mask |= 1u << k;
+        else if (pp == hn && pack(r, c) == hp) hu_mask |= 1u << k;
+    }
+    const unsigned rep_mask = la >= 0 ? 1u << opp(la) : 0u;
+
+    // ---- getRestrictedActions (:363-402), evaluated against actual actions --
+    const int Xr = pr + dr(a), Xc = pc + dc(a);
+    unsigned keys = 0, conf = 0;   // conf: my actions t that collide with some j's actual action
+    uint64_t M = 0;                // agents j colliding with my actual action
+    for (int j = 0; j < N; ++j) {
+        const uint32_t pj = g.shfl(pp, j);
+        const int aj = g.shfl_i(a, j);
+        if (!act || j == i) continue;
+        const int qr = prow(pj), qc = pcol(pj);
+        if (abs(qr - pr) + abs(qc - pc) > 2) continue;
+        const int Yr = qr + dr(aj), Yc = qc + dc(aj);
+        unsigned cj = 0;
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            const int tr = pr + dr(t), tc = pc + dc(t);
+            if (abs(tr - qr) + abs(tc - qc) <= 1) keys |= 1u << t;
+            if ((tr == Yr && tc == Yc) || (tr == qr && tc == qc && Yr == pr && Yc == pc)) cj |= 1u << t;
+        }
+        conf |= cj;
+        if ((cj >> a) & 1u) M |= 1ull << j;
+    }
+    const unsigned good = ~(st_mask | hu_mask | rep_mask | keys) & 0x1Fu;   // setdiff1d (:423)
+
+    // ---- getActionStatus (:434-480) ----------------------------------------
+    int s0;
+    bool cb = false;
+    if ((st_mask >> a) & 1u) s0 = -1;
+    else if ((hu_mask >> a) & 1u) s0 = -2;
+    else if ((good >> a) & 1u) s0 = 1;
+    else if (M) { s0 = -3; cb = true; }
+    else s0 = ((rep_mask >> a) & 1u) ? -4 : 1;
+    // sequential scan: agent k is skipped if an earlier agent already set it to
+    // -3; an agent taking the conflict branch sets itself and all of M_k to -3
+    // (overwriting earlier statuses, :471-472).
+    uint64_t T = 0;
+    for (uint64_t rem = g.ballot(act && cb); rem; rem &= rem - 1) {
+        const int k = ctz64(rem);
+        const uint64_t Mk = g.shfl64(M, k);
+        if (!((T >> k) & 1ull)) T |= Mk | (1ull << k);
+    }
+    const int st = ((T >> i) & 1ull) ? -3 : s0;
+
+    // ---- calculateActionReward (:483-511) ----------------------------------
+    float rw;
+    switch (st) {
+        case -1: rw = e.collision_cost; break;
+        case -2: rw = e.human_collision_cost; break;
+        case -3: rw = e.collision_cost; break;
+        case -4: rw = e.repeat_cost; break;
+        default: rw = e.action_cost; break;
+    }
+    const bool shadow_hit = act && st == 1 && Xr == prow(gg) && Xc == pcol(gg);
+    const uint64_t shadow_mask = g.ballot(shadow_hit);
+
+    // ---- calculateCostReward (:528-533): pre-step human next position -------
+    float cost = 0.f;
+    {
+        const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
+        const int d2 = d0 * d0 + d1 * d1;
+        if (d2 <= e.R * e.R) cost = e.cost_lut[d2];
+    }
+
+    if (act) {
+        if (out.status) out.status[ai] = (int8_t)st;
+        if (out.reward) out.reward[ai] = rw;
+        if (out.cost) out.cost[ai] = cost;
+        if (out.train_valid) {   // getTrainValid (:535-550)
+            float *tv = out.train_valid + ai * NA;
+#pragma unroll
+            for (int t = 0; t < NA; ++t)
+                tv[t] = (((good >> t) & 1u) || (((keys >> t) & 1u) && !((conf >> t) & 1u))) ? 1.f : 0.f;
+        }
+    }
+    if (i == 0 && out.shadow_goals) out.shadow_goals[b] = popc64(shadow_mask);
+    if (!(flags & 1u)) return;
+
+    // ---- jointStep: fixActions (:552-612) ----------------------------------
+    int fixed = a;
+    const uint64_t need = g.ballot(act && (st == -1 || st == -2 || st == -3));
+    if (need) {
+        int assigned = (act && st == 1) ? a : -1;
+        const uint64_t qm = g.ballot(act && st < 0);
+        int q = (act && st < 0) ? popc64(qm & below(i)) : -1;
+        int next_q = popc64(qm), head = 0, rounds = 0, iters = 0;
+        const unsigned viable_me = ~(st_mask | hu_mask) & 0x1Fu;
+        while (head < next_q) {
+            if (++iters > 64 * N) {
+                if (i == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
+                break;
+            }
+            const uint64_t hm = g.ballot(act && q == head);
+            const int idx = ctz64(hm);
+            ++head;
+            const unsigned good_idx = g.shfl(good, idx);
+            if (good_idx) {
+                if (i == idx) { assigned = __builtin_ctz(good_idx); q = -1; }
+                continue;
+            }
+            const unsigned viable = g.shfl(viable_me, idx);
+            const uint32_t pidx = g.shfl(pp, idx);
+            const int ir = prow(pidx), ic = pcol(pidx);
+            unsigned cj = 0;   // idx's actions that collide with MY assigned action
+            if (act && i != idx && assigned >= 0 && abs(pr - ir) + abs(pc - ic) <= 2) {
+                const int Yr = pr + dr(assigned), Yc = pc + dc(assigned);
+#pragma unroll
+                for (int t = 0; t < NA; ++t) {
+                    const int tr = ir + dr(t), tc = ic + dc(t);
+                    if ((tr == Yr && tc == Yc) || (tr == pr && tc == pc && Yr == ir && Yc == ic)) cj |= 1u << t;
+                }
+            }
+            unsigned U = 0;
+#pragma unroll
+            for (int t = 0; t < NA; ++t)
+                if (g.ballot((cj >> t) & 1u)) U |= 1u << t;
+            const unsigned fr = viable & ~U;
+            if (fr) {
+                if (i == idx) { assigned = __builtin_ctz(fr); q = -1; }
+                continue;
+            }
+            const int nv = __popc(viable);
+            int rsel = 0;
+            if (nv == 0) {      // reference: random.choice([]) raises IndexError
+                if (i == idx) atomicAdd(&e.counters[C_EMPTY_VIABLE], 1u);
+            } else {
+                int pick;
+                if (e.fix_choice == 0) pick = rounds % nv;
+                else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)rounds, e.seed).x,
+                                          (uint32_t)nv);
+                ++rounds;
+                rsel = nth_bit(viable, pick);
+                const uint64_t ev = g.ballot((cj >> rsel) & 1u);   // evicted (ascending agent order)
+                if ((ev >> i) & 1ull) { assigned = -1; q = next_q + popc64(ev & below(i)); }
+                next_q += popc64(ev);
+            }
+            if (i == idx) { assigned = rsel; q = -1; }
+        }
+        fixed = assigned >= 0 ? assigned : 0;
+    }
+
+    // ---- takeStep (:158-161) + lifelong goals (:623-627) --------------------
+    const int nr = pr + dr(fixed), nc = pc + dc(fixed);
+    const uint32_t np = act ? pack(nr, nc) : 0xFFFFFFFFu;
+    const bool reached = act && e.lifelong && np == gg;
+    uint32_t ng = gg;
+    int cur = 0;
+    if (e.goal_mode == 0) {
+        if (reached) {   // Sequence.getNext (util.py:33-39)
+            cur = e.seq_cur[ai];
+            const int len = e.seq_len[ai];
+            const uint32_t *s = e.seq + ai * e.S;
+            if (cur >= len) ng = s[len - 1];
+            else ng = s[cur++];
+            e.seq_cur[ai] = cur;
+        }
+    } else {
+        // getNextGoal(worldWithAgentsAndGoals()) for the reached agents in
+        // index order: agents <= k at new positions, > k at old; goals of
+        // agents < k already replaced (mapf_gym.py:200-209, :620-627).
+        for (uint64_t rem = g.ballot(reached); rem; rem &= rem - 1) {
+            const int k = ctz64(rem);
+            const uint32_t mypos = (i <= k) ? np : pp;
+            const uint32_t mygoal = ng;
+            auto ok = [&](int r, int c) -> bool {
+                if (obstacle_at(e, bits, r, c)) return false;
+                const uint32_t cell = pack(r, c);
+                return g.ballot(act && (mypos == cell || mygoal == cell)) == 0ull;
+            };
+            int r, c;
+            if (!group_free_cell(e, env_id, P_GOAL, k, clock, ok, r, c)) {
+                if (i == k) atomicAdd(&e.counters[C_FREECELL], 1u);
+                r = prow(g.shfl(np, k)); c = pcol(g.shfl(np, k));
+            }
+            if (i == k) ng = pack(r, c);
+        }
+    }
+    if (act) {
+        e.pos[ai] = np;
+        e.goal[ai] = ng;
+        e.last_act[ai] = (int8_t)fixed;
+        if (reached && e.keep_bfs) {
+            const uint32_t slot = atomicAdd(&e.counters[C_BFS_COUNT + parity], 1u);
+            e.bfs_list[(size_t)parity * e.B * N + slot] = (uint32_t)ai;
+        }
+    }
+
+    // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94) -------------------
+    uint32_t hp_new;
+    {
+        const int hs = e.hstep[b], hl = e.hlen[b];
+        const uint32_t *path = e.hpath + (size_t)b * e.Lmax;
+        if (hs >= hl - 1) {
+            bool replan = false;
+            if (e.human_mode == 0) {
+                hp_new = path[0];
+            } else if (e.human_mode == 1) {
+                const uint32_t ent = e.hentr[b];
+                auto ok = [&](int r, int c) -> bool { return !obstacle_at(e, bits, r, c) && pack(r, c) != ent; };
+                int r, c;
+                if (!group_free_cell(e, env_id, P_HGOAL, 0, clock, ok, r, c)) {
+                    if (i == 0) atomicAdd(&e.counters[C_FREECELL], 1u);
+                    r = prow(hp); c = pcol(hp);
+                }
+                if (i == 0) { e.hgoal[b] = pack(r, c); e.hreplans[b] += 1u; }
+                replan = true;
+                hp_new = hp;      // the new path starts at the current position
+            } else {
+                const int idx = e.hseq_idx[b] + 1;
+                const int len = e.hseq_len[b];
+                if (idx >= len) {
+                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];
+                    hp_new = path[0];
+                } else {
+                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + idx];
+                    replan = true;
+                    hp_new = hp;
+                }
+                if (i == 0) e.hseq_idx[b] = idx;
+            }
+            if (i == 0) {
+                e.hstep[b] = 0;
+                if (replan) {
+                    const uint32_t slot = atomicAdd(&e.counters[C_REPLAN_COUNT + parity], 1u);
+                    e.replan_list[(size_t)parity * e.B + slot] = (uint32_t)b;
+                }
+            }
+        } else {
+            hp_new = path[hs + 1];
+            if (i == 0) e.hstep[b] = hs + 1;
+        }
+        if (i == 0) { e.hpos[b] = hp_new; e.clock[b] = clock + 1u; }
+    }
+
+    // ---- outputs ------------------------------------------------------------
+    if (act) {
+        const int d0 = prow(hp_new) - nr, d1 = pcol(hp_new) - nc;
+        const float cv = (d0 * d0 + d1 * d1 <= e.constr_d2) ? 1.f : 0.f;   // (:632-633)
+        if (out.actions_fixed) out.actions_fixed[ai] = fixed;
+        if (out.goals_reached) out.goals_reached[ai] = reached ? 1.f : 0.f;
+        if (out.constraints) out.constraints[ai] = cv;
+        if (out.reward_total) out.reward_total[ai] = reached ? rw + e.goal_reward : rw;   // runner.py:89-91
+    }
+}
+
+// Uniform random policy: counter (env, P_ACT | agent << 8, clock, 0).
+__global__ __launch_bounds__(256) void random_actions_kernel(DevEnv e, int32_t *__restrict__ actions) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= e.B * e.N) return;
+    const int b = t / e.N, i = t - b * e.N;
+    const u32x4 o = philox(e.env_offset + (uint32_t)b, P_ACT | ((uint32_t)i << 8), e.clock[b], 0u, e.seed);
+    actions[t] = (int32_t)__umulhi(o.x, (uint32_t)NA);
+}
+
+void launch_step(const DevEnv &e, const int32_t *actions, const StepOut &out, uint32_t flags, int parity,
+                 hipStream_t s) {
+    const long threads = (long)e.B * e.G;
+    const int grid = (int)((threads + 255) / 256);
+    hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, s, e, actions, out, flags, parity);
+}
+
+void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s) {
+    const int n = e.B * e.N;
+    hipLaunchKernelGGL(random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, s, e, actions);
+}
+
+}  // namespace mapf

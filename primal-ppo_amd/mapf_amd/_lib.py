@@ -1,0 +1,79 @@
+"""ctypes binding of libmapf.so (include/mapf.h).
+
+This is the binding a maintainer of the reference would add;
+every entry point declared in include/mapf.h is bound here with its exact
+C signature.  Loading fails loudly when the library is missing.
+"""
+import ctypes
+import os
+
+from .config import MapfConfig
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MAPF_LIB", os.path.join(PKG, "lib", "libmapf.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+U32 = ctypes.c_uint32
+
+
+class ResetSpec(ctypes.Structure):
+    _fields_ = [("mode", I32), ("reserved", I32), ("maps", P), ("seq", P), ("seq_len", P),
+                ("human_start", P), ("human_goal", P), ("human_seq", P), ("human_seq_len", P),
+                ("seed", ctypes.c_uint64)]
+
+
+class StepOut(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("status", "reward", "shadow_goals", "cost", "train_valid", "actions_fixed",
+                                 "goals_reached", "constraints", "reward_total")]
+
+
+class State(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("pos", "goal", "last_action", "seq_cursor", "human", "human_path", "clock")]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "mapf_last_error": (ctypes.c_char_p, []),
+    "mapf_abi_version": (ctypes.c_int, []),
+    "mapf_create": (ctypes.c_int, [ctypes.POINTER(MapfConfig), ctypes.c_int, ctypes.POINTER(P)]),
+    "mapf_destroy": (ctypes.c_int, [P]),
+    "mapf_path_capacity": (ctypes.c_int, [P]),
+    "mapf_reset": (ctypes.c_int, [P, ctypes.POINTER(ResetSpec), P]),
+    "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
+    "mapf_observe": (ctypes.c_int, [P, P, P, P]),
+    "mapf_random_actions": (ctypes.c_int, [P, P, P]),
+    "mapf_bfs": (ctypes.c_int, [P, P, P]),
+    "mapf_get_counters": (ctypes.c_int, [P, P, P]),
+    "mapf_get_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
+    "mapf_set_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
+    "mapf_gae": (ctypes.c_int, [P, P, P, P, P, I32, I32, ctypes.c_double, ctypes.c_double, P]),
+    "mapf_normalize_advantages": (ctypes.c_int, [P, P, P, P, P, P, I32, ctypes.c_double, I32, P]),
+    "mapf_sample_actions": (ctypes.c_int, [P, I32, P, P, I32, ctypes.c_uint64, U32, P]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libmapf.so not found at {LIB_PATH}: build it with `python -c 'import "
+                               f"__graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.mapf_abi_version() != 1:
+            raise RuntimeError("libmapf.so ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().mapf_last_error()
+        raise RuntimeError(f"libmapf error {rc}: {msg.decode() if msg else ''}")
+    return rc

@@ -1,0 +1,225 @@
+"""BatchedMapfGym: B lockstep MAPF environments resident on one MI355X.
+
+Python face of libmapf.so (include/mapf.h).  Every call is asynchronous on
+the current torch HIP stream; inputs and outputs are torch tensors in HBM.
+Reference API it batches: mapf_gym.MapfGym / FixedMapfGym (mapf_gym.py:163-669).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import MapfConfig, make_config
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class BatchedMapfGym:
+    """B environments x N agents on one GPU (one handle per process/GPU)."""
+
+    def __init__(self, cfg: MapfConfig = None, device=None, **kw):
+        if cfg is None:
+            cfg = make_config(**kw)
+        if not torch.cuda.is_available():
+            raise RuntimeError("BatchedMapfGym needs a GPU (MI355X); there is no CPU fallback")
+        self.cfg = cfg
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+        self.B, self.N, self.H, self.W = cfg.num_envs, cfg.num_agents, cfg.height, cfg.width
+        self.F, self.C = cfg.fov, cfg.num_channel
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().mapf_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
+        self.h = h
+        self.path_capacity = _lib.lib().mapf_path_capacity(self.h)
+        dev = self.device
+        B, N = self.B, self.N
+        self.out = dict(
+            status=torch.zeros(B, N, dtype=torch.int8, device=dev),
+            reward=torch.zeros(B, N, dtype=torch.float32, device=dev),
+            shadow_goals=torch.zeros(B, dtype=torch.int32, device=dev),
+            cost=torch.zeros(B, N, dtype=torch.float32, device=dev),
+            train_valid=torch.zeros(B, N, 5, dtype=torch.float32, device=dev),
+            actions_fixed=torch.zeros(B, N, dtype=torch.int32, device=dev),
+            goals_reached=torch.zeros(B, N, dtype=torch.float32, device=dev),
+            constraints=torch.zeros(B, N, dtype=torch.float32, device=dev),
+            reward_total=torch.zeros(B, N, dtype=torch.float32, device=dev))
+        self._stepout = self._make_stepout(self.out)
+        self.obs = torch.zeros(B, N, self.C, self.F, self.F, dtype=torch.float32, device=dev)
+        self.vec = torch.zeros(B, N, 4, dtype=torch.float32, device=dev)
+        self.actions = torch.zeros(B, N, dtype=torch.int32, device=dev)
+
+    @staticmethod
+    def _make_stepout(out):
+        so = _lib.StepOut()
+        for name, _ in _lib.StepOut._fields_:
+            t = out.get(name)
+            setattr(so, name, t.data_ptr() if t is not None else None)
+        return so
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().mapf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- reset
+    def _maps_array(self, maps):
+        maps = np.ascontiguousarray(maps, dtype=np.int8)
+        if self.cfg.shared_map:
+            maps = maps.reshape(1, self.H, self.W)
+        else:
+            maps = maps.reshape(self.B, self.H, self.W)
+        return maps
+
+    def reset_fixed(self, maps, seqs, human_start=None, human_goal=None, human_seq=None):
+        """FixedMapfGym (mapf_gym.py:648-669) for every env.
+
+        seqs: [B][N] lists of (row, col) -- start then goals (util.Sequence).
+        human_start/goal: [B, 2] (LoopingHuman) or human_seq: [B] lists (FixedPathHuman)."""
+        m = self._maps_array(maps)
+        S = self.cfg.max_seq
+        seq = np.zeros((self.B, self.N, S, 2), np.int32)
+        sl = np.zeros((self.B, self.N), np.int32)
+        for b in range(self.B):
+            for i in range(self.N):
+                s = np.asarray(seqs[b][i], np.int32).reshape(-1, 2)
+                if len(s) > S:
+                    raise ValueError(f"sequence of {len(s)} cells exceeds max_seq={S}")
+                seq[b, i, :len(s)] = s
+                sl[b, i] = len(s)
+        spec = _lib.ResetSpec()
+        spec.mode = 0
+        keep = [m, seq, sl]
+        spec.maps = m.ctypes.data
+        spec.seq = seq.ctypes.data
+        spec.seq_len = sl.ctypes.data
+        if human_seq is not None:
+            HS = self.cfg.max_human_seq
+            hs = np.zeros((self.B, HS, 2), np.int32)
+            hl = np.zeros(self.B, np.int32)
+            for b in range(self.B):
+                q = np.asarray(human_seq[b], np.int32).reshape(-1, 2)
+                hs[b, :len(q)] = q
+                hl[b] = len(q)
+            keep += [hs, hl]
+            spec.human_seq = hs.ctypes.data
+            spec.human_seq_len = hl.ctypes.data
+        else:
+            a = np.ascontiguousarray(np.asarray(human_start, np.int32).reshape(self.B, 2))
+            g = np.ascontiguousarray(np.asarray(human_goal, np.int32).reshape(self.B, 2))
+            keep += [a, g]
+            spec.human_start = a.ctypes.data
+            spec.human_goal = g.ctypes.data
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().mapf_reset(self.h, ctypes.byref(spec), _stream(self.device)))
+        del keep
+
+    def reset_seeded(self, maps, seed=0):
+        """MapfGym (mapf_gym.py:164-184): human entrance/goal and agent starts/goals drawn on device."""
+        m = self._maps_array(maps)
+        spec = _lib.ResetSpec()
+        spec.mode = 1
+        spec.maps = m.ctypes.data
+        spec.seed = seed
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().mapf_reset(self.h, ctypes.byref(spec), _stream(self.device)))
+
+    # ----------------------------------------------------------------- step
+    def step(self, actions=None, commit=True):
+        """One lockstep step (runner.py:64-100 order).  actions: int32 [B, N] on device.
+        Returns the dict of output tensors (reused between calls)."""
+        if actions is None:
+            actions = self.actions
+        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
+        _lib.check(_lib.lib().mapf_step(self.h, _ptr(actions), ctypes.byref(self._stepout),
+                                        1 if commit else 0, _stream(self.device)))
+        return self.out
+
+    def observe(self, obs=None, vec=None):
+        """getAllObservations for all envs: obs [B, N, C, F, F], vec [B, N, 4] (float32)."""
+        obs = self.obs if obs is None else obs
+        vec = self.vec if vec is None else vec
+        assert obs.is_contiguous() and vec.is_contiguous()
+        assert obs.numel() == self.B * self.N * self.C * self.F * self.F and vec.numel() == self.B * self.N * 4
+        _lib.check(_lib.lib().mapf_observe(self.h, _ptr(obs), _ptr(vec), _stream(self.device)))
+        return obs, vec
+
+    def random_actions(self, out=None):
+        out = self.actions if out is None else out
+        _lib.check(_lib.lib().mapf_random_actions(self.h, _ptr(out), _stream(self.device)))
+        return out
+
+    def bfs(self):
+        d = torch.empty(self.B, self.N, self.H, self.W, dtype=torch.int16, device=self.device)
+        _lib.check(_lib.lib().mapf_bfs(self.h, _ptr(d), _stream(self.device)))
+        return d
+
+    def counters(self):
+        c = np.zeros(16, np.uint32)
+        _lib.check(_lib.lib().mapf_get_counters(self.h, ctypes.c_void_p(c.ctypes.data), _stream(self.device)))
+        return c
+
+    def get_state(self):
+        B, N, L = self.B, self.N, self.path_capacity
+        st = dict(pos=np.zeros((B, N, 2), np.int32), goal=np.zeros((B, N, 2), np.int32),
+                  last_action=np.zeros((B, N), np.int32), seq_cursor=np.zeros((B, N), np.int32),
+                  human=np.zeros((B, 10), np.int32), human_path=np.zeros((B, L, 2), np.int32),
+                  clock=np.zeros(B, np.uint32))
+        s = _lib.State(*[st[n].ctypes.data for n, _ in _lib.State._fields_])
+        _lib.check(_lib.lib().mapf_get_state(self.h, ctypes.byref(s), _stream(self.device)))
+        return st
+
+    def set_state(self, **kw):
+        keep = {}
+        s = _lib.State()
+        for n, _ in _lib.State._fields_:
+            if n in kw and kw[n] is not None:
+                dt = np.uint32 if n == "clock" else np.int32
+                a = np.ascontiguousarray(kw[n], dtype=dt)
+                keep[n] = a
+                setattr(s, n, a.ctypes.data)
+        _lib.check(_lib.lib().mapf_set_state(self.h, ctypes.byref(s), _stream(self.device)))
+
+
+def gae(rewards, values, last_values, gamma=0.95, lam=0.95):
+    """runner.py:117-149 on device: rewards/values [T, ...] float32, last_values [...]."""
+    T = rewards.shape[0]
+    M = rewards[0].numel()
+    adv = torch.empty_like(rewards)
+    ret = torch.empty_like(rewards)
+    _lib.check(_lib.lib().mapf_gae(_ptr(rewards), _ptr(values), _ptr(last_values), _ptr(adv), _ptr(ret), T, M,
+                                   gamma, lam, _stream(rewards.device)))
+    return adv, ret
+
+
+def normalize_advantages(returns, values, cost_returns, cost_values, lagrange=0.0, mix=False):
+    """model.py:106-113 on device; returns (advantage, cost_advantage)."""
+    adv = torch.empty_like(returns)
+    cadv = torch.empty_like(returns)
+    _lib.check(_lib.lib().mapf_normalize_advantages(
+        _ptr(returns), _ptr(values), _ptr(cost_returns), _ptr(cost_values), _ptr(adv), _ptr(cadv),
+        returns.numel(), float(lagrange), int(mix), _stream(returns.device)))
+    return adv, cadv
+
+
+def sample_actions(ps, seed, step, out32=None, out64=None):
+    """model.py:38-40 on device: ps [..., 5] float32 -> actions."""
+    ps2 = ps.reshape(-1, ps.shape[-1])
+    assert ps2.dtype == torch.float32 and ps2.stride(1) == 1
+    M = ps2.shape[0]
+    _lib.check(_lib.lib().mapf_sample_actions(_ptr(ps2), ps2.stride(0), _ptr(out32), _ptr(out64), M, seed, step,
+                                              _stream(ps.device)))
+    return out32 if out32 is not None else out64

@@ -1,0 +1,356 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+vectors and the CPU oracle.  Bit-exact for every integer output, every
+observation bit and every float the reference computes (rewards, costs,
+vectors are exact restatements); GAE bit-exact; advantage normalisation
+within 1e-5 of torch fp32 (model.py:106-113 computes it in torch).
+"""
+import collections
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import G1_NAMES, Fuzz, load, unpack_obs
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+
+
+def mk_env(**kw):
+    from mapf_amd.config import make_config
+    from mapf_amd.env import BatchedMapfGym
+    B = kw.pop("B")
+    H, W = kw.pop("H"), kw.pop("W")
+    return BatchedMapfGym(make_config(B, H, W, **kw))
+
+
+def host(out):
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def assert_no_errors(env, allow=()):
+    c = env.counters()
+    for k in range(8):
+        if k not in allow:
+            assert c[k] == 0, f"device counter {k} = {c[k]}"
+
+
+# --------------------------------------------------------------------------- g1
+@pytest.mark.parametrize("name", G1_NAMES)
+def test_g1_episode_on_device(name):
+    z = load(name)
+    n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
+    world = z["map"]
+    H, W = world.shape
+    hmode = int(z["human_mode"])
+    B = 37   # replicas: partial last workgroup, several envs per wave
+    env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=nch, use_da=int(z["use_da"]),
+                 use_hp=int(z["use_hp"]), human_mode=hmode, goal_mode="sequence", fix_choice=0,
+                 max_seq=z["seq"].shape[1], max_human_seq=max(2, len(z["hseq"])))
+    seqs = [z["seq"][i, :z["seq_len"][i]] for i in range(n)]
+    if hmode == 2:
+        env.reset_fixed(world, [seqs] * B, human_seq=[z["hseq"]] * B)
+    else:
+        env.reset_fixed(world, [seqs] * B, [z["hstart"]] * B, [z["hgoal"]] * B)
+    st = env.get_state()
+    for b in (0, B - 1):
+        np.testing.assert_array_equal(st["pos"][b], z["pos0"])
+        L = st["human"][b, 7]
+        np.testing.assert_array_equal(st["human_path"][b, :L], z["hpath0"])
+    np.testing.assert_array_equal(env.bfs().cpu().numpy(), np.broadcast_to(z["bfs0"], (B,) + z["bfs0"].shape))
+    obs, vec = env.observe()
+    ref = unpack_obs(z["obs0"], (n, nch, fov, fov))
+    o = obs.cpu().numpy()
+    for b in range(B):
+        np.testing.assert_array_equal(o[b], ref, err_msg=f"obs0 env {b}")
+        np.testing.assert_array_equal(vec.cpu().numpy()[b], z["vec0"][0])
+    acts = torch.zeros(B, n, dtype=torch.int32, device="cuda")
+    for t in range(int(z["steps"])):
+        acts.copy_(torch.from_numpy(np.tile(z["actions"][t].astype(np.int32), (B, 1))))
+        out = host(env.step(acts))
+        for k, key in [("status", "status"), ("reward", "reward"), ("cost", "cost"), ("train_valid", "valid"),
+                       ("actions_fixed", "fixed"), ("goals_reached", "goals"), ("constraints", "constr")]:
+            ref = np.broadcast_to(z[key][t].astype(out[k].dtype), out[k].shape)
+            np.testing.assert_array_equal(out[k], ref, err_msg=f"{name} t={t} {k}")
+        assert (out["shadow_goals"] == int(z["shadow"][t])).all()
+        rt = z["reward"][t] + np.where(z["goals"][t] == 1, np.float32(1.5), np.float32(0)).astype(np.float32)
+        np.testing.assert_array_equal(out["reward_total"][0], rt.astype(np.float32))
+        obs, vec = env.observe()
+        o = obs.cpu().numpy()
+        ref = unpack_obs(z["obs"][t], (n, nch, fov, fov))
+        for b in (0, B // 2, B - 1):
+            np.testing.assert_array_equal(o[b], ref, err_msg=f"{name} t={t} obs env {b}")
+            np.testing.assert_array_equal(vec.cpu().numpy()[b], z["vec"][t])
+        if t % 25 == 0 or t == int(z["steps"]) - 1:
+            st = env.get_state()
+            np.testing.assert_array_equal(st["pos"][B - 1], z["pos"][t])
+            np.testing.assert_array_equal(st["goal"][B - 1], z["goal"][t])
+            np.testing.assert_array_equal(st["human"][0, 0:2], z["hpos"][t])
+            np.testing.assert_array_equal(st["human"][0, 2:4], z["hnext"][t])
+    np.testing.assert_array_equal(env.bfs().cpu().numpy()[B - 1], z["bfs_final"])
+    assert_no_errors(env)
+
+
+# --------------------------------------------------------------------------- g2
+def test_g2_fuzz_on_device():
+    fz = Fuzz()
+    groups = collections.defaultdict(list)
+    for k in range(fz.count):
+        c = fz.case(k)
+        groups[(int(c["H"]), int(c["W"]), int(c["n"]), int(c["fov"]), int(c["use_da"]), int(c["use_hp"]))].append(c)
+    bad = []
+    for (H, W, n, fov, da, hp), cases in groups.items():
+        B = len(cases)
+        env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=6, use_da=da, use_hp=hp,
+                     human_mode="looping", goal_mode="sequence", fix_choice=0, max_seq=3, shared_map=False)
+        maps = np.stack([c["map"].reshape(H, W) for c in cases])
+        hps = [c["hpath"] for c in cases]
+        env.reset_fixed(maps, [list(c["seq"]) for c in cases], [p[0] for p in hps], [p[len(p) // 2] for p in hps])
+        st = env.get_state()
+        human = st["human"].copy()
+        for b, c in enumerate(cases):
+            hs = int(c["hstep0"])
+            human[b, 6] = hs
+            human[b, 0:2] = hps[b][hs]
+        prev = np.stack([c["prev"] if c["prev"].size == n else np.full(n, -1) for c in cases]).astype(np.int32)
+        env.set_state(human=human, last_action=prev)
+        obs0, vec0 = [x.cpu().numpy().copy() for x in env.observe()]
+        acts = torch.from_numpy(np.stack([c["actions"] for c in cases]).astype(np.int32)).cuda()
+        out = host(env.step(acts))
+        obs1, vec1 = [x.cpu().numpy().copy() for x in env.observe()]
+        st = env.get_state()
+        for b, c in enumerate(cases):
+            if not np.array_equal(obs0[b], unpack_obs(c["obs0"], (n, 6, fov, fov))) or not np.array_equal(vec0[b], c["vec0"]):
+                bad.append(("obs0", H, W, n, b))
+            for k, key in [("status", "status"), ("reward", "reward"), ("cost", "cost"), ("train_valid", "valid"),
+                           ("actions_fixed", "fixed"), ("goals_reached", "goals"), ("constraints", "constr")]:
+                if not np.array_equal(out[k][b], c[key].astype(out[k].dtype)):
+                    bad.append((k, H, W, n, b))
+            if out["shadow_goals"][b] != int(c["shadow"]):
+                bad.append(("shadow", H, W, n, b))
+            if not np.array_equal(st["pos"][b], c["pos1"]) or not np.array_equal(st["goal"][b], c["goal1"]):
+                bad.append(("pos1", H, W, n, b))
+            if not np.array_equal(obs1[b], unpack_obs(c["obs1"], (n, 6, fov, fov))) or not np.array_equal(vec1[b], c["vec1"]):
+                bad.append(("obs1", H, W, n, b))
+        env.close()
+    assert not bad, f"{len(bad)} mismatches: {bad[:20]}"
+
+
+# --------------------------------------------------------------------------- g3
+def test_g3_astar_paths_and_bfs_on_device():
+    z = load("g3_search")
+    offs = np.concatenate([[0], np.cumsum(z["path_len"])])
+    boffs = [0]
+    for k in range(len(z["mi"])):
+        boffs.append(boffs[-1] + z[f"map{int(z['mi'][k])}"].size)
+    for mi in range(int(z["nmaps"])):
+        world = z[f"map{mi}"]
+        H, W = world.shape
+        ks = [k for k in range(len(z["mi"])) if int(z["mi"][k]) == mi and not np.array_equal(z["s"][k], z["g"][k])]
+        if not ks:
+            continue
+        free = np.argwhere(world == 0)
+        B = len(ks)
+        env = mk_env(B=B, H=H, W=W, num_agents=1, fov=3, num_channel=5, human_mode="looping", goal_mode="sequence",
+                     fix_choice=0, max_seq=2)
+        seqs = [[[free[0], z["g"][k]]] for k in ks]
+        env.reset_fixed(world, seqs, [z["s"][k] for k in ks], [z["g"][k] for k in ks])
+        st = env.get_state()
+        bfs = env.bfs().cpu().numpy()
+        unreachable = 0
+        for b, k in enumerate(ks):
+            ref_bfs = z["bfs"][boffs[k]:boffs[k + 1]].reshape(H, W)
+            np.testing.assert_array_equal(bfs[b, 0], ref_bfs, err_msg=f"bfs map {mi} case {k}")
+            if not z["ok"][k]:
+                unreachable += 1
+                assert st["human"][b, 7] == 1
+                continue
+            path = z["path"][offs[k]:offs[k + 1]]            # goal -> start (construct_path_from_dict)
+            want = np.concatenate([path[::-1], path[1:]])     # Human.getAstarPath (mapf_gym.py:33-37)
+            L = st["human"][b, 7]
+            np.testing.assert_array_equal(st["human_path"][b, :L], want, err_msg=f"astar map {mi} case {k}")
+        assert env.counters()[4] == unreachable
+
+
+# ------------------------------------------------------------ random mode vs oracle
+RANDOM_CASES = {
+    "c2_20x20_n8_f11": dict(B=64, H=20, W=20, n=8, fov=11, nch=6, steps=300, map="wh"),
+    "c1_10x10_n4_f11": dict(B=33, H=10, W=10, n=4, fov=11, nch=6, steps=300, map="wh"),
+    "dense_12x12_n16_f9_dahp": dict(B=16, H=12, W=12, n=16, fov=9, nch=6, steps=200, map="wh", da=1, hp=1),
+    "c4_40x40_n16_f9_looping": dict(B=16, H=40, W=40, n=16, fov=9, nch=6, steps=100, map="wh", human="looping"),
+    "c5_80x80_n64_f11_bfsch": dict(B=3, H=80, W=80, n=64, fov=11, nch=7, steps=40, map="rand"),
+}
+
+
+def build_maps(case, B, rng):
+    from mapf_amd.maps import generate_warehouse, keep_largest_component, random_map
+    if case["map"] == "wh":
+        return generate_warehouse(case["H"], case["W"]), True
+    return np.stack([keep_largest_component(random_map(rng, case["H"], case["W"], 0.3)) for _ in range(B)]), False
+
+
+@pytest.mark.parametrize("name", list(RANDOM_CASES))
+def test_random_mode_matches_oracle(name):
+    case = RANDOM_CASES[name]
+    B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
+    rng = np.random.default_rng(5)
+    maps, shared = build_maps(case, B, rng)
+    human = case.get("human", "random")
+    seed = 0x5EED0000 + len(name)
+    env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=nch, use_da=case.get("da", 0),
+                 use_hp=case.get("hp", 0), human_mode=human, goal_mode="random", fix_choice=1, shared_map=shared,
+                 seed=seed, env_offset=7)
+    env.reset_seeded(maps)
+    hm = {"random": 1, "looping": 0}[human]
+    cfg = O.make_config(H, W, n, fov, nch, use_da=case.get("da", 0), use_hp=case.get("hp", 0), human_mode=hm,
+                        goal_mode=1, fix_choice=1, seed=seed, env_offset=7)
+    oracles = []
+    for b in range(B):
+        oe = O.OracleEnv(cfg, env_id=7 + b)
+        oe.reset_random(maps if shared else maps[b])
+        oracles.append(oe)
+    st = env.get_state()
+    for b in range(B):
+        p, g = oracles[b].agents()
+        np.testing.assert_array_equal(st["pos"][b], p)
+        np.testing.assert_array_equal(st["goal"][b], g)
+        hp = oracles[b].human_path()
+        np.testing.assert_array_equal(st["human_path"][b, :len(hp)], hp)
+    checked_obs = 0
+    for t in range(case["steps"]):
+        acts = env.random_actions()
+        a_host = acts.cpu().numpy()
+        out = host(env.step(acts))
+        obs, vec = env.observe()
+        obs, vec = obs.cpu().numpy(), vec.cpu().numpy()
+        for b in range(B):
+            oe = oracles[b]
+            np.testing.assert_array_equal(a_host[b], oe.random_actions(), err_msg=f"{name} actions t={t} b={b}")
+            o = oe.step(a_host[b])
+            for k, key in [("status", "status"), ("reward", "reward"), ("cost", "cost"), ("train_valid", "valid"),
+                           ("actions_fixed", "fixed"), ("goals_reached", "goals"), ("constraints", "constr")]:
+                np.testing.assert_array_equal(out[k][b], o[key].astype(out[k].dtype), err_msg=f"{name} t={t} b={b} {k}")
+            assert out["shadow_goals"][b] == o["shadow"]
+            if b % 4 == t % 4:
+                oo, ov = oe.observe()
+                np.testing.assert_array_equal(obs[b], oo, err_msg=f"{name} t={t} b={b} obs")
+                np.testing.assert_array_equal(vec[b], ov, err_msg=f"{name} t={t} b={b} vec")
+                checked_obs += 1
+        if t % 20 == 19:
+            st = env.get_state()
+            bfs = env.bfs().cpu().numpy()
+            for b in range(B):
+                p, g = oracles[b].agents()
+                np.testing.assert_array_equal(st["pos"][b], p)
+                np.testing.assert_array_equal(st["goal"][b], g)
+                h = oracles[b].human()
+                np.testing.assert_array_equal(st["human"][b, 0:2], h["pos"])
+                np.testing.assert_array_equal(st["human"][b, 4:6], h["goal"])
+                np.testing.assert_array_equal(bfs[b], oracles[b].bfs())
+    assert checked_obs > 0
+    assert_no_errors(env)
+    for oe in oracles:
+        assert oe.errors() == 0
+
+
+# ---------------------------------------------------------------- full-size c2
+def test_c2_full_size_invariants_and_sampled_oracle():
+    """BASELINE config c2 (4096 envs x 8 agents, 20x20, FOV 11): size-independent
+    invariants on every env + bit-exact oracle replays of sampled envs."""
+    from mapf_amd.maps import generate_warehouse
+    B, n, H, W, fov = 4096, 8, 20, 20, 11
+    world = generate_warehouse(H, W)
+    env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=6, human_mode="random", goal_mode="random",
+                 fix_choice=1, seed=1234)
+    env.reset_seeded(world)
+    cfg = O.make_config(H, W, n, fov, 6, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
+    sample = [0, 1, 63, 64, 2047, 4095]
+    oracles = {b: O.OracleEnv(cfg, env_id=b) for b in sample}
+    for b, oe in oracles.items():
+        oe.reset_random(world)
+    free = world == 0
+    for t in range(60):
+        acts = env.random_actions()
+        a_host = acts.cpu().numpy()
+        out = host(env.step(acts))
+        obs, vec = env.observe()
+        st = env.get_state()
+        pos = st["pos"]
+        # invariants: agents on free cells, pairwise distinct, statuses legal, fixed moves legal
+        assert free[pos[..., 0], pos[..., 1]].all()
+        flat = pos[..., 0] * W + pos[..., 1]
+        srt = np.sort(flat, axis=1)
+        assert (np.diff(srt, axis=1) > 0).all()
+        assert np.isin(out["status"], [1, -1, -2, -3, -4]).all()
+        if t % 10 == 0:
+            o = obs.cpu().numpy()
+            c = fov // 2
+            assert (o[:, :, 0, c, c] == 1).all()                  # self marked in ch0
+            assert ((o == 0) | (o == 1)).all()
+        for b, oe in oracles.items():
+            r = oe.step(a_host[b])
+            np.testing.assert_array_equal(out["status"][b], r["status"])
+            np.testing.assert_array_equal(out["actions_fixed"][b], r["fixed"])
+            np.testing.assert_array_equal(out["train_valid"][b], r["valid"])
+            oo, ov = oe.observe()
+            np.testing.assert_array_equal(obs[b].cpu().numpy(), oo)
+            np.testing.assert_array_equal(vec[b].cpu().numpy(), ov)
+    assert_no_errors(env)
+
+
+# --------------------------------------------------------------- GAE / normalise
+def test_gae_bit_exact_vs_golden():
+    from mapf_amd.env import gae
+    z = load("g4_gae")
+    for r, v, lv, want in [("rewards", "values", "last_v", "returns"),
+                           ("cost_rewards", "cost_values", "last_cv", "cost_returns")]:
+        adv, ret = gae(torch.from_numpy(z[r]).cuda(), torch.from_numpy(z[v]).cuda(), torch.from_numpy(z[lv]).cuda(),
+                       float(z["gamma"]), float(z["lam"]))
+        np.testing.assert_array_equal(ret.cpu().numpy(), z[want])
+
+
+def test_gae_large_matches_oracle():
+    from mapf_amd.env import gae
+    g = np.random.default_rng(1)
+    T, M = 256, 4096 * 8
+    r = g.normal(size=(T, M)).astype(np.float32)
+    v = g.normal(size=(T, M)).astype(np.float32)
+    lv = g.normal(size=M).astype(np.float32)
+    adv, ret = gae(torch.from_numpy(r).cuda(), torch.from_numpy(v).cuda(), torch.from_numpy(lv).cuda())
+    cols = g.choice(M, 64, replace=False)
+    oa, orr = O.gae(r[:, cols], v[:, cols], lv[cols])
+    np.testing.assert_array_equal(adv.cpu().numpy()[:, cols], oa)
+    np.testing.assert_array_equal(ret.cpu().numpy()[:, cols], orr)
+
+
+def test_normalize_advantages_vs_torch():
+    from mapf_amd.env import normalize_advantages
+    z = load("g4_gae")
+    x = torch.from_numpy(z["norm_x"]).cuda()
+    y = torch.from_numpy(z["norm_y"]).cuda()
+    zero = torch.zeros_like(x)
+    adv, cadv = normalize_advantages(x, zero, y, zero, lagrange=float(z["norm_lam"]), mix=True)
+    np.testing.assert_allclose(cadv.cpu().numpy(), z["norm_cadv"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(adv.cpu().numpy(), z["norm_mixed"], rtol=0, atol=1e-5)
+    adv, _ = normalize_advantages(x, zero, y, zero, mix=False)
+    np.testing.assert_allclose(adv.cpu().numpy(), z["norm_adv"], rtol=0, atol=1e-5)
+
+
+def test_sample_actions_distribution():
+    from mapf_amd.env import sample_actions
+    M = 200000
+    p = torch.tensor([0.1, 0.2, 0.3, 0.15, 0.25]).cuda().expand(M, 5).contiguous()
+    a = torch.zeros(M, dtype=torch.int32, device="cuda")
+    sample_actions(p, 99, 3, out32=a)
+    freq = np.bincount(a.cpu().numpy(), minlength=5) / M
+    np.testing.assert_allclose(freq, [0.1, 0.2, 0.3, 0.15, 0.25], atol=5e-3)
+    b = torch.zeros(M, dtype=torch.int64, device="cuda")
+    sample_actions(p, 99, 3, out64=b)
+    assert torch.equal(a.long(), b)

@@ -1,0 +1,39 @@
+#!/bin/bash
+# GPU validation pass, run on the gpurun box from the repo root:
+#   smoke -> GPU parity tests -> bench -> rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a fault, abort, segfault or time
+# limit ends the script (no further GPU work in this call).  A plain test
+# failure (pytest rc 1) still lets the bench and the profile run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export PYTHONUNBUFFERED=1
+
+stop_if_fatal() {   # $1 = rc, $2 = step name
+  case "$1" in
+    0|1) return 0 ;;
+    *) echo "FATAL: $2 exited with $1 -- stopping GPU work"; exit "$1" ;;
+  esac
+}
+
+STEPS="${STEPS:-smoke pytest bench prof}"
+for s in $STEPS; do
+  case "$s" in
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; stop_if_fatal $rc smoke ;;
+    pytest)
+      timeout -k 10 1000 python3 -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"; stop_if_fatal $rc pytest ;;
+    bench)
+      timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; stop_if_fatal $rc bench ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 20 --no-cpu) > "$OUT/prof.log" 2>&1
+      rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; stop_if_fatal $rc prof
+      find "$OUT/prof" -name "*stats*" | head ;;
+  esac
+done
