@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--channels", type=int, default=6)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=16, help="steps per captured hipGraph (0 = direct launches)")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,28 +93,36 @@ def main():
     obs, vec, acts = env.obs, env.vec, env.actions
 
     def one_step():
-        env.random_actions(acts)
-        env.step(acts)
+        env.step_random(acts)        # random policy's actions drawn in the step kernel
         env.observe(obs, vec)
 
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
 
+    # The K timed steps are replays of a hipGraph holding G consecutive steps
+    # (every kernel of every step runs; the graph only removes host launch cost).
+    G = args.graph_steps
     K = args.steps
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    graph = None
+    if G > 0:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(G):
+                one_step()
+        torch.cuda.synchronize()
+        graph.replay()               # these G steps are warm-up too
+        torch.cuda.synchronize()
+    n_replay, n_direct = (K // G, K % G) if G > 0 else (0, K)
+
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        e0, e1, e2 = ev[k]
-        e0.record()
-        env.random_actions(acts)
-        env.step(acts)
-        e1.record()
-        env.observe(obs, vec)
-        e2.record()
+    for _ in range(n_replay):
+        graph.replay()
+    for _ in range(n_direct):
+        one_step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -122,8 +131,21 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(K)]))
-    obs_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(K)]))
+
+    # Per-kernel timing: HIP events around each launch on the launch stream,
+    # direct (non-graph) launches of the same steps.
+    KT = min(K, 400)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(KT)]
+    for k in range(KT):
+        e0, e1, e2 = ev[k]
+        e0.record()
+        env.step_random(acts)
+        e1.record()
+        env.observe(obs, vec)
+        e2.record()
+    torch.cuda.synchronize()
+    step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KT)]))
+    obs_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(KT)]))
     counters = env.counters()
 
     if rank == 0:
@@ -141,7 +163,8 @@ def main():
                        "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
                        "parallelism": f"env-shards x{world_size}"},
-            "breakdown_ms": {"actions+step+replan+bfs": round(step_ms, 4), "observe": round(obs_ms, 4)},
+            "breakdown_ms": {"step(actions+step+search)": round(step_ms, 4), "observe": round(obs_ms, 4),
+                             "timing": f"HIP events around {KT} direct launches; value from hipGraph replays of {G} steps"},
             "roofline": {"kernel": "observe_kernel", "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_agent": bpa, "agents_per_launch": B * N},

@@ -138,6 +138,11 @@ int mapf_reset(mapf_env *env, const mapf_reset_spec *spec, void *stream);
 /* One lockstep step for all B envs: actions are DEVICE int32 [B][N] in 0..4. */
 int mapf_step(mapf_env *env, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream);
 
+/* Env-only benchmark / random-policy rollouts: draw the uniform random policy's
+ * actions on the device (same Philox stream as mapf_random_actions), write them
+ * to actions_out (DEVICE int32 [B][N]) and step with them, in one launch. */
+int mapf_step_random(mapf_env *env, int32_t *actions_out, const mapf_step_out *out, uint32_t flags, void *stream);
+
 /* getAllObservations for all envs: obs DEVICE float [B][N][C][F][F], vec [B][N][4]. */
 int mapf_observe(mapf_env *env, float *obs, float *vec, void *stream);
 

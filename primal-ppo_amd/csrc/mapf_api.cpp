@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -104,6 +105,9 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.seed = c.seed;
     d.maxd2 = (d.H - 1) * (d.H - 1) + (d.W - 1) * (d.W - 1);
     d.obs_envs = 64 / d.N > 1 ? 64 / d.N : 1;
+    d.step_block = 256;
+    if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }
+    if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
     if (d.obs_envs > d.B) d.obs_envs = d.B;
 
     // fp64 lookup tables, computed exactly like the reference (numpy sqrt / python pow)
@@ -137,6 +141,8 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(d.counters, C_NUM);
     rc |= e->alloc(d.replan_list, 2 * (size_t)d.B);
     rc |= e->alloc(d.bfs_list, 2 * BN);
+    int16_t *binit = nullptr;
+    rc |= e->alloc(binit, nmaps * (size_t)((d.H * d.W + 7) & ~7));
     rc |= e->alloc(cl, cost_lut.size());
     rc |= e->alloc(dl, dist_lut.size());
     if (rc) {
@@ -145,6 +151,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
         return fail(MAPF_ENOMEM, m);
     }
     d.map_bits = map_bits;
+    d.bfs_init = binit;
     d.cost_lut = cl;
     d.dist_lut = dl;
     if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
@@ -195,6 +202,10 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
                 if (ob) mb[r * d.WW + (c >> 5)] |= 1u << (c & 31);
             }
     }
+    const int cells_pad = (H * W + 7) & ~7;
+    std::vector<int16_t> binit(nmaps * cells_pad, (int16_t)-1);
+    for (size_t m = 0; m < nmaps; ++m)
+        for (int k = 0; k < H * W; ++k) binit[m * cells_pad + k] = spec->maps[m * H * W + k] == 0 ? (int16_t)-2 : (int16_t)-1;
     auto free_at = [&](int b, int r, int c) {
         if (r < 0 || r >= H || c < 0 || c >= W) return false;
         const size_t m = d.shared_map ? 0 : (size_t)b;
@@ -255,6 +266,7 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     }
 
     HIPCHK(hipMemcpyAsync((void *)d.map_bits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync((void *)d.bfs_init, binit.data(), binit.size() * 2, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d.counters, 0, C_NUM * sizeof(uint32_t), s));
     if (spec->mode == 0) {
         HIPCHK(hipMemcpyAsync(d.seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice, s));
@@ -270,8 +282,7 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     } else {
         launch_reset_seeded(d, s);
     }
-    launch_replan(d, 0, true, s);
-    if (d.keep_bfs) launch_bfs(d, 0, true, s);
+    launch_search(d, 0, true, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // host staging buffers die at return
     e->parity = 1;
@@ -279,7 +290,7 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     return MAPF_OK;
 }
 
-int mapf_step(mapf_env *e, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream) {
+static int step_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream) {
     if (!e || !actions) return fail(MAPF_EINVAL, "null argument");
     if (!e->ready) return fail(MAPF_ESTATE, "mapf_step before mapf_reset");
     HIPCHK(hipSetDevice(e->device));
@@ -293,12 +304,19 @@ int mapf_step(mapf_env *e, const int32_t *actions, const mapf_step_out *out, uin
     const int parity = e->parity;
     launch_step(e->d, actions, o, flags, parity, s);
     if (flags & MAPF_STEP_COMMIT) {
-        if (e->d.human_mode != 0) launch_replan(e->d, parity, false, s);
-        if (e->d.keep_bfs) launch_bfs(e->d, parity, false, s);
+        if (e->d.human_mode != 0 || e->d.keep_bfs) launch_search(e->d, parity, false, s);
         e->parity ^= 1;
     }
     HIPCHK(hipGetLastError());
     return MAPF_OK;
+}
+
+int mapf_step(mapf_env *e, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream) {
+    return step_impl(e, const_cast<int32_t *>(actions), out, flags & MAPF_STEP_COMMIT, stream);
+}
+
+int mapf_step_random(mapf_env *e, int32_t *actions_out, const mapf_step_out *out, uint32_t flags, void *stream) {
+    return step_impl(e, actions_out, out, (flags & MAPF_STEP_COMMIT) | 2u, stream);
 }
 
 int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {

@@ -45,6 +45,7 @@ struct DevEnv {
     int maxd2;
     int constr_d2;            // largest d2 with (R - sqrt(d2)) / R >= 0.01 in fp64 (mapf_gym.py:633)
     int obs_envs;             // envs per observe workgroup
+    int step_block;           // threads per step workgroup (64..256)
     const uint32_t *map_bits;
     uint32_t *pos, *goal;
     int8_t *last_act;
@@ -60,6 +61,7 @@ struct DevEnv {
     uint32_t *counters, *replan_list, *bfs_list;
     const float *cost_lut;    // [R*R+1]: float32(max(R - sqrt(d2), 0) / R) (fp64 like the reference)
     const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
+    const int16_t *bfs_init;  // [nmaps][cells rounded up to 8]: makeBfsMap's initial copy (-1 obstacle, -2 free)
 };
 
 __host__ __device__ inline uint32_t pack(int r, int c) { return (uint32_t)(r & 0xFFFF) | ((uint32_t)c << 16); }

@@ -16,13 +16,12 @@ struct StepOut {          // device pointers (mapf_step_out)
     float *reward_total;
 };
 
-void launch_step(const DevEnv &e, const int32_t *actions, const StepOut &out, uint32_t flags, int parity,
-                 hipStream_t s);
+// flags: bit0 commit (jointStep), bit1 random policy (draw actions in-kernel into `actions`)
+void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s);
 void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s);
-// human path (re)planning for the envs in replan_list[parity] (or all envs when all = true)
-void launch_replan(const DevEnv &e, int parity, bool all, hipStream_t s);
-// agent BFS maps for bfs_list[parity] (or all agents when all = true)
-void launch_bfs(const DevEnv &e, int parity, bool all, hipStream_t s);
+// human path (re)plans for replan_list[parity] + agent BFS maps for bfs_list[parity]
+// (all envs / all agents when all = true)
+void launch_search(const DevEnv &e, int parity, bool all, hipStream_t s);
 void launch_observe(const DevEnv &e, float *obs, float *vec, hipStream_t s);
 void launch_reset_fixed(const DevEnv &e, hipStream_t s);
 void launch_reset_seeded(const DevEnv &e, hipStream_t s);

@@ -25,7 +25,7 @@
 
 namespace mapf {
 
-__global__ __launch_bounds__(256) void step_kernel(DevEnv e, const int32_t *__restrict__ actions, StepOut out,
+__global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict__ actions, StepOut out,
                                                    uint32_t flags, int parity) {
     const int G = e.G, N = e.N;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,8 +47,16 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, const int32_t *__re
     const int pr = act ? prow(pp) : -100, pc = act ? pcol(pp) : -100;
     const uint32_t gg = act ? e.goal[ai] : 0u;
     const int la = act ? (int)e.last_act[ai] : -1;
-    int a = act ? actions[ai] : 0;
-    if (act && (a < 0 || a >= NA)) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
+    int a = 0;
+    if (flags & 2u) {          // random policy fused in: same stream as random_actions_kernel
+        if (act) {
+            a = (int)__umulhi(philox(env_id, P_ACT | ((uint32_t)i << 8), clock, 0u, e.seed).x, (uint32_t)NA);
+            actions[ai] = a;
+        }
+    } else if (act) {
+        a = actions[ai];
+        if (a < 0 || a >= NA) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
+    }
     const uint32_t *bits = env_map(e, b);
     const uint32_t hp = e.hpos[b], hn = human_next(e, b);
 
@@ -315,11 +323,11 @@ __global__ __launch_bounds__(256) void random_actions_kernel(DevEnv e, int32_t *
     actions[t] = (int32_t)__umulhi(o.x, (uint32_t)NA);
 }
 
-void launch_step(const DevEnv &e, const int32_t *actions, const StepOut &out, uint32_t flags, int parity,
-                 hipStream_t s) {
+void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s) {
     const long threads = (long)e.B * e.G;
-    const int grid = (int)((threads + 255) / 256);
-    hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, s, e, actions, out, flags, parity);
+    const int blk = e.step_block;
+    const int grid = (int)((threads + blk - 1) / blk);
+    hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(blk), 0, s, e, actions, out, flags, parity);
 }
 
 void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s) {

@@ -41,6 +41,7 @@ SIGNATURES = {
     "mapf_path_capacity": (ctypes.c_int, [P]),
     "mapf_reset": (ctypes.c_int, [P, ctypes.POINTER(ResetSpec), P]),
     "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
+    "mapf_step_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_observe": (ctypes.c_int, [P, P, P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),

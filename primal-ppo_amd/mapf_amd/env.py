@@ -148,6 +148,15 @@ class BatchedMapfGym:
                                         1 if commit else 0, _stream(self.device)))
         return self.out
 
+    def step_random(self, actions=None, commit=True):
+        """Random-policy step: actions drawn on device (written to `actions`), then stepped, one launch."""
+        if actions is None:
+            actions = self.actions
+        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
+        _lib.check(_lib.lib().mapf_step_random(self.h, _ptr(actions), ctypes.byref(self._stepout),
+                                               1 if commit else 0, _stream(self.device)))
+        return self.out
+
     def observe(self, obs=None, vec=None):
         """getAllObservations for all envs: obs [B, N, C, F, F], vec [B, N, 4] (float32)."""
         obs = self.obs if obs is None else obs
