@@ -146,6 +146,11 @@ int mapf_step_random(mapf_env *env, int32_t *actions_out, const mapf_step_out *o
 /* getAllObservations for all envs: obs DEVICE float [B][N][C][F][F], vec [B][N][4]. */
 int mapf_observe(mapf_env *env, float *obs, float *vec, void *stream);
 
+/* Launch the search work a committed step left pending (agent.bfsMap updates, the
+ * humans' next paths) on its own; mapf_observe otherwise runs it inside the
+ * observation launch.  Any later call that needs it flushes implicitly. */
+int mapf_flush(mapf_env *env, void *stream);
+
 /* Uniform random policy (Philox, counter = env clock): DEVICE int32 [B][N]. */
 int mapf_random_actions(mapf_env *env, int32_t *actions, void *stream);
 

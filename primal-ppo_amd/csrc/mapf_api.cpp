@@ -48,6 +48,7 @@ struct mapf_env {
     int device = 0;
     DevEnv d{};
     int parity = 1;
+    int pending = -1;        // parity whose search work has not been launched yet
     bool ready = false;
     std::vector<void *> allocs;
     template <class T>
@@ -106,6 +107,8 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.maxd2 = (d.H - 1) * (d.H - 1) + (d.W - 1) * (d.W - 1);
     d.obs_envs = 64 / d.N > 1 ? 64 / d.N : 1;
     d.step_block = 256;
+    d.search_blocks = 64;
+    if (const char *v = std::getenv("MAPF_SEARCH_BLOCKS")) { int x = std::atoi(v); if (x >= 1 && x <= 1024) d.search_blocks = x; }
     if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }
     if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
     if (d.obs_envs > d.B) d.obs_envs = d.B;
@@ -132,17 +135,18 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(map_bits, nmaps * d.Hp * d.WW);
     rc |= e->alloc(d.pos, BN); rc |= e->alloc(d.goal, BN); rc |= e->alloc(d.last_act, BN);
     rc |= e->alloc(d.seq, BN * d.S); rc |= e->alloc(d.seq_len, BN); rc |= e->alloc(d.seq_cur, BN);
-    rc |= e->alloc(d.hpath, (size_t)d.B * d.Lmax);
-    rc |= e->alloc(d.hlen, d.B); rc |= e->alloc(d.hstep, d.B);
-    rc |= e->alloc(d.hpos, d.B); rc |= e->alloc(d.hgoal, d.B); rc |= e->alloc(d.hentr, d.B);
+    rc |= e->alloc(d.hpath, (size_t)d.B * 2 * d.Lmax);
+    rc |= e->alloc(d.hlen, 2 * (size_t)d.B); rc |= e->alloc(d.hstep, d.B); rc |= e->alloc(d.hcur, d.B);
+    rc |= e->alloc(d.hpos, d.B); rc |= e->alloc(d.hnext, d.B); rc |= e->alloc(d.hgoal, d.B); rc |= e->alloc(d.hentr, d.B);
+    rc |= e->alloc(d.hnext_start, d.B); rc |= e->alloc(d.hnext_goal, d.B);
     rc |= e->alloc(d.hseq, (size_t)d.B * d.HS); rc |= e->alloc(d.hseq_len, d.B); rc |= e->alloc(d.hseq_idx, d.B);
     rc |= e->alloc(d.hreplans, d.B); rc |= e->alloc(d.clock, d.B);
     if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * d.H * d.W);
     rc |= e->alloc(d.counters, C_NUM);
     rc |= e->alloc(d.replan_list, 2 * (size_t)d.B);
     rc |= e->alloc(d.bfs_list, 2 * BN);
-    int16_t *binit = nullptr;
-    rc |= e->alloc(binit, nmaps * (size_t)((d.H * d.W + 7) & ~7));
+    uint8_t *smask = nullptr;
+    rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
     rc |= e->alloc(dl, dist_lut.size());
     if (rc) {
@@ -151,7 +155,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
         return fail(MAPF_ENOMEM, m);
     }
     d.map_bits = map_bits;
-    d.bfs_init = binit;
+    d.smask = smask;
     d.cost_lut = cl;
     d.dist_lut = dl;
     if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
@@ -202,10 +206,18 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
                 if (ob) mb[r * d.WW + (c >> 5)] |= 1u << (c & 31);
             }
     }
-    const int cells_pad = (H * W + 7) & ~7;
-    std::vector<int16_t> binit(nmaps * cells_pad, (int16_t)-1);
+    // static-invalid action mask of every cell (getInvalidActions' first list, mapf_gym.py:349-352)
+    std::vector<uint8_t> smask(nmaps * H * W, 0);
     for (size_t m = 0; m < nmaps; ++m)
-        for (int k = 0; k < H * W; ++k) binit[m * cells_pad + k] = spec->maps[m * H * W + k] == 0 ? (int16_t)-2 : (int16_t)-1;
+        for (int r = 0; r < H; ++r)
+            for (int c = 0; c < W; ++c) {
+                uint8_t mk = 0;
+                for (int a = 0; a < 5; ++a) {
+                    const int rr = r + dr(a), cc = c + dc(a);
+                    if (rr < 0 || rr >= H || cc < 0 || cc >= W || spec->maps[m * H * W + rr * W + cc] != 0) mk |= 1u << a;
+                }
+                smask[m * H * W + r * W + c] = mk;
+            }
     auto free_at = [&](int b, int r, int c) {
         if (r < 0 || r >= H || c < 0 || c >= W) return false;
         const size_t m = d.shared_map ? 0 : (size_t)b;
@@ -266,7 +278,7 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     }
 
     HIPCHK(hipMemcpyAsync((void *)d.map_bits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync((void *)d.bfs_init, binit.data(), binit.size() * 2, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync((void *)d.smask, smask.data(), smask.size(), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d.counters, 0, C_NUM * sizeof(uint32_t), s));
     if (spec->mode == 0) {
         HIPCHK(hipMemcpyAsync(d.seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice, s));
@@ -282,10 +294,13 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     } else {
         launch_reset_seeded(d, s);
     }
-    launch_search(d, 0, true, s);
+    launch_search(d, 0, 1, s);     // first human paths (buffer 0) + every agent's BFS map
+    launch_plan(d, 1, s);          // promote them, plan each human's next path
+    launch_search(d, 0, 2, s);     // ... and search it (buffer 1)
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // host staging buffers die at return
     e->parity = 1;
+    e->pending = -1;
     e->ready = true;
     return MAPF_OK;
 }
@@ -301,13 +316,26 @@ static int step_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, ui
         o.train_valid = out->train_valid; o.actions_fixed = out->actions_fixed; o.goals_reached = out->goals_reached;
         o.constraints = out->constraints; o.reward_total = out->reward_total;
     }
+    if (e->pending >= 0) {             // previous step's search work was not observed-through
+        launch_search(e->d, e->pending, 0, s);
+        e->pending = -1;
+    }
     const int parity = e->parity;
     launch_step(e->d, actions, o, flags, parity, s);
     if (flags & MAPF_STEP_COMMIT) {
-        if (e->d.human_mode != 0 || e->d.keep_bfs) launch_search(e->d, parity, false, s);
+        if (e->d.human_mode != 0 || e->d.keep_bfs) e->pending = parity;
         e->parity ^= 1;
     }
     HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+static int flush_search(mapf_env *e, hipStream_t s) {
+    if (e->pending >= 0) {
+        launch_search(e->d, e->pending, 0, s);
+        e->pending = -1;
+        HIPCHK(hipGetLastError());
+    }
     return MAPF_OK;
 }
 
@@ -323,9 +351,26 @@ int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
     if (!e || !obs || !vec) return fail(MAPF_EINVAL, "null argument");
     if (!e->ready) return fail(MAPF_ESTATE, "mapf_observe before mapf_reset");
     HIPCHK(hipSetDevice(e->device));
-    launch_observe(e->d, obs, vec, (hipStream_t)stream);
+    hipStream_t s = (hipStream_t)stream;
+    int nsearch = 0, parity = 0;
+    if (e->pending >= 0) {
+        if (e->d.C >= 7 || !observe_hosts_search(e->d)) {   // BFS channel needs the maps / wide grids: search first
+            if (int rc = flush_search(e, s)) return rc;
+        } else {                       // search work rides in the observe launch
+            nsearch = e->d.search_blocks;
+            parity = e->pending;
+            e->pending = -1;
+        }
+    }
+    launch_observe(e->d, obs, vec, nsearch, parity, s);
     HIPCHK(hipGetLastError());
     return MAPF_OK;
+}
+
+int mapf_flush(mapf_env *e, void *stream) {
+    if (!e) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    return flush_search(e, (hipStream_t)stream);
 }
 
 int mapf_random_actions(mapf_env *e, int32_t *actions, void *stream) {
@@ -341,6 +386,7 @@ int mapf_bfs(mapf_env *e, int16_t *dist, void *stream) {
     if (!e || !dist) return fail(MAPF_EINVAL, "null argument");
     if (!e->d.keep_bfs) return fail(MAPF_ESTATE, "keep_bfs is off");
     HIPCHK(hipSetDevice(e->device));
+    if (int rc = flush_search(e, (hipStream_t)stream)) return rc;
     const size_t n = (size_t)e->d.B * e->d.N * e->d.H * e->d.W * sizeof(int16_t);
     HIPCHK(hipMemcpyAsync(dist, e->d.bfs, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return MAPF_OK;
@@ -350,6 +396,7 @@ int mapf_get_counters(mapf_env *e, uint32_t *host16, void *stream) {
     if (!e || !host16) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = flush_search(e, s)) return rc;
     HIPCHK(hipMemcpyAsync(host16, e->d.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return MAPF_OK;
@@ -361,17 +408,20 @@ int mapf_get_state(mapf_env *e, const mapf_state *h, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     const DevEnv &d = e->d;
     const size_t BN = (size_t)d.B * d.N;
-    std::vector<uint32_t> pos(BN), goal(BN), hpath((size_t)d.B * d.Lmax), hp(d.B), hg(d.B), he(d.B), clk(d.B);
+    std::vector<uint32_t> pos(BN), goal(BN), hpath((size_t)d.B * 2 * d.Lmax), hp(d.B), hn(d.B), hg(d.B), he(d.B), clk(d.B);
     std::vector<int8_t> la(BN);
-    std::vector<int32_t> cur(BN), hl(d.B), hs(d.B);
+    std::vector<int32_t> cur(BN), hl(2 * (size_t)d.B), hs(d.B), hc(d.B);
+    if (int rc = flush_search(e, s)) return rc;
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipMemcpy(pos.data(), d.pos, BN * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(goal.data(), d.goal, BN * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(la.data(), d.last_act, BN, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(cur.data(), d.seq_cur, BN * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hpath.data(), d.hpath, hpath.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(hl.data(), d.hlen, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hl.data(), d.hlen, 2 * d.B * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hs.data(), d.hstep, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hc.data(), d.hcur, d.B * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hn.data(), d.hnext, d.B * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hp.data(), d.hpos, d.B * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hg.data(), d.hgoal, d.B * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(he.data(), d.hentr, d.B * 4, hipMemcpyDeviceToHost));
@@ -383,9 +433,9 @@ int mapf_get_state(mapf_env *e, const mapf_state *h, void *stream) {
         if (h->seq_cursor) h->seq_cursor[k] = cur[k];
     }
     for (int b = 0; b < d.B; ++b) {
-        const uint32_t *path = hpath.data() + (size_t)b * d.Lmax;
-        const int st = hs[b], len = hl[b];
-        const uint32_t nx = (len <= 0) ? hp[b] : (st >= len - 1 ? path[len - 1] : path[st + 1]);
+        const uint32_t *path = hpath.data() + ((size_t)b * 2 + hc[b]) * d.Lmax;
+        const int st = hs[b], len = hl[2 * b + hc[b]];
+        const uint32_t nx = hn[b];
         if (h->human) {
             int32_t *o = h->human + 10 * b;
             o[0] = prow(hp[b]); o[1] = pcol(hp[b]); o[2] = prow(nx); o[3] = pcol(nx);
@@ -408,6 +458,7 @@ int mapf_set_state(mapf_env *e, const mapf_state *h, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     DevEnv &d = e->d;
     const size_t BN = (size_t)d.B * d.N;
+    if (int rc = flush_search(e, s)) return rc;
     HIPCHK(hipStreamSynchronize(s));
     if (h->pos) {
         std::vector<uint32_t> v(BN);
@@ -437,18 +488,20 @@ int mapf_set_state(mapf_env *e, const mapf_state *h, void *stream) {
     }
     if (h->seq_cursor) HIPCHK(hipMemcpy(d.seq_cur, h->seq_cursor, BN * 4, hipMemcpyHostToDevice));
     if (h->human_path && h->human) {
-        std::vector<uint32_t> path((size_t)d.B * d.Lmax, 0u);
-        std::vector<int32_t> hl(d.B);
+        // the given path becomes buffer 0 (current); buffer 1 is re-planned below
+        std::vector<uint32_t> path((size_t)d.B * 2 * d.Lmax, 0u);
+        std::vector<int32_t> hl(2 * (size_t)d.B, 1), hc(d.B, 0);
         for (int b = 0; b < d.B; ++b) {
             const int len = h->human[10 * b + 7];
             if (len < 1 || len > d.Lmax) return fail(MAPF_EINVAL, "human path length out of range");
-            hl[b] = len;
+            hl[2 * b] = len;
             for (int k = 0; k < len; ++k)
-                path[(size_t)b * d.Lmax + k] = pack(h->human_path[((size_t)b * d.Lmax + k) * 2],
-                                                    h->human_path[((size_t)b * d.Lmax + k) * 2 + 1]);
+                path[(size_t)b * 2 * d.Lmax + k] = pack(h->human_path[((size_t)b * d.Lmax + k) * 2],
+                                                        h->human_path[((size_t)b * d.Lmax + k) * 2 + 1]);
         }
         HIPCHK(hipMemcpy(d.hpath, path.data(), path.size() * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(d.hlen, hl.data(), d.B * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hlen, hl.data(), hl.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.hcur, hc.data(), d.B * 4, hipMemcpyHostToDevice));
     }
     if (h->human) {
         std::vector<uint32_t> hp(d.B), hg(d.B), he(d.B);
@@ -463,6 +516,14 @@ int mapf_set_state(mapf_env *e, const mapf_state *h, void *stream) {
         HIPCHK(hipMemcpy(d.hentr, he.data(), d.B * 4, hipMemcpyHostToDevice));
     }
     if (h->clock) HIPCHK(hipMemcpy(d.clock, h->clock, d.B * 4, hipMemcpyHostToDevice));
+    if (h->human || h->clock) {
+        // position / next position follow the path and step (Human.getPos / getNextPos);
+        // the next path is re-planned for the new (clock, step) and searched
+        launch_plan(d, 0, s);
+        launch_search(d, 0, 2, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(s));
+    }
     return MAPF_OK;
 }
 

@@ -7,7 +7,11 @@
 //   pos, goal [B*N] u32             packed cell (row | col << 16)
 //   last_act  [B*N] i8              -1 = none (Agent.invalidActions[2] empty)
 //   seq       [B*N*S] u32, seq_len/seq_cur [B*N]   agentsSequence
-//   hpath     [B*Lmax] u32, hlen/hstep [B], hpos/hgoal/hentr [B]   human
+//   hpath     [B][2][Lmax] u32      human path, double buffered: hcur[b] is the
+//                                   current path, the other buffer holds the path
+//                                   the human will switch to at the end of it
+//                                   (precomputed off the critical path)
+//   hlen [B][2], hcur/hstep [B], hpos/hnext/hgoal/hentr [B], hnext_start/hnext_goal [B]
 //   bfs       [B*N*H*W] i16         agent.bfsMap (keep_bfs)
 //   counters  [32] u32              error counters + work-list counts
 //   replan_list [2][B], bfs_list [2][B*N]  per-step work lists (step parity)
@@ -51,9 +55,11 @@ struct DevEnv {
     int8_t *last_act;
     uint32_t *seq;
     int32_t *seq_len, *seq_cur;
-    uint32_t *hpath;
-    int32_t *hlen, *hstep;
-    uint32_t *hpos, *hgoal, *hentr;
+    uint32_t *hpath;          // [B][2][Lmax]
+    int32_t *hlen;            // [B][2]
+    int32_t *hcur, *hstep;
+    uint32_t *hpos, *hnext, *hgoal, *hentr;
+    uint32_t *hnext_start, *hnext_goal;   // the next path's endpoints (NO_CELL = none)
     uint32_t *hseq;
     int32_t *hseq_len, *hseq_idx;
     uint32_t *hreplans, *clock;
@@ -61,8 +67,11 @@ struct DevEnv {
     uint32_t *counters, *replan_list, *bfs_list;
     const float *cost_lut;    // [R*R+1]: float32(max(R - sqrt(d2), 0) / R) (fp64 like the reference)
     const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
-    const int16_t *bfs_init;  // [nmaps][cells rounded up to 8]: makeBfsMap's initial copy (-1 obstacle, -2 free)
+    const uint8_t *smask;     // [nmaps][H*W]: static-invalid action mask of each cell (getInvalidActions[0])
+    int search_blocks;        // workgroups of the observe launch that run search work
 };
+
+constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
 
 __host__ __device__ inline uint32_t pack(int r, int c) { return (uint32_t)(r & 0xFFFF) | ((uint32_t)c << 16); }
 __host__ __device__ inline int prow(uint32_t p) { return (int)(p & 0xFFFF); }
@@ -95,12 +104,11 @@ __device__ inline const uint32_t *env_map(const DevEnv &e, int b) {
     return e.map_bits + (e.shared_map ? 0 : (size_t)b * e.Hp * e.WW);
 }
 
-// Human.getNextPos (mapf_gym.py:46-50).
-__device__ inline uint32_t human_next(const DevEnv &e, int b) {
-    int st = e.hstep[b], len = e.hlen[b];
-    const uint32_t *path = e.hpath + (size_t)b * e.Lmax;
-    return st >= len - 1 ? path[len - 1] : path[st + 1];
+__device__ inline uint32_t *human_path(const DevEnv &e, int b, int buf) {
+    return e.hpath + ((size_t)b * 2 + buf) * e.Lmax;
 }
+// Human.getNextPos (mapf_gym.py:46-50), maintained in hnext[b] by the step kernel.
+__device__ inline uint32_t human_next(const DevEnv &e, int b) { return e.hnext[b]; }
 
 // Wave-level helpers ---------------------------------------------------------
 __device__ inline int lane_id() { return threadIdx.x & 63; }

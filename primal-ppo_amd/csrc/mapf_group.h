@@ -68,4 +68,30 @@ __device__ bool group_free_cell(const DevEnv &e, uint32_t env_id, uint32_t purpo
     return false;
 }
 
+// The path the human switches to when its current path ends.  The reference
+// replans at that end-step (Human.nextStep -> getNextGoal, mapf_gym.py:25-31,
+// :42-44; FixedPathHuman.getNextGoal :87-94); its goal draw depends only on
+// the clock of that step, `epoch` = clock + len - 1 - hstep, so the path can be
+// planned (and searched) ahead of time.  Mode 1: a fresh getFreeCell goal on the
+// human's world (entrance marked) from the entrance; mode 2: the next scripted
+// pose from the current one; mode 0 (LoopingHuman) never switches.
+__device__ inline void plan_next_path(const DevEnv &e, int b, uint32_t env_id, uint32_t epoch, int seq_idx,
+                                      uint32_t &nstart, uint32_t &ngoal, bool leader) {
+    nstart = NO_CELL;
+    ngoal = NO_CELL;
+    if (e.human_mode == 1) {
+        const uint32_t ent = e.hentr[b];
+        const uint32_t *bits = env_map(e, b);
+        auto ok = [&](int r, int c) -> bool { return !obstacle_at(e, bits, r, c) && pack(r, c) != ent; };
+        int r, c;
+        if (group_free_cell(e, env_id, P_HGOAL, 0, epoch, ok, r, c)) { nstart = ent; ngoal = pack(r, c); }
+        else if (leader) atomicAdd(&e.counters[C_FREECELL], 1u);
+    } else if (e.human_mode == 2) {
+        if (seq_idx + 1 < e.hseq_len[b]) {
+            nstart = e.hseq[(size_t)b * e.HS + seq_idx];
+            ngoal = e.hseq[(size_t)b * e.HS + seq_idx + 1];
+        }
+    }
+}
+
 }  // namespace mapf

@@ -19,10 +19,14 @@ struct StepOut {          // device pointers (mapf_step_out)
 // flags: bit0 commit (jointStep), bit1 random policy (draw actions in-kernel into `actions`)
 void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s);
 void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s);
-// human path (re)plans for replan_list[parity] + agent BFS maps for bfs_list[parity]
-// (all envs / all agents when all = true)
-void launch_search(const DevEnv &e, int parity, bool all, hipStream_t s);
-void launch_observe(const DevEnv &e, float *obs, float *vec, hipStream_t s);
+// humans' next paths (replan_list[parity]) + agent BFS maps (bfs_list[parity]);
+// all = 1: every env's next path and every agent's map, 2: every env's next path
+void launch_search(const DevEnv &e, int parity, int all, hipStream_t s);
+// plan every human's next path from the state (promote: buffer hcur^1 becomes current first)
+void launch_plan(const DevEnv &e, int promote, hipStream_t s);
+// observations; the first nsearch workgroups run the search work of `parity`
+void launch_observe(const DevEnv &e, float *obs, float *vec, int nsearch, int parity, hipStream_t s);
+bool observe_hosts_search(const DevEnv &e);
 void launch_reset_fixed(const DevEnv &e, hipStream_t s);
 void launch_reset_seeded(const DevEnv &e, hipStream_t s);
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,

@@ -21,6 +21,7 @@
 //  phase 4  stream -> float4 stores (coalesced, 1 KiB per wave instruction)
 #include "mapf_common.h"
 #include "mapf_kernels.h"
+#include "mapf_search.h"
 
 namespace mapf {
 
@@ -53,10 +54,29 @@ __device__ inline int isqrt_floor(int x) {
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restrict__ obs, float *__restrict__ vec) {
+// The first `nsearch` workgroups run the step's search work (agent BFS maps,
+// humans' next paths -- mapf_search.h), the rest write observations: the
+// latency-bound searches hide under the HBM-bound observation stores.
+// Only the narrow-row search (W <= 32, H <= 64: configs c1-c3) is hosted: its
+// register footprint matches the observation role's; wider grids search in
+// their own launch so the observation workgroups keep their occupancy.
+template <bool HOST>
+__global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restrict__ obs, float *__restrict__ vec,
+                                                      int nsearch, int parity) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if constexpr (HOST) {
+        if ((int)blockIdx.x < nsearch) {
+            const int wave = threadIdx.x >> 6;
+            char *lds = smem + (size_t)wave * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+            srch::search_items<uint32_t, 1>(e, parity, 0, lds, blockIdx.x * (blockDim.x >> 6) + wave,
+                                            nsearch * (blockDim.x >> 6));
+            return;
+        }
+    } else {
+        nsearch = 0;
+    }
     const int E = e.obs_envs, N = e.N, F = e.F, C = e.C, FF = F * F, CFF = C * FF;
-    const int b0 = blockIdx.x * E;
+    const int b0 = ((int)blockIdx.x - nsearch) * E;
     const int nenv = min(E, e.B - b0);
     const int K = nenv * N;                       // agents in this workgroup
     const int rowsz = e.Hp * e.WW;
@@ -89,8 +109,9 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
         shn[k] = human_next(e, b);
         int cnt = 0;
         if (e.use_hp && C >= 6) {
-            const int len = e.hlen[b];
-            const uint32_t *path = e.hpath + (size_t)b * e.Lmax;
+            const int cur = e.hcur[b];
+            const int len = e.hlen[b * 2 + cur];
+            const uint32_t *path = human_path(e, b, cur);
             for (int q = 1; q <= e.k_predict && q < len; ++q) shp[k * e.k_predict + cnt++] = path[q];
         }
         shpn[k] = cnt;
@@ -219,9 +240,19 @@ size_t observe_lds(const DevEnv &e) {
     return words * 4;
 }
 
-void launch_observe(const DevEnv &e, float *obs, float *vec, hipStream_t s) {
-    const int grid = (e.B + e.obs_envs - 1) / e.obs_envs;
-    hipLaunchKernelGGL(observe_kernel, dim3(grid), dim3(256), observe_lds(e), s, e, obs, vec);
+bool observe_hosts_search(const DevEnv &e) { return e.W <= 32 && e.H <= 64; }
+
+void launch_observe(const DevEnv &e, float *obs, float *vec, int nsearch, int parity, hipStream_t s) {
+    if (!observe_hosts_search(e)) nsearch = 0;
+    const int grid = (e.B + e.obs_envs - 1) / e.obs_envs + nsearch;
+    size_t lds = observe_lds(e);
+    if (nsearch > 0) {
+        const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+        if (sl > lds) lds = sl;
+        hipLaunchKernelGGL(observe_kernel<true>, dim3(grid), dim3(256), lds, s, e, obs, vec, nsearch, parity);
+    } else {
+        hipLaunchKernelGGL(observe_kernel<false>, dim3(grid), dim3(256), lds, s, e, obs, vec, 0, parity);
+    }
 }
 
 }  // namespace mapf

@@ -31,15 +31,19 @@ __global__ __launch_bounds__(256) void reset_fixed_kernel(DevEnv e) {
         e.last_act[t] = -1;
     }
     if (t < e.B) {
+        // the first path is searched into buffer hcur ^ 1 = 0, then promoted (launch_plan)
         e.hstep[t] = 0;
         e.hseq_idx[t] = 1;
         e.clock[t] = 0;
         e.hreplans[t] = 0;
+        e.hcur[t] = 1;
         if (e.human_mode == 2) {
             e.hpos[t] = e.hseq[(size_t)t * e.HS + 0];
             e.hgoal[t] = e.hseq[(size_t)t * e.HS + 1];
         }
         e.hentr[t] = e.hpos[t];
+        e.hnext_start[t] = e.hpos[t];
+        e.hnext_goal[t] = e.hgoal[t];
     }
 }
 
@@ -105,6 +109,9 @@ __global__ __launch_bounds__(256) void reset_seeded_kernel(DevEnv e) {
         e.hseq_idx[b] = 1;
         e.clock[b] = 0;
         e.hreplans[b] = 0;
+        e.hcur[b] = 1;
+        e.hnext_start[b] = ent;
+        e.hnext_goal[b] = hgoal;
     }
 }
 

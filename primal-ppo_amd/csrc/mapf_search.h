@@ -1,0 +1,335 @@
+// primal-ppo_amd/csrc/mapf_search.h -- wave-level grid searches (device code).
+//
+// Two kinds of work item, both one wave each:
+//  * makeBfsMap (mapf_gym.py:211-244) for an agent whose goal changed:
+//    bfs[b][i] = obstacleMap copy with free cells -2, then the level-order
+//    distance from the goal (goal = 0, even on an obstacle).
+//  * the human's next path (Human.getAstarPath, mapf_gym.py:33-37, astar_4.py:
+//    21-109) between hnext_start[b] and hnext_goal[b], into the path buffer
+//    the human is NOT using (hcur[b] ^ 1).
+//
+// astar_4 as BFS + walk-back.  astar_4's heap pops in the total order of the
+// keys (f, g, row, col) -- duplicate entries of one cell share their key, so
+// the parent field of the heap tuple never matters -- and the pops are
+// monotone under the consistent Manhattan heuristic; `parents[c]` is
+// overwritten whenever new_g <= g_scores[c] (astar_4.py:58).  So parent(c) is
+// the LAST expanded neighbour p with d(p) = d(c) - 1, i.e. the one with the
+// largest key (h(p), row, col) -- every such p has a smaller key than c and is
+// expanded before c is popped.  The path is therefore: BFS distances from the
+// start (stopped at the goal's level), then a walk back from the goal taking,
+// at each step, the neighbour at distance d-1 with the largest
+// (manhattan-to-goal, row, col).  Pinned by tests/golden/g3_search.npz (the
+// reference's own astar_4 outputs) and by the oracle's literal heap A*.
+//
+// Register-only BFS.  Grid rows live on the lanes (row r = lane + 64k, k < RW),
+// each row a W-bit mask (u32 / u64 / 2 x u64).  One BFS level = one frontier
+// dilation: horizontal neighbours by shifting the row, vertical neighbours by
+// DPP wave_shr:1 / wave_shl:1.  Distances are accumulated as K bit planes
+// (plane k holds bit k of every visited cell's distance) -- no memory traffic
+// inside the loop.  The walk-back needs only d mod 4: the grid graph is
+// bipartite, so two adjacent reachable cells differ by exactly one level and
+// "d(p) == d(c) - 1" <=> p visited and d(p) = d(c) - 1 (mod 4).
+#pragma once
+#include "mapf_common.h"
+
+namespace mapf {
+namespace srch {
+
+struct Row2 { uint64_t lo, hi; };
+
+__device__ inline uint32_t r_or(uint32_t a, uint32_t b) { return a | b; }
+__device__ inline uint64_t r_or(uint64_t a, uint64_t b) { return a | b; }
+__device__ inline Row2 r_or(Row2 a, Row2 b) { return {a.lo | b.lo, a.hi | b.hi}; }
+__device__ inline uint32_t r_and(uint32_t a, uint32_t b) { return a & b; }
+__device__ inline uint64_t r_and(uint64_t a, uint64_t b) { return a & b; }
+__device__ inline Row2 r_and(Row2 a, Row2 b) { return {a.lo & b.lo, a.hi & b.hi}; }
+__device__ inline uint32_t r_andn(uint32_t a, uint32_t b) { return a & ~b; }
+__device__ inline uint64_t r_andn(uint64_t a, uint64_t b) { return a & ~b; }
+__device__ inline Row2 r_andn(Row2 a, Row2 b) { return {a.lo & ~b.lo, a.hi & ~b.hi}; }
+__device__ inline uint32_t r_nb(uint32_t a) { return (a << 1) | (a >> 1); }
+__device__ inline uint64_t r_nb(uint64_t a) { return (a << 1) | (a >> 1); }
+__device__ inline Row2 r_nb(Row2 a) {
+    return {(a.lo << 1) | (a.lo >> 1) | (a.hi << 63), (a.hi << 1) | (a.hi >> 1) | (a.lo >> 63)};
+}
+__device__ inline uint32_t r_shl1(uint32_t a) { return a << 1; }
+__device__ inline uint64_t r_shl1(uint64_t a) { return a << 1; }
+__device__ inline Row2 r_shl1(Row2 a) { return {a.lo << 1, (a.hi << 1) | (a.lo >> 63)}; }
+__device__ inline uint32_t r_shr1(uint32_t a) { return a >> 1; }
+__device__ inline uint64_t r_shr1(uint64_t a) { return a >> 1; }
+__device__ inline Row2 r_shr1(Row2 a) { return {(a.lo >> 1) | (a.hi << 63), a.hi >> 1}; }
+__device__ inline bool r_any(uint32_t a) { return a != 0; }
+__device__ inline bool r_any(uint64_t a) { return a != 0; }
+__device__ inline bool r_any(Row2 a) { return (a.lo | a.hi) != 0; }
+__device__ inline uint32_t r_get(uint32_t a, int c) { return (a >> c) & 1u; }
+__device__ inline uint32_t r_get(uint64_t a, int c) { return (uint32_t)((a >> c) & 1ull); }
+__device__ inline uint32_t r_get(Row2 a, int c) {
+    return c < 64 ? (uint32_t)((a.lo >> c) & 1ull) : (uint32_t)((a.hi >> (c - 64)) & 1ull);
+}
+template <class T> __device__ inline T r_bit(int c);
+template <> __device__ inline uint32_t r_bit<uint32_t>(int c) { return 1u << c; }
+template <> __device__ inline uint64_t r_bit<uint64_t>(int c) { return 1ull << c; }
+template <> __device__ inline Row2 r_bit<Row2>(int c) { return c < 64 ? Row2{1ull << c, 0} : Row2{0, 1ull << (c - 64)}; }
+template <class T> __device__ inline T r_zero() { return T{}; }
+
+// lane i <- lane i-1 (DPP wave_shr:1) / lane i <- lane i+1 (wave_shl:1); edge lanes read 0
+__device__ inline uint32_t from_below(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+}
+__device__ inline uint32_t from_above(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
+}
+__device__ inline uint64_t from_below(uint64_t x) {
+    return ((uint64_t)from_below((uint32_t)(x >> 32)) << 32) | from_below((uint32_t)x);
+}
+__device__ inline uint64_t from_above(uint64_t x) {
+    return ((uint64_t)from_above((uint32_t)(x >> 32)) << 32) | from_above((uint32_t)x);
+}
+__device__ inline Row2 from_below(Row2 x) { return {from_below(x.lo), from_below(x.hi)}; }
+__device__ inline Row2 from_above(Row2 x) { return {from_above(x.lo), from_above(x.hi)}; }
+__device__ inline uint32_t rdlane(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+__device__ inline uint64_t rdlane(uint64_t x, int l) {
+    return ((uint64_t)rdlane((uint32_t)(x >> 32), l) << 32) | rdlane((uint32_t)x, l);
+}
+__device__ inline Row2 rdlane(Row2 x, int l) { return {rdlane(x.lo, l), rdlane(x.hi, l)}; }
+
+__device__ inline uint64_t bits64_at(const uint32_t *row, int WW, int off) {
+    const int w = off >> 5, s = off & 31;
+    auto word = [&](int k) -> uint64_t { return (k < WW) ? (uint64_t)row[k] : 0xFFFFFFFFull; };
+    const uint64_t a = word(w) | (word(w + 1) << 32);
+    const uint64_t b = word(w + 2);
+    return s == 0 ? a : ((a >> s) | (b << (64 - s)));
+}
+template <class T> __device__ inline T free_row(const DevEnv &e, const uint32_t *bits, int r);
+template <> __device__ inline uint64_t free_row<uint64_t>(const DevEnv &e, const uint32_t *bits, int r) {
+    if (r >= e.H) return 0;
+    const uint64_t f = ~bits64_at(bits + (size_t)(r + e.P) * e.WW, e.WW, e.P);
+    return e.W >= 64 ? f : (f & ((1ull << e.W) - 1));
+}
+template <> __device__ inline uint32_t free_row<uint32_t>(const DevEnv &e, const uint32_t *bits, int r) {
+    return (uint32_t)free_row<uint64_t>(e, bits, r);
+}
+template <> __device__ inline Row2 free_row<Row2>(const DevEnv &e, const uint32_t *bits, int r) {
+    if (r >= e.H) return {0, 0};
+    const uint32_t *row = bits + (size_t)(r + e.P) * e.WW;
+    Row2 f = {~bits64_at(row, e.WW, e.P), ~bits64_at(row, e.WW, e.P + 64)};
+    if (e.W < 128) f.hi &= (1ull << (e.W - 64)) - 1;
+    return f;
+}
+
+template <class T> struct Kbits;   // distance bit planes: max distance < cells <= 64*RW*width
+template <> struct Kbits<uint32_t> { static constexpr int v = 12; };
+template <> struct Kbits<uint64_t> { static constexpr int v = 13; };
+template <> struct Kbits<Row2> { static constexpr int v = 14; };
+
+// Level-synchronous BFS over free cells from (sr, sc).  V = visited rows,
+// D[k] = bit k of each visited cell's distance.  Stops after the level that
+// reaches (stop_r, stop_c) when stop_r >= 0 and returns that level; returns the
+// last level otherwise (-1 if the stop cell was never reached).
+template <class T, int RW, int K>
+__device__ int bfs_planes(const T (&fre)[RW], int sr, int sc, int stop_r, int stop_c, T (&V)[RW], T (&D)[K][RW]) {
+    const int lane = lane_id();
+    T fr[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        fr[k] = (lane + 64 * k == sr) ? r_bit<T>(sc) : r_zero<T>();
+        V[k] = fr[k];
+#pragma unroll
+        for (int q = 0; q < K; ++q) D[q][k] = r_zero<T>();
+    }
+    if (stop_r == sr && stop_c == sc) return 0;
+    int d = 1;
+    for (;; ++d) {
+        T up[RW], dn[RW], nw[RW];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) { up[k] = from_below(fr[k]); dn[k] = from_above(fr[k]); }
+        if (RW == 2) {
+            const T a = rdlane(fr[0], 63), b = rdlane(fr[RW - 1], 0);
+            if (lane == 0) up[RW - 1] = a;      // row 64 <- row 63
+            if (lane == 63) dn[0] = b;          // row 63 <- row 64
+        }
+        bool any = false, hit = false;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            nw[k] = r_andn(r_and(r_or(r_or(r_nb(fr[k]), up[k]), dn[k]), fre[k]), V[k]);
+            any |= r_any(nw[k]);
+            if (lane + 64 * k == stop_r && r_get(nw[k], stop_c)) hit = true;
+        }
+        if (__ballot(any) == 0ull) return stop_r >= 0 ? -1 : d - 1;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            V[k] = r_or(V[k], nw[k]);
+            fr[k] = nw[k];
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                if ((d >> q) & 1) D[q][k] = r_or(D[q][k], nw[k]);
+        }
+        if (stop_r >= 0 && __ballot(hit) != 0ull) return d;
+    }
+}
+
+// bit c of the row held by lane `ln` in slot `sl` (ln, sl, c wave-uniform): a v_readlane
+__device__ inline uint32_t word_of(uint32_t x, int) { return x; }
+__device__ inline uint32_t word_of(uint64_t x, int w) { return w ? (uint32_t)(x >> 32) : (uint32_t)x; }
+__device__ inline uint32_t word_of(Row2 x, int w) {
+    const uint64_t q = (w >> 1) ? x.hi : x.lo;
+    return (w & 1) ? (uint32_t)(q >> 32) : (uint32_t)q;
+}
+template <class T, int RW>
+__device__ inline uint32_t row_bit(const T (&m)[RW], int sl, int ln, int c) {
+    const uint32_t w = word_of(sl ? m[RW - 1] : m[0], c >> 5);
+    return ((uint32_t)__builtin_amdgcn_readlane((int)w, ln) >> (c & 31)) & 1u;
+}
+
+// LDS bytes one wave needs
+template <class T, int RW>
+__host__ __device__ inline size_t wave_lds(int H, int W) {
+    const size_t planes = 3 * (size_t)64 * RW * sizeof(T);
+    const size_t img = (size_t)((H * W + 7) & ~7) * 2;
+    return ((planes > img ? planes : img) + 15) & ~(size_t)15;
+}
+
+// All search items of one step (or of a reset), grid-strided over waves.
+//   all = 0: the step's work lists (parity); 1: every env's next path + every
+//   agent's BFS map; 2: every env's next path only.
+template <class T, int RW>
+__device__ void search_items(const DevEnv &e, int parity, int all, char *lds, uint32_t wave_id, uint32_t nwaves) {
+    constexpr int K = Kbits<T>::v;
+    const int lane = lane_id();
+    const int W = e.W, H = e.H, cells = H * W;
+    const uint32_t n_replan = all ? (uint32_t)e.B : e.counters[C_REPLAN_COUNT + parity];
+    const uint32_t n_bfs = (!e.keep_bfs || all == 2) ? 0u : (all ? (uint32_t)(e.B * e.N) : e.counters[C_BFS_COUNT + parity]);
+    const uint32_t total = n_replan + n_bfs;
+    for (uint32_t item = wave_id; item < total; item += nwaves) {
+        const bool replan = item < n_replan;
+        uint32_t ai = 0, sr_cell, stop_cell = NO_CELL;
+        int b;
+        if (replan) {
+            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];
+            stop_cell = e.hnext_goal[b];
+            if (stop_cell == NO_CELL) continue;
+            sr_cell = e.hnext_start[b];
+        } else {
+            const uint32_t k = item - n_replan;
+            ai = all ? k : e.bfs_list[(size_t)parity * e.B * e.N + k];
+            b = (int)(ai / (uint32_t)e.N);
+            sr_cell = e.goal[ai];
+        }
+        const uint32_t *bits = env_map(e, b);
+        T fre[RW], V[RW], D[K][RW];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) fre[k] = free_row<T>(e, bits, lane + 64 * k);
+        const int sr = prow(sr_cell), sc = pcol(sr_cell);
+        if (!replan) {
+            const int maxd = bfs_planes<T, RW, K>(fre, sr, sc, -1, -1, V, D);
+            const int kq = 32 - __builtin_clz((unsigned)maxd | 1u);   // planes in use
+            // decode each row's distances into the LDS image, then one coalesced sweep out
+            int16_t *img = reinterpret_cast<int16_t *>(lds);
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const int r = lane + 64 * k;
+                if (r < H)
+                    for (int c = 0; c < W; ++c) {
+                        int v;
+                        if (r_get(V[k], c)) {
+                            v = 0;
+#pragma unroll
+                            for (int q = 0; q < K; ++q)
+                                if (q < kq) v |= (int)r_get(D[q][k], c) << q;
+                        } else {
+                            v = r_get(fre[k], c) ? -2 : -1;
+                        }
+                        img[r * W + c] = (int16_t)v;
+                    }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            int16_t *outp = e.bfs + (size_t)ai * cells;
+            if ((cells & 7) == 0) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(img);
+                uint4 *dst = reinterpret_cast<uint4 *>(outp);
+                for (int k = lane; k < cells / 8; k += 64) dst[k] = src[k];
+            } else {
+                for (int k = lane; k < cells; k += 64) outp[k] = img[k];
+            }
+        } else {
+            const int gr = prow(stop_cell), gc = pcol(stop_cell);
+            T V2[RW], D2[2][RW];
+            const int d = bfs_planes<T, RW, 2>(fre, sr, sc, gr, gc, V2, D2);
+            // Predecessor masks per row: bit c of pX[k] = the X neighbour of cell (r, c) lies one
+            // BFS level closer to the start (levels compared mod 4: bipartite grid, see header).
+            T pL[RW], pR[RW], pU[RW], pD[RW];
+            {
+                T Lm[4][RW];
+#pragma unroll
+                for (int k = 0; k < RW; ++k) {
+                    const T n0 = r_andn(V2[k], D2[0][k]), n1 = r_and(V2[k], D2[0][k]);
+                    Lm[0][k] = r_andn(n0, D2[1][k]);
+                    Lm[1][k] = r_andn(n1, D2[1][k]);
+                    Lm[2][k] = r_and(n0, D2[1][k]);
+                    Lm[3][k] = r_and(n1, D2[1][k]);
+                    pL[k] = pR[k] = pU[k] = pD[k] = r_zero<T>();
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int pm = (m + 3) & 3;
+                    T up[RW], dn[RW];
+#pragma unroll
+                    for (int k = 0; k < RW; ++k) { up[k] = from_below(Lm[pm][k]); dn[k] = from_above(Lm[pm][k]); }
+                    if (RW == 2) {
+                        const T a = rdlane(Lm[pm][0], 63), bb = rdlane(Lm[pm][RW - 1], 0);
+                        if (lane == 0) up[RW - 1] = a;
+                        if (lane == 63) dn[0] = bb;
+                    }
+#pragma unroll
+                    for (int k = 0; k < RW; ++k) {
+                        pL[k] = r_or(pL[k], r_and(Lm[m][k], r_shl1(Lm[pm][k])));
+                        pR[k] = r_or(pR[k], r_and(Lm[m][k], r_shr1(Lm[pm][k])));
+                        pU[k] = r_or(pU[k], r_and(Lm[m][k], up[k]));
+                        pD[k] = r_or(pD[k], r_and(Lm[m][k], dn[k]));
+                    }
+                }
+            }
+            const int buf = e.hcur[b] ^ 1;
+            uint32_t *path = human_path(e, b, buf);
+            int len;
+            if (d <= 0) {
+                // start == goal (astar_4 returns []) or unreachable (it returns a ValueError):
+                // the reference crashes right after; the human stays put.
+                if (lane == 0) { atomicAdd(&e.counters[C_UNREACHABLE], 1u); path[0] = sr_cell; }
+                len = 1;
+            } else {
+                // walk back from the goal on the scalar unit: parent = predecessor neighbour with
+                // the largest (manhattan-to-goal, row, col) -- astar_4's last overwrite (:58)
+                const bool round_trip = e.human_mode != 2;
+                len = round_trip ? 2 * d + 1 : d + 1;
+                int r = gr, c = gc;
+                for (int k = d; k >= 0; --k) {
+                    const uint32_t cell = pack(r, c);
+                    if (lane == 0) {
+                        path[k] = cell;
+                        if (round_trip) path[2 * d - k] = cell;
+                    }
+                    if (k == 0) break;
+                    const int ln = r & 63, sl = r >> 6;
+                    const uint32_t bl = row_bit(pL, sl, ln, c), br_ = row_bit(pR, sl, ln, c);
+                    const uint32_t bu = row_bit(pU, sl, ln, c), bd = row_bit(pD, sl, ln, c);
+                    int nr = -1, nc = -1, bh = -1;
+                    auto cand = [&](uint32_t ok, int qr, int qc) {
+                        if (!ok) return;
+                        const int h = abs(qr - gr) + abs(qc - gc);
+                        if (h > bh || (h == bh && (qr > nr || (qr == nr && qc > nc)))) { bh = h; nr = qr; nc = qc; }
+                    };
+                    cand(bl, r, c - 1); cand(bu, r - 1, c); cand(br_, r, c + 1); cand(bd, r + 1, c);
+                    if (nr < 0) { if (lane == 0) atomicAdd(&e.counters[C_BAD_STATUS], 1u); break; }
+                    r = nr; c = nc;
+                }
+            }
+            if (lane == 0) e.hlen[b * 2 + buf] = len;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+}  // namespace srch
+}  // namespace mapf

@@ -61,12 +61,14 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     const uint32_t hp = e.hpos[b], hn = human_next(e, b);
 
     // ---- getInvalidActions (mapf_gym.py:339-360) ---------------------------
-    unsigned st_mask = 0, hu_mask = 0;
+    // static part: a per-cell 5-bit mask precomputed from the map (off-map / obstacle)
+    const unsigned st_mask = act ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc] : 0x1Fu;
+    unsigned hu_mask = 0;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
         const int r = pr + dr(k), c = pc + dc(k);
-        if (!in_map(e, r, c) || obstacle_at(e, bits, r, c)) st_mask |= 1u << k;
-        else if (pack(r, c) == hn) hu_mask |= 1u << k;
+        if ((st_mask >> k) & 1u) continue;
+        if (pack(r, c) == hn) hu_mask |= 1u << k;
         else if (pp == hn && pack(r, c) == hp) hu_mask |= 1u << k;
     }
     const unsigned rep_mask = la >= 0 ? 1u << opp(la) : 0u;
@@ -257,50 +259,60 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     }
 
     // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94) -------------------
+    // The path switched to at an end-step was searched one path ahead (search
+    // kernel, buffer hcur ^ 1); here the human only advances, switches buffers
+    // and plans the path after the new one (same goal draw as the reference's).
     uint32_t hp_new;
     {
-        const int hs = e.hstep[b], hl = e.hlen[b];
-        const uint32_t *path = e.hpath + (size_t)b * e.Lmax;
-        if (hs >= hl - 1) {
-            bool replan = false;
-            if (e.human_mode == 0) {
-                hp_new = path[0];
-            } else if (e.human_mode == 1) {
-                const uint32_t ent = e.hentr[b];
-                auto ok = [&](int r, int c) -> bool { return !obstacle_at(e, bits, r, c) && pack(r, c) != ent; };
-                int r, c;
-                if (!group_free_cell(e, env_id, P_HGOAL, 0, clock, ok, r, c)) {
-                    if (i == 0) atomicAdd(&e.counters[C_FREECELL], 1u);
-                    r = prow(hp); c = pcol(hp);
+        const int hs = e.hstep[b], cur = e.hcur[b];
+        const int L = e.hlen[b * 2 + cur];
+        int cur2 = cur, hs2 = hs + 1, seq_idx = 0;
+        bool swapped = false;
+        if (hs >= L - 1) {
+            hs2 = 0;
+            if (e.human_mode == 1) {
+                if (e.hnext_goal[b] != NO_CELL) {
+                    cur2 = cur ^ 1;
+                    swapped = true;
+                    if (i == 0) { e.hgoal[b] = e.hnext_goal[b]; e.hreplans[b] += 1u; }
                 }
-                if (i == 0) { e.hgoal[b] = pack(r, c); e.hreplans[b] += 1u; }
-                replan = true;
-                hp_new = hp;      // the new path starts at the current position
-            } else {
+            } else if (e.human_mode == 2) {
                 const int idx = e.hseq_idx[b] + 1;
                 const int len = e.hseq_len[b];
+                seq_idx = idx;
                 if (idx >= len) {
-                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];
-                    hp_new = path[0];
+                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];   // path kept, restarts at [0]
                 } else {
                     if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + idx];
-                    replan = true;
-                    hp_new = hp;
+                    cur2 = cur ^ 1;
+                    swapped = true;
                 }
                 if (i == 0) e.hseq_idx[b] = idx;
             }
+        }
+        const uint32_t *p2 = human_path(e, b, cur2);
+        const int L2 = e.hlen[b * 2 + cur2];
+        hp_new = p2[hs2];
+        const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
+        if (swapped) {
+            uint32_t ns, ng;
+            plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ng, i == 0);
             if (i == 0) {
-                e.hstep[b] = 0;
-                if (replan) {
+                e.hnext_start[b] = ns;
+                e.hnext_goal[b] = ng;
+                if (ng != NO_CELL) {
                     const uint32_t slot = atomicAdd(&e.counters[C_REPLAN_COUNT + parity], 1u);
                     e.replan_list[(size_t)parity * e.B + slot] = (uint32_t)b;
                 }
             }
-        } else {
-            hp_new = path[hs + 1];
-            if (i == 0) e.hstep[b] = hs + 1;
         }
-        if (i == 0) { e.hpos[b] = hp_new; e.clock[b] = clock + 1u; }
+        if (i == 0) {
+            e.hcur[b] = cur2;
+            e.hstep[b] = hs2;
+            e.hpos[b] = hp_new;
+            e.hnext[b] = hn_new;
+            e.clock[b] = clock + 1u;
+        }
     }
 
     // ---- outputs ------------------------------------------------------------

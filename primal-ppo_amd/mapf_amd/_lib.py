@@ -43,6 +43,7 @@ SIGNATURES = {
     "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_step_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_observe": (ctypes.c_int, [P, P, P, P]),
+    "mapf_flush": (ctypes.c_int, [P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),
     "mapf_get_counters": (ctypes.c_int, [P, P, P]),

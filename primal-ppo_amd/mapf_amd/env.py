@@ -166,6 +166,10 @@ class BatchedMapfGym:
         _lib.check(_lib.lib().mapf_observe(self.h, _ptr(obs), _ptr(vec), _stream(self.device)))
         return obs, vec
 
+    def flush(self):
+        """Run pending search work (BFS maps, next human paths) now, in its own launch."""
+        _lib.check(_lib.lib().mapf_flush(self.h, _stream(self.device)))
+
     def random_actions(self, out=None):
         out = self.actions if out is None else out
         _lib.check(_lib.lib().mapf_random_actions(self.h, _ptr(out), _stream(self.device)))
