@@ -68,7 +68,8 @@ def main():
     ap.add_argument("--channels", type=int, default=6)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--graph-steps", type=int, default=16, help="steps per captured hipGraph (0 = direct launches)")
+    ap.add_argument("--graph-steps", type=int, default=24,
+                    help="steps per captured hipGraph, a multiple of 3 (work-list slots rotate mod 3); 0 = direct")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,6 +104,7 @@ def main():
     # The K timed steps are replays of a hipGraph holding G consecutive steps
     # (every kernel of every step runs; the graph only removes host launch cost).
     G = args.graph_steps
+    assert G % 3 == 0, "--graph-steps must be a multiple of 3"
     K = args.steps
     graph = None
     if G > 0:

@@ -160,6 +160,11 @@ int mapf_bfs(mapf_env *env, int16_t *dist, void *stream);
 /* Counters of impossible states / clamped events (host uint32[16]); synchronises the stream. */
 int mapf_get_counters(mapf_env *env, uint32_t *host16, void *stream);
 
+/* Phase-cycle sums over the waves of the last step launch, recorded by the
+ * -DMAPF_STAMPS diagnostic build ([15] = waves; all zero in the product
+ * build): host uint64[16]; synchronises. */
+int mapf_get_profile(mapf_env *env, uint64_t *host16, int reset, void *stream);
+
 int mapf_get_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
 int mapf_set_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
 

@@ -47,8 +47,8 @@ struct mapf_env {
     mapf_config cfg;
     int device = 0;
     DevEnv d{};
-    int parity = 1;
-    int pending = -1;        // parity whose search work has not been launched yet
+    int parity = 1;          // work-list slot of the next step (step count mod 3)
+    int pending = -1;        // slot whose search work has not been launched yet
     bool ready = false;
     std::vector<void *> allocs;
     template <class T>
@@ -111,6 +111,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     if (const char *v = std::getenv("MAPF_SEARCH_BLOCKS")) { int x = std::atoi(v); if (x >= 1 && x <= 1024) d.search_blocks = x; }
     if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }
     if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
+    if (const char *v = std::getenv("MAPF_AGENT_LANES")) d.force_agent_lanes = std::atoi(v) != 0;
     if (d.obs_envs > d.B) d.obs_envs = d.B;
 
     // fp64 lookup tables, computed exactly like the reference (numpy sqrt / python pow)
@@ -143,8 +144,9 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(d.hreplans, d.B); rc |= e->alloc(d.clock, d.B);
     if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * d.H * d.W);
     rc |= e->alloc(d.counters, C_NUM);
-    rc |= e->alloc(d.replan_list, 2 * (size_t)d.B);
-    rc |= e->alloc(d.bfs_list, 2 * BN);
+    rc |= e->alloc(d.prof, 65536 * 8);
+    rc |= e->alloc(d.replan_list, 3 * (size_t)d.B);
+    rc |= e->alloc(d.bfs_list, 3 * BN);
     uint8_t *smask = nullptr;
     rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
@@ -160,7 +162,8 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.dist_lut = dl;
     if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dl, dist_lut.data(), dist_lut.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(d.counters, 0, C_NUM * sizeof(uint32_t)) != hipSuccess) {
+        hipMemset(d.counters, 0, C_NUM * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(d.prof, 0, 65536 * 8 * sizeof(unsigned long long)) != hipSuccess) {
         mapf_destroy(e);
         return fail(MAPF_EDEVICE, "initial upload failed");
     }
@@ -324,7 +327,7 @@ static int step_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, ui
     launch_step(e->d, actions, o, flags, parity, s);
     if (flags & MAPF_STEP_COMMIT) {
         if (e->d.human_mode != 0 || e->d.keep_bfs) e->pending = parity;
-        e->parity ^= 1;
+        e->parity = (parity + 1) % 3;
     }
     HIPCHK(hipGetLastError());
     return MAPF_OK;
@@ -399,6 +402,23 @@ int mapf_get_counters(mapf_env *e, uint32_t *host16, void *stream) {
     if (int rc = flush_search(e, s)) return rc;
     HIPCHK(hipMemcpyAsync(host16, e->d.counters, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    return MAPF_OK;
+}
+
+int mapf_get_profile(mapf_env *e, uint64_t *host16, int reset, void *stream) {
+    if (!e || !host16) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<uint64_t> all(65536 * 8);
+    HIPCHK(hipMemcpyAsync(all.data(), e->d.prof, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (reset) HIPCHK(hipMemsetAsync(e->d.prof, 0, all.size() * sizeof(uint64_t), s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int k = 0; k < 16; ++k) host16[k] = 0;
+    for (size_t w = 0; w < 65536; ++w) {   // sums over waves of the LAST launch; [15] = waves
+        if (!all[w * 8 + 7]) continue;
+        for (int k = 0; k < 7; ++k) host16[k] += all[w * 8 + k];
+        host16[15] += 1;
+    }
     return MAPF_OK;
 }
 

@@ -14,7 +14,7 @@
 //   hlen [B][2], hcur/hstep [B], hpos/hnext/hgoal/hentr [B], hnext_start/hnext_goal [B]
 //   bfs       [B*N*H*W] i16         agent.bfsMap (keep_bfs)
 //   counters  [32] u32              error counters + work-list counts
-//   replan_list [2][B], bfs_list [2][B*N]  per-step work lists (step parity)
+//   replan_list [3][B], bfs_list [3][B*N]  per-step work lists, slot = step count mod 3
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,8 +36,8 @@ enum : uint32_t { P_ENTRANCE = 1, P_HGOAL0 = 2, P_START = 3, P_GOAL0 = 4, P_GOAL
 // counters[] slots
 enum : int { C_BAD_ACTION = 0, C_FIX_BOUND = 1, C_EMPTY_VIABLE = 2, C_FREECELL = 3,
              C_UNREACHABLE = 4, C_BAD_STATUS = 5, C_PATH_OVERFLOW = 6,
-             C_REPLAN_COUNT = 8,   // [8],[9]  by step parity
-             C_BFS_COUNT = 10,     // [10],[11]
+             C_REPLAN_COUNT = 8,   // [8..10]  by work-list slot (step count mod 3)
+             C_BFS_COUNT = 12,     // [12..14]
              C_NUM = 32 };
 
 struct DevEnv {
@@ -50,6 +50,7 @@ struct DevEnv {
     int constr_d2;            // largest d2 with (R - sqrt(d2)) / R >= 0.01 in fp64 (mapf_gym.py:633)
     int obs_envs;             // envs per observe workgroup
     int step_block;           // threads per step workgroup (64..256)
+    int force_agent_lanes;    // use the agent-per-lane step kernel even for N <= 8 (testing)
     const uint32_t *map_bits;
     uint32_t *pos, *goal;
     int8_t *last_act;
@@ -65,6 +66,7 @@ struct DevEnv {
     uint32_t *hreplans, *clock;
     int16_t *bfs;
     uint32_t *counters, *replan_list, *bfs_list;
+    unsigned long long *prof;  // [65536][8] per-wave phase cycles of the MAPF_STAMPS diagnostic build
     const float *cost_lut;    // [R*R+1]: float32(max(R - sqrt(d2), 0) / R) (fp64 like the reference)
     const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
     const uint8_t *smask;     // [nmaps][H*W]: static-invalid action mask of each cell (getInvalidActions[0])
@@ -109,6 +111,29 @@ __device__ inline uint32_t *human_path(const DevEnv &e, int b, int buf) {
 }
 // Human.getNextPos (mapf_gym.py:46-50), maintained in hnext[b] by the step kernel.
 __device__ inline uint32_t human_next(const DevEnv &e, int b) { return e.hnext[b]; }
+
+// In-kernel phase stamps (diagnostic build only, -DMAPF_STAMPS): lane 0 of
+// every wave adds the s_memtime delta of each phase into prof[k]; prof[15]
+// counts the waves.  The product build compiles them out.
+__device__ inline uint64_t stamp_now() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#ifdef MAPF_STAMPS
+// per-wave phase deltas kept in registers, one plain store per phase at the end
+// (prof[wave * 8 + k]; no atomics, so the stamps do not contend)
+#define STAMP_BEGIN() uint64_t _stamp_prev = stamp_now(); uint64_t _stamp_d[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define STAMP(k) do { __builtin_amdgcn_sched_barrier(0); const uint64_t _t = stamp_now(); \
+    _stamp_d[k] += _t - _stamp_prev; _stamp_prev = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
+#define STAMP_END() do { if ((threadIdx.x & 63) == 0) { \
+    const size_t _w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; \
+    if (_w < 65536) { for (int _k = 0; _k < 7; ++_k) e.prof[_w * 8 + _k] = _stamp_d[_k]; e.prof[_w * 8 + 7] = 1; } } } while (0)
+#else
+#define STAMP_BEGIN() do { } while (0)
+#define STAMP(k) do { } while (0)
+#define STAMP_END() do { } while (0)
+#endif
 
 // Wave-level helpers ---------------------------------------------------------
 __device__ inline int lane_id() { return threadIdx.x & 63; }

@@ -18,6 +18,8 @@ struct StepOut {          // device pointers (mapf_step_out)
 
 // flags: bit0 commit (jointStep), bit1 random policy (draw actions in-kernel into `actions`)
 void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s);
+bool launch_step_pairs(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,
+                       hipStream_t s);   // N <= 8: one lane per agent pair; false if N > 8
 void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s);
 // humans' next paths (replan_list[parity]) + agent BFS maps (bfs_list[parity]);
 // all = 1: every env's next path and every agent's map, 2: every env's next path

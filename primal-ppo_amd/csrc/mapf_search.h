@@ -204,7 +204,7 @@ __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, ui
         uint32_t ai = 0, sr_cell, stop_cell = NO_CELL;
         int b;
         if (replan) {
-            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];
+            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];   // parity = list slot
             stop_cell = e.hnext_goal[b];
             if (stop_cell == NO_CELL) continue;
             sr_cell = e.hnext_start[b];

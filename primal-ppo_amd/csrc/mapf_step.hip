@@ -30,11 +30,12 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     const int G = e.G, N = e.N;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = gt / G;
-    if (gt == 0 && (flags & 1u)) {       // zero the other parity's work-list counts (consumed last step)
-        e.counters[C_REPLAN_COUNT + (parity ^ 1)] = 0;
-        e.counters[C_BFS_COUNT + (parity ^ 1)] = 0;
+    if (gt == 0 && (flags & 1u)) {       // zero the next step's work-list slot (consumed two steps ago)
+        e.counters[C_REPLAN_COUNT + (parity + 1) % 3] = 0;
+        e.counters[C_BFS_COUNT + (parity + 1) % 3] = 0;
     }
     if (b >= e.B) return;                 // whole group leaves together
+    STAMP_BEGIN();
     Group g(G);
     const int i = g.i;
     const bool act = i < N;
@@ -73,6 +74,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     }
     const unsigned rep_mask = la >= 0 ? 1u << opp(la) : 0u;
 
+    STAMP(0);
     // ---- getRestrictedActions (:363-402), evaluated against actual actions --
     const int Xr = pr + dr(a), Xc = pc + dc(a);
     unsigned keys = 0, conf = 0;   // conf: my actions t that collide with some j's actual action
@@ -96,6 +98,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     }
     const unsigned good = ~(st_mask | hu_mask | rep_mask | keys) & 0x1Fu;   // setdiff1d (:423)
 
+    STAMP(1);
     // ---- getActionStatus (:434-480) ----------------------------------------
     int s0;
     bool cb = false;
@@ -149,6 +152,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     if (i == 0 && out.shadow_goals) out.shadow_goals[b] = popc64(shadow_mask);
     if (!(flags & 1u)) return;
 
+    STAMP(2);
     // ---- jointStep: fixActions (:552-612) ----------------------------------
     int fixed = a;
     const uint64_t need = g.ballot(act && (st == -1 || st == -2 || st == -3));
@@ -212,6 +216,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
         fixed = assigned >= 0 ? assigned : 0;
     }
 
+    STAMP(3);
     // ---- takeStep (:158-161) + lifelong goals (:623-627) --------------------
     const int nr = pr + dr(fixed), nc = pc + dc(fixed);
     const uint32_t np = act ? pack(nr, nc) : 0xFFFFFFFFu;
@@ -258,6 +263,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
         }
     }
 
+    STAMP(4);
     // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94) -------------------
     // The path switched to at an end-step was searched one path ahead (search
     // kernel, buffer hcur ^ 1); here the human only advances, switches buffers
@@ -315,6 +321,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
         }
     }
 
+    STAMP(5);
     // ---- outputs ------------------------------------------------------------
     if (act) {
         const int d0 = prow(hp_new) - nr, d1 = pcol(hp_new) - nc;
@@ -324,6 +331,8 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
         if (out.constraints) out.constraints[ai] = cv;
         if (out.reward_total) out.reward_total[ai] = reached ? rw + e.goal_reward : rw;   // runner.py:89-91
     }
+    STAMP(6);
+    STAMP_END();
 }
 
 // Uniform random policy: counter (env, P_ACT | agent << 8, clock, 0).
@@ -336,6 +345,7 @@ __global__ __launch_bounds__(256) void random_actions_kernel(DevEnv e, int32_t *
 }
 
 void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s) {
+    if (!e.force_agent_lanes && launch_step_pairs(e, actions, out, flags, parity, s)) return;
     const long threads = (long)e.B * e.G;
     const int blk = e.step_block;
     const int grid = (int)((threads + blk - 1) / blk);

@@ -140,7 +140,11 @@ class BatchedMapfGym:
     # ----------------------------------------------------------------- step
     def step(self, actions=None, commit=True):
         """One lockstep step (runner.py:64-100 order).  actions: int32 [B, N] on device.
-        Returns the dict of output tensors (reused between calls)."""
+        Returns the dict of output tensors (reused between calls).
+
+        Graph capture: steps and observes may be captured into a hipGraph and
+        replayed, provided a captured sequence holds a multiple of 3 committed
+        steps (the device work lists rotate over 3 slots)."""
         if actions is None:
             actions = self.actions
         assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
@@ -183,6 +187,13 @@ class BatchedMapfGym:
     def counters(self):
         c = np.zeros(16, np.uint32)
         _lib.check(_lib.lib().mapf_get_counters(self.h, ctypes.c_void_p(c.ctypes.data), _stream(self.device)))
+        return c
+
+    def profile(self, reset=True):
+        """Phase-cycle sums of the MAPF_STAMPS diagnostic build (zeros otherwise)."""
+        c = np.zeros(16, np.uint64)
+        _lib.check(_lib.lib().mapf_get_profile(self.h, ctypes.c_void_p(c.ctypes.data), int(reset),
+                                               _stream(self.device)))
         return c
 
     def get_state(self):

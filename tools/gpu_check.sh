@@ -36,6 +36,9 @@ for s in $STEPS; do
         rc=$?; echo "sweep $cfg rc=$rc $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['breakdown_ms'])" "$OUT/sweep.log" 2>/dev/null)"
         stop_if_fatal $rc sweep
       done ;;
+    stamps)
+      timeout -k 10 200 python3 tools/stamps.py > "$OUT/stamps.log" 2>&1
+      rc=$?; echo "stamps rc=$rc"; cat "$OUT/stamps.log" | grep -v amdgpu.ids; stop_if_fatal $rc stamps ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 20 --no-cpu) > "$OUT/prof.log" 2>&1
