@@ -1,0 +1,199 @@
+"""Model: action sampling, value bootstrap and the PPO-Lagrangian update.
+
+Mirrors the reference's Model (model.py:13-231) and Lagrangian multipliers
+(lagrange.py:26-88), with the device-resident pieces of the hot path:
+  * step(): the policy forward + on-device categorical sampling (mapf_sample_actions
+    in place of np.random.choice, model.py:38-40);
+  * train(): advantage normalisation by the HIP kernel (mapf_normalize_advantages,
+    model.py:106-113) -- statistics over the GLOBAL minibatch when distributed --
+    then the reference's loss (:115-170), AMP GradScaler, and between backward and
+    unscale the RCCL all-reduce of the flattened gradient bucket (SURVEY.md §3.4:
+    the only exchange step of the path).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .config import EnvParameters, LagrangianParameters, NetParameters, TrainingParameters
+from .net import SCRIMPNet
+
+
+class Lagrangian:
+    """lagrange.py:26-53: softplus-parameterised multiplier trained by Adam."""
+
+    def __init__(self, cost_limit):
+        self.cost_limit = cost_limit
+        self.lagrangian_param = torch.tensor(max(0.0, LagrangianParameters.INIT_VALUE), requires_grad=True).float()
+        self.lagrangian_optimizer = torch.optim.Adam([self.lagrangian_param], lr=LagrangianParameters.LR)
+
+    def get_lagrangian_param(self):
+        return F.softplus(self.lagrangian_param).detach().item()
+
+    def update_lagrangian_multiplier(self, ep_cost_avg):
+        loss = -self.lagrangian_param * (ep_cost_avg - self.cost_limit)
+        self.lagrangian_optimizer.zero_grad()
+        loss.backward()
+        self.lagrangian_optimizer.step()
+        self.lagrangian_param.data.clamp_(0.0, LagrangianParameters.UPPER_BOUND)
+
+
+class PIDLagrangian:
+    """lagrange.py:55-88: PID-controlled multiplier (CPPO-PID)."""
+
+    def __init__(self, cost_limit):
+        self.cost_limit = cost_limit
+        self.i_term = max(0.0, LagrangianParameters.INIT_VALUE)
+        self.lagrangian_param = 0.0
+        self.delta_moving_avg = 0.0
+        self.cost_moving_avg = 0.0
+        self.cost_moving_avg_prev = 0.0
+
+    def get_lagrangian_param(self):
+        return self.lagrangian_param
+
+    def update_lagrangian_multiplier(self, ep_cost_avg):
+        P = LagrangianParameters
+        delta = ep_cost_avg - self.cost_limit
+        self.delta_moving_avg = self.delta_moving_avg * P.DELTA_MOVING_AVG_ALPHA + (1 - P.DELTA_MOVING_AVG_ALPHA) * delta
+        self.cost_moving_avg = self.cost_moving_avg * P.COST_MOVING_AVG_ALPHA + (1 - P.COST_MOVING_AVG_ALPHA) * ep_cost_avg
+        d_term = max(0.0, self.cost_moving_avg - self.cost_moving_avg_prev)
+        self.i_term = max(0.0, self.i_term + delta * P.KI)
+        self.lagrangian_param = max(0.0, P.KP * self.delta_moving_avg + self.i_term + P.KD * d_term)
+        self.cost_moving_avg_prev = self.cost_moving_avg
+
+
+def get_lagrangian(kind, cost_limit):
+    return Lagrangian(cost_limit) if kind == 0 else PIDLagrangian(cost_limit)
+
+
+def _normalize(x):
+    """model.py:106: (x - mean) / (std_unbiased + 1e-6); global statistics across ranks."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        s = torch.stack([x.sum(), (x * x).sum(), torch.tensor(float(x.numel()), device=x.device)]).double()
+        dist.all_reduce(s)
+        n = s[2]
+        mean = s[0] / n
+        var = (s[1] - n * mean * mean) / (n - 1)
+        return (x - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-6)
+    return (x - x.mean()) / (x.std() + 1e-6)
+
+
+class Model:
+    def __init__(self, env_id, device, global_model=False, numChannel=None, num_agents=None, fov=None):
+        self.ID = env_id
+        self.device = torch.device(device)
+        self.network = SCRIMPNet(numChannel=numChannel, num_agents=num_agents, fov=fov).to(self.device)
+        self.num_agents = num_agents or EnvParameters.N_AGENTS
+        self._flat = None
+        if global_model:
+            self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr)
+            self.lagrange = get_lagrangian(LagrangianParameters.LAGRANGIAN_TYPE, TrainingParameters.COST_LIMIT_PER_AGENT)
+            self.net_scaler = torch.amp.GradScaler(self.device.type, enabled=self.device.type == "cuda")
+
+    # ------------------------------------------------------------ acting
+    @torch.no_grad()
+    def step(self, observation, vector, input_state=None, seed=0, step=0, actions_out=None):
+        """model.py:26-41 on device: returns (actions int64, ps, v, block, output_state, cv) as tensors.
+        Sampling: inverse CDF with a Philox uniform (mapf_sample_actions)."""
+        ps, v, block, _, out_state, _, cv = self.network(observation, vector, input_state)
+        ps32 = ps.float().contiguous()
+        if self.device.type == "cuda":
+            from .env import sample_actions
+            a = actions_out if actions_out is not None else torch.empty(ps32.shape[:-1], dtype=torch.int64,
+                                                                         device=self.device)
+            sample_actions(ps32, seed, step, out64=a)
+        else:
+            a = torch.multinomial(ps32.reshape(-1, ps32.shape[-1]), 1).reshape(ps32.shape[:-1])
+        return a, ps32, v.float(), block.float(), out_state, cv.float()
+
+    @torch.no_grad()
+    def value(self, obs, vector, input_state=None):
+        """model.py:62-69."""
+        _, v, _, _, _, _, cv = self.network(obs, vector, input_state)
+        return v.float(), cv.float()
+
+    def set_weights(self, weights):
+        self.network.load_state_dict(weights)
+
+    # ------------------------------------------------------------ learning
+    def _allreduce_grads(self):
+        """One bucketed all-reduce (RCCL over xGMI) of every gradient, averaged over ranks."""
+        if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            return
+        params = [p for p in self.network.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        dist.all_reduce(flat)
+        flat.div_(dist.get_world_size())
+        off = 0
+        for p in params:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
+    def train(self, observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, input_state,
+              train_valid, episode_cost):
+        """model.py:78-199.  Inputs may be numpy arrays (reference contract) or device tensors."""
+        dev = self.device
+        t = lambda x: (torch.from_numpy(x) if isinstance(x, np.ndarray) else x).to(dev)
+        self.net_optimizer.zero_grad()
+        observation, vector = t(observation), t(vector)
+        returns, old_v, cost_returns, old_cv = t(returns).float(), t(old_v).float(), t(cost_returns).float(), t(old_cv).float()
+        action = t(action).long().unsqueeze(-1)
+        old_ps, train_valid = t(old_ps).float(), t(train_valid).float()
+
+        lam = self.lagrange.get_lagrangian_param()
+        distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if dev.type == "cuda" and not distributed:
+            from .env import normalize_advantages
+            advantage, cost_advantage = normalize_advantages(returns.contiguous(), old_v.contiguous(),
+                                                             cost_returns.contiguous(), old_cv.contiguous(),
+                                                             lagrange=lam, mix=TrainingParameters.MINUS_ADV_WITH_CADV)
+        else:
+            advantage = _normalize(returns - old_v)
+            cost_advantage = _normalize(cost_returns - old_cv)
+            if TrainingParameters.MINUS_ADV_WITH_CADV:
+                advantage = (advantage - lam * cost_advantage) / (lam + 1)
+
+        with torch.autocast(device_type=dev.type, enabled=dev.type == "cuda"):
+            new_ps, new_v, block, policy_sig, _, _, new_cv = self.network(observation, vector, input_state)
+            new_p = new_ps.gather(-1, action)
+            old_p = old_ps.gather(-1, action)
+            ratio = torch.exp(torch.log(torch.clamp(new_p, 1e-6, 1.0)) - torch.log(torch.clamp(old_p, 1e-6, 1.0)))
+            entropy = torch.mean(-torch.sum(new_ps * torch.log(torch.clamp(new_ps, 1e-6, 1.0)), dim=-1, keepdim=True))
+            clip = TrainingParameters.CLIP_RANGE
+            new_v = torch.squeeze(new_v)
+            v_clip = old_v + torch.clamp(new_v - old_v, -clip, clip)
+            critic_loss = torch.mean(torch.maximum(torch.square(new_v - returns), torch.square(v_clip - returns)))
+            new_cv = torch.squeeze(new_cv)
+            cv_clip = old_cv + torch.clamp(new_cv - old_cv, -clip, clip)
+            cost_critic_loss = torch.mean(torch.maximum(torch.square(new_cv - cost_returns),
+                                                        torch.square(cv_clip - cost_returns)))
+            ratio = torch.squeeze(ratio)
+            policy_loss = torch.mean(torch.min(advantage * ratio, advantage * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)))
+            valid_loss = -torch.mean(torch.log(torch.clamp(policy_sig, 1e-6, 1.0 - 1e-6)) * train_valid +
+                                     torch.log(torch.clamp(1 - policy_sig, 1e-6, 1.0 - 1e-6)) * (1 - train_valid))
+            cost_loss = torch.mean(ratio * cost_advantage)
+            all_loss = (-policy_loss - entropy * TrainingParameters.ENTROPY_COEF
+                        + TrainingParameters.VALUE_COEF * critic_loss + TrainingParameters.VALID_COEF * valid_loss
+                        + TrainingParameters.COST_VALUE_COEF * cost_critic_loss
+                        + TrainingParameters.COST_COEF * lam * cost_loss)
+        clip_frac = torch.mean(torch.greater(torch.abs(ratio - 1.0), clip).float())
+
+        self.net_scaler.scale(all_loss).backward()
+        self._allreduce_grads()
+        self.net_scaler.unscale_(self.net_optimizer)
+        if distributed:   # every rank must update the multiplier with the same episode cost
+            c = torch.tensor([float(episode_cost)], dtype=torch.float64, device=dev)
+            dist.all_reduce(c)
+            episode_cost = c.item() / dist.get_world_size()
+        self.lagrange.update_lagrangian_multiplier(episode_cost / EnvParameters.N_AGENTS)
+        grad_norm = torch.nn.utils.clip_grad_norm_(self.network.parameters(), TrainingParameters.MAX_GRAD_NORM)
+        self.net_scaler.step(self.net_optimizer)
+        self.net_scaler.update()
+        return [all_loss.detach().cpu().numpy(), policy_loss.detach().cpu().numpy(), entropy.detach().cpu().numpy(),
+                critic_loss.detach().cpu().numpy(), valid_loss.detach().cpu().numpy(),
+                cost_critic_loss.detach().cpu().numpy(), cost_loss.detach().cpu().numpy(),
+                clip_frac.detach().cpu().numpy(), grad_norm.detach().cpu().numpy(),
+                torch.mean(advantage).detach().cpu().numpy(), torch.mean(cost_advantage).detach().cpu().numpy(),
+                self.lagrange.get_lagrangian_param()]

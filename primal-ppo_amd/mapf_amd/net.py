@@ -1,0 +1,195 @@
+"""SCRIMPNet policy/value network, state_dict-compatible with the reference.
+
+Architecture and parameter names follow net.py:38-155 and transformer.py:1-100
+of the reference so that a reference checkpoint (`torch.save({"model": ...})`,
+driver.py:182-193) loads with `load_state_dict` unchanged:
+
+  obs [.., C, F, F] -> 3x conv3x3(128) -> maxpool -> 3x conv2x2(256) -> maxpool
+  -> conv3x3(500) -> flatten ++ fc(vector 4 -> 12) -> 512 -> residual MLP
+  -> 16-token tokeniser + cls token + positional embedding
+  -> 2 pre-norm transformer blocks (16 heads, MLP 512, GELU, dropout 0.2)
+  -> cls -> nn_same applied twice -> policy(5) / value / cost value / blocking
+
+The tokeniser keeps the reference's exact arithmetic: its einsum
+'bij,zjk->bik' SUMS over the 8 token matrices and its softmax runs over a
+length-1 axis, so every token equals the summed-V projection (kept literally).
+Runs under torch autocast like the reference (net.py:101).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .config import EnvParameters, NetParameters
+
+
+def _xavier_like(module):
+    """weights_init (net.py:18-35): uniform(+-sqrt(6/(fan_in+fan_out))), zero bias."""
+    name = module.__class__.__name__
+    if name.find("Conv") != -1:
+        shape = list(module.weight.data.size())
+        fan_in = np.prod(shape[1:4])
+        fan_out = np.prod(shape[2:4]) * shape[0]
+        bound = math.sqrt(6.0 / (fan_in + fan_out))
+        module.weight.data.uniform_(-bound, bound)
+        module.bias.data.fill_(0)
+    elif name.find("Linear") != -1:
+        fan_out, fan_in = module.weight.data.size()
+        bound = math.sqrt(6.0 / (fan_in + fan_out))
+        module.weight.data.uniform_(-bound, bound)
+        if module.bias is not None:
+            module.bias.data.fill_(0)
+
+
+class _PreNorm(nn.Module):
+    """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
+
+    def __init__(self, dim, fn):
+        super().__init__()
+        self.fn = nn.Module()
+        self.fn.norm = nn.LayerNorm(dim)
+        self.fn.fn = fn
+
+    def forward(self, x):
+        return self.fn.fn(self.fn.norm(x)) + x
+
+
+class _SelfAttention(nn.Module):
+    """transformer.py:48-85: fused qkv projection, softmax(q k^T / sqrt(dim)) v, output projection.
+    Note the reference scales by dim ** -0.5 (the model width), not the head width."""
+
+    def __init__(self, dim, heads, dropout):
+        super().__init__()
+        self.heads = heads
+        self.scale = dim ** -0.5
+        self.to_qkv = nn.Linear(dim, dim * 3, bias=True)
+        nn.init.xavier_uniform_(self.to_qkv.weight)
+        nn.init.zeros_(self.to_qkv.bias)
+        self.nn1 = nn.Linear(dim, dim)
+        nn.init.xavier_uniform_(self.nn1.weight)
+        nn.init.zeros_(self.nn1.bias)
+        self.do1 = nn.Dropout(dropout)
+
+    def forward(self, x):
+        b, n, d = x.shape
+        h = self.heads
+        qkv = self.to_qkv(x).view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        att = torch.matmul(q, k.transpose(-1, -2)) * self.scale
+        att = att.softmax(dim=-1)
+        out = torch.matmul(att, v).transpose(1, 2).reshape(b, n, d)
+        return self.do1(self.nn1(out))
+
+
+class _FeedForward(nn.Module):
+    """MLP_Block (transformer.py:27-45)."""
+
+    def __init__(self, dim, hidden, dropout):
+        super().__init__()
+        self.nn1 = nn.Linear(dim, hidden)
+        nn.init.xavier_uniform_(self.nn1.weight)
+        nn.init.normal_(self.nn1.bias, std=1e-6)
+        self.af1 = nn.GELU()
+        self.do1 = nn.Dropout(dropout)
+        self.nn2 = nn.Linear(hidden, dim)
+        nn.init.xavier_uniform_(self.nn2.weight)
+        nn.init.normal_(self.nn2.bias, std=1e-6)
+        self.do2 = nn.Dropout(dropout)
+
+    def forward(self, x):
+        return self.do2(self.nn2(self.do1(self.af1(self.nn1(x)))))
+
+
+class _Encoder(nn.Module):
+    def __init__(self, dim, depth, heads, mlp_dim, dropout):
+        super().__init__()
+        self.layers = nn.ModuleList([
+            nn.ModuleList([_PreNorm(dim, _SelfAttention(dim, heads, dropout)),
+                           _PreNorm(dim, _FeedForward(dim, mlp_dim, dropout))])
+            for _ in range(depth)])
+
+    def forward(self, x):
+        for att, ff in self.layers:
+            x = ff(att(x))
+        return x
+
+
+class SCRIMPNet(nn.Module):
+    def __init__(self, numChannel=None, num_agents=None, fov=None):
+        super().__init__()
+        W = NetParameters.NET_SIZE
+        self.L = 16
+        self.cT = W
+        self.num_channel = NetParameters.NUM_CHANNEL if numChannel is None else numChannel
+        self.num_agents = num_agents
+        self.fov = fov
+        self.conv1 = nn.Conv2d(self.num_channel, W // 4, 3, 1, 1)
+        self.conv1a = nn.Conv2d(W // 4, W // 4, 3, 1, 1)
+        self.conv1b = nn.Conv2d(W // 4, W // 4, 3, 1, 1)
+        self.pool1 = nn.MaxPool2d(2)
+        self.conv2 = nn.Conv2d(W // 4, W // 2, 2, 1, 1)
+        self.conv2a = nn.Conv2d(W // 2, W // 2, 2, 1, 1)
+        self.conv2b = nn.Conv2d(W // 2, W // 2, 2, 1, 1)
+        self.pool2 = nn.MaxPool2d(2)
+        self.conv3 = nn.Conv2d(W // 2, W - NetParameters.GOAL_REPR_SIZE, 3, 1, 0)
+        self.fully_connected_1 = nn.Linear(NetParameters.VECTOR_LEN, NetParameters.GOAL_REPR_SIZE)
+        self.fully_connected_2 = nn.Linear(W, W)
+        self.fully_connected_3 = nn.Linear(W, W)
+        self.token_wA = nn.Parameter(torch.empty(8, self.L, 512))
+        nn.init.xavier_uniform_(self.token_wA)
+        self.token_wV = nn.Parameter(torch.empty(8, 512, self.cT))
+        nn.init.xavier_uniform_(self.token_wV)
+        self.pos_embedding = nn.Parameter(torch.empty(1, self.L + 1, self.cT))
+        nn.init.normal_(self.pos_embedding, std=0.02)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, self.cT))
+        self.dropout = nn.Dropout(0.2)
+        self.transformer = _Encoder(self.cT, 2, 16, 512, 0.2)
+        self.nn_same = nn.Linear(self.cT, self.cT)
+        nn.init.xavier_uniform_(self.nn_same.weight)
+        nn.init.normal_(self.nn_same.bias, std=1e-6)
+        self.policy_layer = nn.Linear(W, EnvParameters.N_ACTIONS)
+        self.value_layer = nn.Linear(W, 1)
+        self.cost_value_layer = nn.Linear(W, 1)
+        self.blocking_layer = nn.Linear(W, 1)
+        self.apply(_xavier_like)
+
+    def forward(self, obs, vector, input_state=None):
+        """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
+        obs: [..., N, C, F, F] (any leading shape); the agent axis is num_agents (EnvParameters.N_AGENTS
+        when not given at construction)."""
+        with torch.autocast(device_type=obs.device.type, enabled=obs.device.type == "cuda"):
+            n_agents = self.num_agents or EnvParameters.N_AGENTS
+            F_ = self.fov or obs.shape[-1]
+            x = obs.reshape(-1, self.num_channel, F_, F_)
+            v = vector.reshape(-1, NetParameters.VECTOR_LEN)
+            x = F.relu(self.conv1(x))
+            x = F.relu(self.conv1a(x))
+            x = F.relu(self.conv1b(x))
+            x = self.pool1(x)
+            x = F.relu(self.conv2(x))
+            x = F.relu(self.conv2a(x))
+            x = F.relu(self.conv2b(x))
+            x = self.pool2(x)
+            x = F.relu(self.conv3(x).flatten(1))
+            g = F.relu(self.fully_connected_1(v))
+            x3 = torch.cat((x, g), -1)
+            h = self.fully_connected_3(F.relu(self.fully_connected_2(x3)))
+            h = F.relu(h + x3).unsqueeze(1)                                   # [b, 1, 512]
+            # tokeniser (net.py:124-130): sums over the 8 token matrices, softmax over a length-1 axis
+            A = torch.matmul(h, self.token_wA.sum(0).transpose(0, 1))         # [b, 1, 16]
+            A = A.transpose(1, 2).softmax(dim=-1)                             # [b, 16, 1]
+            VV = torch.matmul(h, self.token_wV.sum(0))                        # [b, 1, 512]
+            T = torch.matmul(A, VV)                                           # [b, 16, 512]
+            x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
+            x = self.transformer(self.dropout(x))
+            x = self.nn_same(self.nn_same(x[:, 0]))
+            x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
+            logits = self.policy_layer(x)
+            policy = logits.softmax(dim=-1)
+            policy_sig = torch.sigmoid(logits)
+            value = self.value_layer(x)
+            cost_value = self.cost_value_layer(x)
+            blocking = torch.sigmoid(self.blocking_layer(x))
+        return policy, value, blocking, policy_sig, x, logits, cost_value

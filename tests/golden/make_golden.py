@@ -381,9 +381,72 @@ def g4_gae():
     print("g4_gae:", {k: np.asarray(v).shape for k, v in out.items() if hasattr(v, 'shape')})
 
 
+def det_weights(state_dict):
+    """Deterministic parameter values from the key names (shared with tests/test_net.py)."""
+    import zlib
+    out = {}
+    for k, v in state_dict.items():
+        n = v.numel()
+        phase = (zlib.crc32(k.encode()) % 1000) / 1000.0
+        x = np.sin(np.arange(n, dtype=np.float64) * 0.37 + phase * 6.283) * 0.05
+        out[k] = x.reshape(tuple(v.shape)).astype(np.float32)
+    return out
+
+
+def g5_net():
+    """SCRIMPNet forward (net.py:101-155) and Model.train (model.py:78-199) on CPU,
+    deterministic weights, dropout disabled (eval mode)."""
+    set_params(2, 9)
+    import torch
+    import net as net_mod
+    import model as model_mod
+    torch.manual_seed(0)
+    ref = net_mod.SCRIMPNet(numChannel=6)
+    sd = ref.state_dict()
+    keys = sorted(sd.keys())
+    w = det_weights(sd)
+    ref.load_state_dict({k: torch.from_numpy(w[k]) for k in sd})
+    ref.eval()
+    g = np.random.default_rng(9)
+    obs = (g.random((3, 2, 6, 9, 9)) < 0.2).astype(np.float32)
+    vec = g.normal(size=(3, 2, 4)).astype(np.float32)
+    with torch.no_grad():
+        outs = ref(torch.from_numpy(obs), torch.from_numpy(vec), None)
+    names = ["policy", "value", "blocking", "policy_sig", "x", "logits", "cost_value"]
+    out = {f"out_{n}": o.numpy() for n, o in zip(names, outs)}
+    out.update(obs=obs, vec=vec, keys=np.array(keys), shapes=np.array(json.dumps([list(sd[k].shape) for k in keys])))
+    # one PPO-Lagrangian update on a fixed minibatch
+    m = model_mod.Model(0, torch.device("cpu"), global_model=True, numChannel=6)
+    m.network.load_state_dict({k: torch.from_numpy(w[k]) for k in sd})
+    m.network.eval()
+    mb = 16
+    tr = dict(observation=(g.random((mb, 2, 6, 9, 9)) < 0.2).astype(np.float32),
+              vector=g.normal(size=(mb, 2, 4)).astype(np.float32),
+              returns=g.normal(size=(mb, 2)).astype(np.float32), cost_returns=g.random((mb, 2)).astype(np.float32),
+              old_v=g.normal(size=(mb, 2)).astype(np.float32), old_cv=g.random((mb, 2)).astype(np.float32),
+              action=g.integers(0, 5, (mb, 2)).astype(np.int64),
+              train_valid=(g.random((mb, 2, 5)) < 0.7).astype(np.float32))
+    ps = g.random((mb, 2, 5)).astype(np.float32)
+    tr["old_ps"] = ps / ps.sum(-1, keepdims=True)
+    hidden = np.zeros((mb, 2, 2, 512), np.float32)
+    stats = m.train(tr["observation"], tr["vector"], tr["returns"], tr["cost_returns"], tr["old_v"], tr["old_cv"],
+                    tr["action"], tr["old_ps"], hidden, tr["train_valid"], 3.0)
+    after = m.network.state_dict()
+    probe = ["conv1.weight", "fully_connected_2.bias", "transformer.layers.1.0.fn.fn.to_qkv.weight", "policy_layer.weight"]
+    out.update({f"train_{k}": v for k, v in tr.items()})
+    out["train_stats"] = np.array([float(np.asarray(x)) for x in stats])
+    for k in probe:
+        out["after_" + k.replace(".", "_")] = after[k].numpy().reshape(-1)[:2048]
+    np.savez_compressed(os.path.join(OUT, "g5_net.npz"), **out)
+    print("g5_net: stats", out["train_stats"])
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["g4"]:
         g4_gae()
+        sys.exit(0)
+    if sys.argv[1:] == ["g5"]:
+        g5_net()
         sys.exit(0)
     run_episode("g1_c1", warehouse(10, 10), 4, 11, 6, 200, 11)
     run_episode("g1_c2", warehouse(20, 20), 8, 11, 6, 200, 12)
