@@ -96,10 +96,11 @@ class DeviceRunner:
             self.shadow[t].copy_(out["shadow_goals"])
             env.observe(self.obs[t + 1], self.vec[t + 1])
         last_v, last_cv = self.model.value(self.obs[T], self.vec[T], None)
-        self.adv, self.returns = gae(self.rewards, self.values, last_v.reshape(self.values[0].shape).contiguous(),
+        self.last_v = last_v.reshape(self.values[0].shape).contiguous()
+        self.last_cv = last_cv.reshape(self.values[0].shape).contiguous()
+        self.adv, self.returns = gae(self.rewards, self.values, self.last_v,
                                      TrainingParameters.GAMMA, TrainingParameters.LAM)
-        self.cost_adv, self.cost_returns = gae(self.cost_rewards, self.cost_values,
-                                               last_cv.reshape(self.values[0].shape).contiguous(),
+        self.cost_adv, self.cost_returns = gae(self.cost_rewards, self.cost_values, self.last_cv,
                                                TrainingParameters.GAMMA, TrainingParameters.LAM)
         self.rollouts += 1
         return self.batch(), self.performance()

@@ -56,7 +56,8 @@ def test_device_runner_contract_and_gae():
     # GAE == oracle GAE on the same buffers, bit-exact
     r = runner.rewards.reshape(T, -1).cpu().numpy()
     v = runner.values.reshape(T, -1).cpu().numpy()
-    lv, lcv = model.value(runner.obs[T], runner.vec[T])
+    # (the net keeps dropout active during rollouts, net.py:50-51 / model.py:26 -- use the runner's own bootstrap)
+    lv, lcv = runner.last_v, runner.last_cv
     adv, ret = O.gae(r, v, lv.reshape(-1).cpu().numpy())
     np.testing.assert_array_equal(runner.returns.reshape(T, -1).cpu().numpy(), ret)
     cr = runner.cost_rewards.reshape(T, -1).cpu().numpy()
@@ -69,7 +70,8 @@ def test_device_runner_contract_and_gae():
     stats = model.train(mb["observations"][rows], mb["vectors"][rows], mb["returns"][rows], mb["costReturns"][rows],
                         mb["values"][rows], mb["costValues"][rows], mb["actions"][rows], mb["ps"][rows], None,
                         mb["trainValid"][rows], float(perf.episodeCostReward) / B)
-    assert all(np.isfinite(float(np.asarray(s))) for s in stats)
+    # losses finite (grad_norm, stats[8], may be inf on the first AMP steps: GradScaler then skips the step)
+    assert all(np.isfinite(float(np.asarray(s))) for k, s in enumerate(stats) if k != 8)
 
 
 def test_env_shards_draw_like_one_device():

@@ -25,7 +25,7 @@ for s in $STEPS; do
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; stop_if_fatal $rc smoke ;;
     pytest)
-      timeout -k 10 1000 python3 -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+      timeout -k 10 1000 python3 -m pytest ${PYTEST_ARGS:-tests} -m gpu -q > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"; stop_if_fatal $rc pytest ;;
     bench)
       timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
