@@ -56,6 +56,19 @@ def cpu_baseline(H, W, N, F, C, seconds):
                       f"agent-steps/s/core on this shape (BASELINE.md)"}
 
 
+PMC_REPORT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_observe_c2.json")
+
+
+def pmc_traffic(B, N, H, W, F, C):
+    """HBM bytes per observe launch from the committed rocprofv3 --pmc passes
+    (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py; collected by
+    `STEPS=pmc tools/gpu_check.sh`), for the c2 workload only -- null otherwise."""
+    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or not os.path.exists(PMC_REPORT):
+        return None
+    with open(PMC_REPORT) as f:
+        return round(json.load(f)["traffic_bytes"] / 1e6, 3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,7 +189,9 @@ def main():
                                        f"from hipGraph replays of {G} steps where search rides in the observe launch"},
             "roofline": {"kernel": "observe_kernel", "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_agent": bpa, "agents_per_launch": B * N},
+                         "traffic": pmc_traffic(B, N, H, W, F, C), "traffic_unit": "MB/launch (PMC)",
+                         "algorithmic_mb": round(bpa * B * N / 1e6, 3), "bytes_per_agent": bpa,
+                         "agents_per_launch": B * N},
             "device_counters": [int(x) for x in counters[:8]],
         }
         if world_size == 1 and not args.no_cpu:

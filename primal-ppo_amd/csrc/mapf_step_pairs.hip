@@ -76,8 +76,13 @@ __global__ __launch_bounds__(256) void step_pairs_kernel(DevEnv e, int32_t *__re
     const bool head = j == 0;               // lane that writes agent i's outputs
     const size_t ai = (size_t)b * N + i, aj = (size_t)b * N + j;
     const uint32_t env_id = e.env_offset + (uint32_t)b;
+    // ---- every per-env / per-agent load is issued here, in two dependent rounds
     const uint32_t clock = e.clock[b];
     const uint32_t hp = e.hpos[b], hn = e.hnext[b];
+    const int hs = e.hstep[b], hcur = e.hcur[b];
+    const int2 hlen2 = *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
+    const uint32_t hng = e.human_mode == 1 ? e.hnext_goal[b] : NO_CELL;
+    const int hsi = e.human_mode == 2 ? e.hseq_idx[b] : 0, hsl = e.human_mode == 2 ? e.hseq_len[b] : 0;
 
     const uint32_t pi = vi ? e.pos[ai] : 0u, pj = vj ? e.pos[aj] : 0u;
     const int ri = prow(pi), ci = pcol(pi), rj = prow(pj), cj = pcol(pj);
@@ -99,6 +104,23 @@ __global__ __launch_bounds__(256) void step_pairs_kernel(DevEnv e, int32_t *__re
         if (a_i < 0 || a_i >= NA) a_i = 0;
         if (a_j < 0 || a_j >= NA) a_j = 0;
     }
+    // human.nextStep does not depend on the agents: decide it now, issue its path loads in round 2
+    const int Lc = hcur ? hlen2.y : hlen2.x;
+    int cur2 = hcur, hs2 = hs + 1, seq_idx = 0;
+    bool swapped = false, at_end = hs >= Lc - 1;
+    if (at_end) {
+        hs2 = 0;
+        if (e.human_mode == 1) {
+            if (hng != NO_CELL) { cur2 = hcur ^ 1; swapped = true; }
+        } else if (e.human_mode == 2) {
+            seq_idx = hsi + 1;
+            if (seq_idx < hsl) { cur2 = hcur ^ 1; swapped = true; }
+        }
+    }
+    const int L2 = cur2 ? hlen2.y : hlen2.x;
+    const uint32_t *p2 = human_path(e, b, cur2);
+    const uint32_t hp_new = p2[hs2];
+    const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
     const unsigned st_mask = vi ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + ri * e.W + ci] : 0x1Fu;
     unsigned hu_mask = 0;
 #pragma unroll
@@ -155,10 +177,10 @@ __global__ __launch_bounds__(256) void step_pairs_kernel(DevEnv e, int32_t *__re
     const int Xr = ri + dr(a_i), Xc = ci + dc(a_i);
     const uint32_t shadow = agents_of(eballot(head && vi && st == 1 && Xr == prow(gi) && Xc == pcol(gi)));
     float cost = 0.f;
-    {
+    {   // max(R - ||h - x||, 0) / R in float64, then float32 (mapf_gym.py:513-526)
         const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
         const int d2 = d0 * d0 + d1 * d1;
-        if (d2 <= e.R * e.R) cost = e.cost_lut[d2];
+        if (d2 < e.R * e.R) cost = (float)(((double)e.R - sqrt((double)d2)) / (double)e.R);
     }
     if (vi) {
         if (head) {
@@ -289,58 +311,35 @@ __global__ __launch_bounds__(256) void step_pairs_kernel(DevEnv e, int32_t *__re
     }
     STAMP(4);
 
-    // ---- human.nextStep (see step_kernel)
-    uint32_t hp_new;
-    {
-        const int hs = e.hstep[b], cur = e.hcur[b];
-        const int Lc = e.hlen[b * 2 + cur];
-        int cur2 = cur, hs2 = hs + 1, seq_idx = 0;
-        bool swapped = false;
-        if (hs >= Lc - 1) {
-            hs2 = 0;
-            if (e.human_mode == 1) {
-                if (e.hnext_goal[b] != NO_CELL) {
-                    cur2 = cur ^ 1;
-                    swapped = true;
-                    if (li == 0) { e.hgoal[b] = e.hnext_goal[b]; e.hreplans[b] += 1u; }
-                }
-            } else if (e.human_mode == 2) {
-                const int idx = e.hseq_idx[b] + 1;
-                const int len = e.hseq_len[b];
-                seq_idx = idx;
-                if (idx >= len) {
-                    if (li == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];
-                } else {
-                    if (li == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + idx];
-                    cur2 = cur ^ 1;
-                    swapped = true;
-                }
-                if (li == 0) e.hseq_idx[b] = idx;
-            }
-        }
-        const uint32_t *p2 = human_path(e, b, cur2);
-        const int L2 = e.hlen[b * 2 + cur2];
-        hp_new = p2[hs2];
-        const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
-        if (swapped) {
-            uint32_t ns, ngl;
-            plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0);
+    // ---- human.nextStep (see step_kernel): side effects of the advance decided above
+    if (at_end) {
+        if (e.human_mode == 1) {
+            if (swapped && li == 0) { e.hgoal[b] = hng; e.hreplans[b] += 1u; }
+        } else if (e.human_mode == 2) {
             if (li == 0) {
-                e.hnext_start[b] = ns;
-                e.hnext_goal[b] = ngl;
-                if (ngl != NO_CELL) {
-                    const uint32_t sl = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], 1u);
-                    e.replan_list[(size_t)slot * e.B + sl] = (uint32_t)b;
-                }
+                e.hgoal[b] = e.hseq[(size_t)b * e.HS + (seq_idx < hsl ? seq_idx : hsl - 1)];
+                e.hseq_idx[b] = seq_idx;
             }
         }
+    }
+    if (swapped) {
+        uint32_t ns, ngl;
+        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0);
         if (li == 0) {
-            e.hcur[b] = cur2;
-            e.hstep[b] = hs2;
-            e.hpos[b] = hp_new;
-            e.hnext[b] = hn_new;
-            e.clock[b] = clock + 1u;
+            e.hnext_start[b] = ns;
+            e.hnext_goal[b] = ngl;
+            if (ngl != NO_CELL) {
+                const uint32_t sl = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], 1u);
+                e.replan_list[(size_t)slot * e.B + sl] = (uint32_t)b;
+            }
         }
+    }
+    if (li == 0) {
+        e.hcur[b] = cur2;
+        e.hstep[b] = hs2;
+        e.hpos[b] = hp_new;
+        e.hnext[b] = hn_new;
+        e.clock[b] = clock + 1u;
     }
     STAMP(5);
 

@@ -1,0 +1,91 @@
+"""Secondary benchmark: BASELINE configs c3 (policy-in-the-loop rollout) and c4
+(PPO update with the RCCL gradient all-reduce).  Not the headline metric
+(bench.py); prints one JSON line per measured phase on rank 0.
+
+  python tools/bench_rollout.py --envs 4096 --agents 8 --size 20 --steps 16
+  torchrun --nproc-per-node 8 tools/bench_rollout.py --envs 1024 --agents 16 --size 40 --train
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd")]
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--size", type=int, default=20)
+    ap.add_argument("--fov", type=int, default=9)
+    ap.add_argument("--steps", type=int, default=16, help="rollout length T")
+    ap.add_argument("--train", action="store_true", help="also time PPO minibatch updates")
+    ap.add_argument("--minibatch", type=int, default=256, help="rows per PPO minibatch (x N agents)")
+    ap.add_argument("--updates", type=int, default=10)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from mapf_amd.config import EnvParameters, make_config
+    from mapf_amd.env import BatchedMapfGym
+    from mapf_amd.maps import generate_warehouse
+    from mapf_amd.model import Model
+    from mapf_amd.runner import DeviceRunner
+    B, N, H, F = args.envs, args.agents, args.size, args.fov
+    EnvParameters.N_AGENTS = N
+    EnvParameters.FOV_SIZE = F
+    env = BatchedMapfGym(make_config(B, H, H, num_agents=N, fov=F, num_channel=6, human_mode="random",
+                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B), device=dev)
+    env.reset_seeded(generate_warehouse(H, H))
+    model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=F)
+    if world > 1:
+        for p in model.network.parameters():
+            torch.distributed.broadcast(p.data, 0)
+    runner = DeviceRunner(env, model, n_steps=args.steps, seed=rank)
+    runner.run()                       # warm-up (kernels, autotuning)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mb, perf = runner.run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"phase": "rollout (policy forward + sampling + env.step + observe + GAE)", "n_gpus": world,
+           "agent_steps_per_s": round(world * B * N * args.steps / dt, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "config": {"envs_per_gpu": B, "agents": N, "grid": H, "fov": F, "T": args.steps}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if args.train:
+        rows = args.minibatch
+        idx = torch.arange(rows, device=dev)
+        sl = lambda k: mb[k][idx]
+        def upd():
+            return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
+                               sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
+        upd()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.updates):
+            upd()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if rank == 0:
+            print(json.dumps({"phase": "PPO minibatch update (fwd+bwd+RCCL all-reduce+Adam)", "n_gpus": world,
+                              "ms_per_update": round(dt / args.updates * 1e3, 3),
+                              "rows_per_update_per_gpu": rows, "agents": N,
+                              "grad_bytes_allreduced": 4 * sum(p.numel() for p in model.network.parameters())}),
+                  flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -39,6 +39,16 @@ for s in $STEPS; do
     stamps)
       timeout -k 10 200 python3 tools/stamps.py > "$OUT/stamps.log" 2>&1
       rc=$?; echo "stamps rc=$rc"; cat "$OUT/stamps.log" | grep -v amdgpu.ids; stop_if_fatal $rc stamps ;;
+    rollout)
+      timeout -k 10 600 python3 tools/bench_rollout.py --train ${ROLLOUT_ARGS:-} > "$OUT/rollout.log" 2>&1
+      rc=$?; echo "rollout rc=$rc"; grep phase "$OUT/rollout.log"; tail -2 "$OUT/rollout.log"; stop_if_fatal $rc rollout ;;
+    pmc)
+      for ctr in WRITE_SIZE FETCH_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
+          -d "$OUT/pmc_$ctr" -o run -- python3 "$ROOT/bench.py" --steps 60 --warmup 10 --no-cpu --graph-steps 0) > "$OUT/pmc_$ctr.log" 2>&1
+        rc=$?; echo "pmc $ctr rc=$rc"; stop_if_fatal $rc pmc
+      done
+      find "$OUT" -path "*pmc_*" -name "*.csv" | head ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 20 --no-cpu) > "$OUT/prof.log" 2>&1
