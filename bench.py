@@ -1,9 +1,11 @@
 """Benchmark: lockstep agent-steps/sec for (env.step + observe), BASELINE.json's metric.
 
 A "step" = one lockstep step of every env on the GPU: the random policy's
-actions (Philox, on device) -> mapf_step (getActionStatus ... jointStep,
-human replans, BFS maps on goal changes) -> mapf_observe (all agents' FOV
-observations + vectors), i.e. runner.py:64-100 with a random policy.
+actions (Philox, on device) -> getActionStatus ... jointStep (human replans,
+BFS maps on goal changes) -> getAllObservations (all agents' FOV observations
++ vectors), i.e. runner.py:64-100 with a random policy, issued as ONE
+mapf_step_observe_random launch per step (--split: mapf_step_random +
+mapf_observe, two launches, same results).
 
 Default workload (N=1): BASELINE config c2 -- 4096 envs x 8 agents, 20x20
 generalised warehouse, FOV 11, 6 channels, Human with random goals,
@@ -36,6 +38,15 @@ def observe_bytes_per_agent(C, F, H, W, N):
     return C * F * F * 4 + 16 + (-(-H * W // 8) + 8 * N + 8) / N
 
 
+def fused_bytes_per_agent(C, F, H, W, N):
+    """Algorithmic HBM bytes per agent of one step_observe launch:
+    obs + vec writes (C*F^2*4 + 16); agent state read (cell, goal, last action: 9)
+    and written (9); random action (4) and step outputs (status 1, reward 4, cost 4,
+    train_valid 20, fixed 4, goal flag 4, constraint 4, total reward 4: 45);
+    per env: obstacle bits ceil(H*W/8) + clock/human/path state 64."""
+    return C * F * F * 4 + 16 + 9 + 9 + 4 + 45 + (-(-H * W // 8) + 64) / N
+
+
 def cpu_baseline(H, W, N, F, C, seconds):
     """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host, one thread."""
     from oracle import oracle as O
@@ -56,16 +67,18 @@ def cpu_baseline(H, W, N, F, C, seconds):
                       f"agent-steps/s/core on this shape (BASELINE.md)"}
 
 
-PMC_REPORT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_observe_c2.json")
+PMC_REPORTS = {"observe_kernel": os.path.join(ROOT, "profiles", "r01_pmc_observe_c2.json"),
+               "step_observe_kernel": os.path.join(ROOT, "profiles", "r01_pmc_step_observe_c2.json")}
 
 
-def pmc_traffic(B, N, H, W, F, C):
-    """HBM bytes per observe launch from the committed rocprofv3 --pmc passes
+def pmc_traffic(B, N, H, W, F, C, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
     (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py; collected by
     `STEPS=pmc tools/gpu_check.sh`), for the c2 workload only -- null otherwise."""
-    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or not os.path.exists(PMC_REPORT):
+    path = PMC_REPORTS.get(kernel)
+    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or path is None or not os.path.exists(path):
         return None
-    with open(PMC_REPORT) as f:
+    with open(path) as f:
         return round(json.load(f)["traffic_bytes"] / 1e6, 3)
 
 
@@ -81,6 +94,7 @@ def main():
     ap.add_argument("--channels", type=int, default=6)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--split", action="store_true", help="step and observe as two launches")
     ap.add_argument("--graph-steps", type=int, default=24,
                     help="steps per captured hipGraph, a multiple of 3 (work-list slots rotate mod 3); 0 = direct")
     args = ap.parse_args()
@@ -107,8 +121,11 @@ def main():
     obs, vec, acts = env.obs, env.vec, env.actions
 
     def one_step():
-        env.step_random(acts)        # random policy's actions drawn in the step kernel
-        env.observe(obs, vec)
+        if args.split:
+            env.step_random(acts)    # random policy's actions drawn in the step kernel
+            env.observe(obs, vec)
+        else:
+            env.step_observe(acts, obs, vec, random_policy=True)
 
     for _ in range(args.warmup):
         one_step()
@@ -147,14 +164,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # Per-kernel timing: HIP events around each launch on the launch stream,
-    # direct (non-graph) launches of the same steps.
-    # The search work (BFS maps, next human paths) is flushed in its own launch
-    # here so that the observe kernel is timed alone (the roofline kernel).
-    KT = min(K, 400)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KT)]
+    # Per-kernel timing: HIP events around each launch on the launch stream
+    # (torch's current stream, which the env launches on), direct launches.
+    # (a) the product path: one step_observe launch per step, the previous
+    #     step's search riding in it -- the roofline kernel;
+    # (b) the split path for the breakdown: step / search flushed alone / observe.
+    KT = min(K, 300)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(KT)]
     for k in range(KT):
-        e0, e1, e2, e3 = ev[k]
+        ev[k][0].record()
+        env.step_observe(acts, obs, vec, random_policy=True)
+        ev[k][1].record()
+    env.flush()
+    for k in range(KT):
+        e0, e1, e2, e3 = ev[k][2:]
         e0.record()
         env.step_random(acts)
         e1.record()
@@ -163,16 +186,20 @@ def main():
         env.observe(obs, vec)
         e3.record()
     torch.cuda.synchronize()
-    step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KT)]))
-    search_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(KT)]))
-    obs_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KT)]))
+    fused_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KT)]))
+    step_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KT)]))
+    search_ms = float(np.mean([ev[k][3].elapsed_time(ev[k][4]) for k in range(KT)]))
+    obs_ms = float(np.mean([ev[k][4].elapsed_time(ev[k][5]) for k in range(KT)]))
     counters = env.counters()
 
     if rank == 0:
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
-        bpa = observe_bytes_per_agent(C, F, H, W, N)
-        achieved = bpa * B * N / (obs_ms * 1e-3) / 1e9
+        if args.split:
+            kname, bpa, kms = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms
+        else:
+            kname, bpa, kms = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms
+        achieved = bpa * B * N / (kms * 1e-3) / 1e9
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -183,13 +210,15 @@ def main():
                        "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
                        "parallelism": f"env-shards x{world_size}"},
-            "breakdown_ms": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
-                             "observe_kernel": round(obs_ms, 4),
-                             "timing": f"HIP events around {KT} direct launches (search flushed alone); value "
-                                       f"from hipGraph replays of {G} steps where search rides in the observe launch"},
-            "roofline": {"kernel": "observe_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+            "breakdown_ms": {"step_observe_kernel": round(fused_ms, 4),
+                             "split": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
+                                       "observe_kernel": round(obs_ms, 4)},
+                             "timing": f"HIP events around {KT} direct launches of each path (split: search "
+                                       f"flushed alone); value from hipGraph replays of {G} steps"
+                                       f" ({'split' if args.split else 'fused'} path)"},
+            "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(B, N, H, W, F, C), "traffic_unit": "MB/launch (PMC)",
+                         "traffic": pmc_traffic(B, N, H, W, F, C, kname), "traffic_unit": "MB/launch (PMC)",
                          "algorithmic_mb": round(bpa * B * N / 1e6, 3), "bytes_per_agent": bpa,
                          "agents_per_launch": B * N},
             "device_counters": [int(x) for x in counters[:8]],

@@ -13,6 +13,7 @@
  *   calculateCostReward(a)          mapf_gym.py:528-533             -> mapf_step (cost)
  *   getTrainValid(a)                mapf_gym.py:535-550             -> mapf_step (train_valid)
  *   jointStep(a, st)                mapf_gym.py:614-637             -> mapf_step (MAPF_STEP_COMMIT)
+ *   jointStep + getAllObservations  runner.py:84-97                 -> mapf_step_observe (one launch)
  *   agent.bfsMap / makeBfsMap       mapf_gym.py:211-244             -> mapf_bfs
  *   Runner.run GAE                  runner.py:117-149               -> mapf_gae
  *   Model.train normalisation       model.py:106-113                -> mapf_normalize_advantages
@@ -146,6 +147,19 @@ int mapf_step_random(mapf_env *env, int32_t *actions_out, const mapf_step_out *o
 /* getAllObservations for all envs: obs DEVICE float [B][N][C][F][F], vec [B][N][4]. */
 int mapf_observe(mapf_env *env, float *obs, float *vec, void *stream);
 
+/* jointStep + getAllObservations in ONE launch (runner.py:84-97 calls them back
+ * to back): the committed step of mapf_step followed by mapf_observe, identical
+ * outputs.  Each workgroup steps its envs and observes them from LDS; the
+ * previous step's search work rides in the same launch (its results are next
+ * needed two steps later).  Configurations the fused kernel does not cover
+ * (N > 8, scripted humans, the BFS channel, very large maps) run the two
+ * launches.  mapf_step_observe_random draws the random policy like
+ * mapf_step_random. */
+int mapf_step_observe(mapf_env *env, const int32_t *actions, const mapf_step_out *out, float *obs, float *vec,
+                      void *stream);
+int mapf_step_observe_random(mapf_env *env, int32_t *actions_out, const mapf_step_out *out, float *obs,
+                             float *vec, void *stream);
+
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the
  * humans' next paths) on its own; mapf_observe otherwise runs it inside the
  * observation launch.  Any later call that needs it flushes implicitly. */
@@ -164,6 +178,9 @@ int mapf_get_counters(mapf_env *env, uint32_t *host16, void *stream);
  * -DMAPF_STAMPS diagnostic build ([15] = waves; all zero in the product
  * build): host uint64[16]; synchronises. */
 int mapf_get_profile(mapf_env *env, uint64_t *host16, int reset, void *stream);
+/* Diagnostic builds only: the fused kernel's per-workgroup timeline of its last
+ * launch, host [nblocks][8] u64 (100 MHz realtime stamps 0-3, HW_ID, XCC_ID). */
+int mapf_get_timeline(mapf_env *env, uint64_t *host, int32_t nblocks, void *stream);
 
 int mapf_get_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
 int mapf_set_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */

@@ -144,7 +144,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(d.hreplans, d.B); rc |= e->alloc(d.clock, d.B);
     if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * d.H * d.W);
     rc |= e->alloc(d.counters, C_NUM);
-    rc |= e->alloc(d.prof, 65536 * 8);
+    rc |= e->alloc(d.prof, PROF_WORDS);
     rc |= e->alloc(d.replan_list, 3 * (size_t)d.B);
     rc |= e->alloc(d.bfs_list, 3 * BN);
     uint8_t *smask = nullptr;
@@ -163,7 +163,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dl, dist_lut.data(), dist_lut.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(d.counters, 0, C_NUM * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(d.prof, 0, 65536 * 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMemset(d.prof, 0, PROF_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         mapf_destroy(e);
         return fail(MAPF_EDEVICE, "initial upload failed");
     }
@@ -370,6 +370,50 @@ int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
     return MAPF_OK;
 }
 
+static int step_observe_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, uint32_t flags, float *obs,
+                             float *vec, void *stream) {
+    if (!e || !actions || !obs || !vec) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_step_observe before mapf_reset");
+    if (!step_observe_fusable(e->d)) {          // two launches, same results
+        if (int rc = step_impl(e, actions, out, MAPF_STEP_COMMIT | flags, stream)) return rc;
+        return mapf_observe(e, obs, vec, stream);
+    }
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    StepOut o{};
+    if (out) {
+        o.status = out->status; o.reward = out->reward; o.shadow_goals = out->shadow_goals; o.cost = out->cost;
+        o.train_valid = out->train_valid; o.actions_fixed = out->actions_fixed; o.goals_reached = out->goals_reached;
+        o.constraints = out->constraints; o.reward_total = out->reward_total;
+    }
+    const bool host = observe_hosts_search(e->d);
+    int nsearch = 0, sslot = 0;
+    if (e->pending >= 0) {
+        if (host) { nsearch = e->d.search_blocks; sslot = e->pending; }
+        else launch_search(e->d, e->pending, 0, s);
+        e->pending = -1;
+    }
+    const int parity = e->parity;
+    launch_step_observe(e->d, actions, o, MAPF_STEP_COMMIT | flags, parity, obs, vec, nsearch, sslot, s);
+    if (e->d.human_mode != 0 || e->d.keep_bfs) {
+        if (host) e->pending = parity;             // rides in the next launch
+        else launch_search(e->d, parity, 0, s);
+    }
+    e->parity = (parity + 1) % 3;
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_step_observe(mapf_env *e, const int32_t *actions, const mapf_step_out *out, float *obs, float *vec,
+                      void *stream) {
+    return step_observe_impl(e, const_cast<int32_t *>(actions), out, 0u, obs, vec, stream);
+}
+
+int mapf_step_observe_random(mapf_env *e, int32_t *actions_out, const mapf_step_out *out, float *obs, float *vec,
+                             void *stream) {
+    return step_observe_impl(e, actions_out, out, 2u, obs, vec, stream);
+}
+
 int mapf_flush(mapf_env *e, void *stream) {
     if (!e) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
@@ -409,9 +453,9 @@ int mapf_get_profile(mapf_env *e, uint64_t *host16, int reset, void *stream) {
     if (!e || !host16) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
-    std::vector<uint64_t> all(65536 * 8);
+    std::vector<uint64_t> all(PROF_TL);
     HIPCHK(hipMemcpyAsync(all.data(), e->d.prof, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    if (reset) HIPCHK(hipMemsetAsync(e->d.prof, 0, all.size() * sizeof(uint64_t), s));
+    if (reset) HIPCHK(hipMemsetAsync(e->d.prof, 0, PROF_WORDS * sizeof(uint64_t), s));
     HIPCHK(hipStreamSynchronize(s));
     for (int k = 0; k < 16; ++k) host16[k] = 0;
     for (size_t w = 0; w < 65536; ++w) {   // sums over waves of the LAST launch; [15] = waves
@@ -419,6 +463,15 @@ int mapf_get_profile(mapf_env *e, uint64_t *host16, int reset, void *stream) {
         for (int k = 0; k < 7; ++k) host16[k] += all[w * 8 + k];
         host16[15] += 1;
     }
+    return MAPF_OK;
+}
+
+int mapf_get_timeline(mapf_env *e, uint64_t *host, int32_t nblocks, void *stream) {
+    if (!e || !host || nblocks < 0 || nblocks > (int)PROF_TL_BLOCKS) return fail(MAPF_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(host, e->d.prof + PROF_TL, (size_t)nblocks * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return MAPF_OK;
 }
 

@@ -74,6 +74,10 @@ struct DevEnv {
 };
 
 constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
+// diagnostic buffer prof[]: [PROF_WAVES][8] per-wave phase cycles, then the
+// fused kernel's block timeline [PROF_TL_BLOCKS][8] (MAPF_STAMPS builds only)
+constexpr size_t PROF_WAVES = 65536, PROF_TL = PROF_WAVES * 8, PROF_TL_BLOCKS = 8192,
+                 PROF_WORDS = PROF_TL + PROF_TL_BLOCKS * 8;
 
 __host__ __device__ inline uint32_t pack(int r, int c) { return (uint32_t)(r & 0xFFFF) | ((uint32_t)c << 16); }
 __host__ __device__ inline int prow(uint32_t p) { return (int)(p & 0xFFFF); }
@@ -129,7 +133,19 @@ __device__ inline uint64_t stamp_now() {
 #define STAMP_END() do { if ((threadIdx.x & 63) == 0) { \
     const size_t _w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; \
     if (_w < 65536) { for (int _k = 0; _k < 7; ++_k) e.prof[_w * 8 + _k] = _stamp_d[_k]; e.prof[_w * 8 + 7] = 1; } } } while (0)
+// block timeline (fused kernel): thread 0 of block k writes the constant-rate
+// (100 MHz) realtime counter of event t to prof[PROF_TL + k * 8 + t]; slot 6 =
+// HW_ID, slot 7 = XCC_ID of the block's CU.
+#define TL_STAMP(t) do { if (threadIdx.x == 0 && blockIdx.x < PROF_TL_BLOCKS) { uint64_t _r; \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_r)::"memory"); \
+    e.prof[PROF_TL + (size_t)blockIdx.x * 8 + (t)] = _r; } } while (0)
+#define TL_HWID() do { if (threadIdx.x == 0 && blockIdx.x < PROF_TL_BLOCKS) { uint32_t _h, _x; \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_h)); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_x)); \
+    e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 6] = _h; e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 7] = _x; } } while (0)
 #else
+#define TL_STAMP(t) do { } while (0)
+#define TL_HWID() do { } while (0)
 #define STAMP_BEGIN() do { } while (0)
 #define STAMP(k) do { } while (0)
 #define STAMP_END() do { } while (0)

@@ -1,0 +1,90 @@
+// primal-ppo_amd/csrc/mapf_fused.hip -- jointStep + getAllObservations in one
+// launch (runner.py:84-97 calls env.jointStep then env.getAllObservations).
+//
+// A workgroup of 256 lanes steps E = 256 / NP^2 envs (step_pairs_env, one lane
+// per agent pair) and then observes exactly those envs: the post-step cells,
+// goals and human state go straight to LDS, so the observation needs no state
+// reload and no second launch.  HBM traffic is the step's state + the
+// observation stores; the step's latency-bound chains of one workgroup overlap
+// the float4 store streams of the others.
+//
+// The first nsearch workgroups run the search work of the PREVIOUS committed
+// step (work-list slot `sslot`): humans' next paths (needed no earlier than
+// two steps after they are queued -- a Human path start->goal->start has >= 3
+// cells, mapf_gym.py:33-38) and agents' BFS maps (read only by mapf_bfs and
+// the BFS channel, which is not fused).  The step of this launch reads none of
+// what they write (the path buffer it walks is the other one).
+#include "mapf_step_pairs.h"
+#include "mapf_search.h"
+
+namespace mapf {
+
+template <int NP, bool HOST>
+__global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__restrict__ actions, StepOut out,
+                                                           uint32_t flags, int slot, float *__restrict__ obs,
+                                                           float *__restrict__ vec, int nsearch, int sslot) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    TL_STAMP(0);
+    TL_HWID();
+    if constexpr (HOST) {
+        if ((int)blockIdx.x < nsearch) {
+            const int wave = threadIdx.x >> 6;
+            char *lds = smem + (size_t)wave * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+            srch::search_items<uint32_t, 1>(e, sslot, 0, lds, blockIdx.x * (blockDim.x >> 6) + wave,
+                                            nsearch * (blockDim.x >> 6));
+            TL_STAMP(1);
+            return;
+        }
+    } else {
+        nsearch = 0;
+    }
+    constexpr int E = 256 / (NP * NP);
+    const int blk = (int)blockIdx.x - nsearch;
+    const int b0 = blk * E;
+    const int nenv = min(E, e.B - b0);
+    const ObsLds L = obs_layout(e, E, smem);
+    const uint32_t mreg = obs_map_word(e, b0, nenv, threadIdx.x);     // issued before the step's loads
+    step_pairs_env<NP, true>(e, actions, out, flags, slot, blk * 256 + (int)threadIdx.x, L, b0);
+    TL_STAMP(1);
+    obs_init(e, L, E, b0, nenv, mreg);
+    __syncthreads();
+    TL_STAMP(2);
+    obs_emit(e, L, obs, vec, E, b0, nenv);
+    TL_STAMP(3);
+}
+
+bool step_observe_fusable(const DevEnv &e) {
+    if (e.G > 8 || e.force_agent_lanes || e.human_mode == 2 || e.C >= 7) return false;
+    const int E = 256 / (e.G * e.G);
+    return obs_lds_bytes(e, E) <= 64 * 1024;
+}
+
+template <int NP>
+static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot, float *obs,
+                      float *vec, int nsearch, int sslot, hipStream_t s) {
+    constexpr int E = 256 / (NP * NP);
+    const int grid = (e.B + E - 1) / E + nsearch;
+    size_t lds = obs_lds_bytes(e, E);
+    if (nsearch > 0) {
+        const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+        if (sl > lds) lds = sl;
+        hipLaunchKernelGGL((step_observe_kernel<NP, true>), dim3(grid), dim3(256), lds, s, e, actions, out, flags,
+                           slot, obs, vec, nsearch, sslot);
+    } else {
+        hipLaunchKernelGGL((step_observe_kernel<NP, false>), dim3(grid), dim3(256), lds, s, e, actions, out, flags,
+                           slot, obs, vec, 0, 0);
+    }
+}
+
+void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,
+                         float *obs, float *vec, int nsearch, int sslot, hipStream_t s) {
+    if (!observe_hosts_search(e)) nsearch = 0;
+    switch (e.G) {
+        case 1: launch_np<1>(e, actions, out, flags, slot, obs, vec, nsearch, sslot, s); break;
+        case 2: launch_np<2>(e, actions, out, flags, slot, obs, vec, nsearch, sslot, s); break;
+        case 4: launch_np<4>(e, actions, out, flags, slot, obs, vec, nsearch, sslot, s); break;
+        default: launch_np<8>(e, actions, out, flags, slot, obs, vec, nsearch, sslot, s); break;
+    }
+}
+
+}  // namespace mapf

@@ -29,6 +29,11 @@ void launch_plan(const DevEnv &e, int promote, hipStream_t s);
 // observations; the first nsearch workgroups run the search work of `parity`
 void launch_observe(const DevEnv &e, float *obs, float *vec, int nsearch, int parity, hipStream_t s);
 bool observe_hosts_search(const DevEnv &e);
+// committed step + observations in one launch (mapf_fused.hip); the first nsearch
+// workgroups run the search work of list slot sslot (the previous step's)
+bool step_observe_fusable(const DevEnv &e);
+void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,
+                         float *obs, float *vec, int nsearch, int sslot, hipStream_t s);
 void launch_reset_fixed(const DevEnv &e, hipStream_t s);
 void launch_reset_seeded(const DevEnv &e, hipStream_t s);
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,

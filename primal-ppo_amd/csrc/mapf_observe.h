@@ -1,0 +1,256 @@
+// primal-ppo_amd/csrc/mapf_observe.h -- getAllObservations for one workgroup's
+// envs, as device functions shared by observe_kernel (mapf_observe.hip) and the
+// fused step+observe kernel (mapf_fused.hip).
+//
+// Reference: observe (mapf_gym.py:246-325), getAllObservations (:327-336),
+// worldWithAgents (:192-198).  Per agent: C x F x F float32 channels
+//   0 obstacle / off-map / self        3 visible agents' goals (clamped to FOV)
+//   1 other agents                     4 human next position (+ danger disc if use_da)
+//   2 own goal                         5 human.path[1:K+1] cells (use_hp)
+//   6 (C = 7, this build's extension) BFS descent: bfsMap >= 0 and < own value
+// and the vector [dx/d, dy/d, d, 0], d = (dx^2 + dy^2) ** .5 in float64.
+//
+// Every channel value is 0/1, so a workgroup first builds its agents'
+// observations as ONE contiguous bit-stream in LDS (bit k of the stream =
+// float k of the workgroup's slice of obs[B][N][C][F][F]) and then expands
+// it with one float4 store per 4 bits: the kernel's HBM traffic is the
+// C*F*F*4 bytes per agent it must write plus ~16 B of state per agent.
+//
+//  obs_init        zero stream / occupancy, stage the padded obstacle rows in LDS
+//  obs_load_agents agents' cells and goals, human next cell and path (from HBM;
+//                  the fused kernel's step writes them here instead)
+//  obs_emit        1 agent occupancy bitmap of each env (worldWithAgents)
+//                  2 (agent, FOV row) tasks: F-bit row segments of ch0/ch1 (+ DA, BFS)
+//                  3 per agent: own goal, visible agents' goals, human, HP, vector
+//                  4 stream -> float4 stores (coalesced, 1 KiB per wave instruction)
+#pragma once
+#include "mapf_common.h"
+
+namespace mapf {
+
+// LDS carve-up of an observing workgroup (E envs).
+struct ObsLds {
+    uint32_t *stream, *occ, *mapc, *spos, *sgoal, *shn, *shp;
+    int32_t *shpn;
+    int stream_words, rowsz;
+};
+
+__host__ __device__ inline int obs_stream_words(const DevEnv &e, int E) { return (E * e.N * e.C * e.F * e.F + 31) / 32 + 1; }
+
+__host__ __device__ inline size_t obs_lds_bytes(const DevEnv &e, int E) {
+    const int rowsz = e.Hp * e.WW;
+    const int nmap = e.shared_map ? 1 : E;
+    const size_t words = ((obs_stream_words(e, E) + 3) & ~3) + (size_t)E * rowsz + (size_t)nmap * rowsz +
+                         2 * (size_t)E * e.N + E + (size_t)E * e.k_predict + E;
+    return words * 4;
+}
+
+__device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
+    ObsLds L;
+    L.stream_words = obs_stream_words(e, E);
+    L.rowsz = e.Hp * e.WW;
+    const int nmap = e.shared_map ? 1 : E;
+    L.stream = reinterpret_cast<uint32_t *>(smem);
+    L.occ = L.stream + ((L.stream_words + 3) & ~3);
+    L.mapc = L.occ + E * L.rowsz;
+    L.spos = L.mapc + nmap * L.rowsz;
+    L.sgoal = L.spos + E * e.N;
+    L.shn = L.sgoal + E * e.N;                  // [E] human next
+    L.shp = L.shn + E;                          // [E][k_predict] human.path[1..K]
+    L.shpn = reinterpret_cast<int32_t *>(L.shp + E * e.k_predict);   // [E] count
+    return L;
+}
+
+namespace obsd {
+
+__device__ inline uint32_t seg_at(const uint32_t *row, int WW, int off, int F) {
+    const int w = off >> 5, s = off & 31;
+    const uint64_t a = (uint64_t)row[w] | ((w + 1 < WW) ? ((uint64_t)row[w + 1] << 32) : 0ull);
+    return (uint32_t)(a >> s) & ((1u << F) - 1u);
+}
+
+__device__ inline void or_bits(uint32_t *stream, int off, uint32_t seg, int F) {
+    if (!seg) return;
+    const int w = off >> 5, s = off & 31;
+    atomicOr(&stream[w], seg << s);
+    if (s + F > 32) {
+        const uint32_t hi = seg >> (32 - s);
+        if (hi) atomicOr(&stream[w + 1], hi);
+    }
+}
+
+__device__ inline void set_bit(uint32_t *stream, int off) { atomicOr(&stream[off >> 5], 1u << (off & 31)); }
+
+__device__ inline int isqrt_floor(int x) {
+    int r = (int)sqrtf((float)x);
+    while (r * r > x) --r;
+    while ((r + 1) * (r + 1) <= x) ++r;
+    return r;
+}
+
+}  // namespace obsd
+
+// Zero the bit-stream and the occupancy maps.  Staging the obstacle rows is
+// split so a caller can issue the loads early and store them later:
+// obs_map_word() loads word k of the workgroup's maps, obs_init() stores the
+// first blockDim.x words from `mreg` and loads+stores the rest itself.
+__device__ inline uint32_t obs_map_word(const DevEnv &e, int b0, int nenv, int k) {
+    const int rowsz = e.Hp * e.WW;
+    const int nw = e.shared_map ? rowsz : nenv * rowsz;
+    if (k >= nw) return 0u;
+    return e.shared_map ? e.map_bits[k] : e.map_bits[(size_t)b0 * rowsz + k];
+}
+
+__device__ inline void obs_init(const DevEnv &e, const ObsLds &L, int E, int b0, int nenv, uint32_t mreg) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int k = tid; k < L.stream_words; k += nt) L.stream[k] = 0u;
+    for (int k = tid; k < E * L.rowsz; k += nt) L.occ[k] = 0u;
+    const int nw = e.shared_map ? L.rowsz : nenv * L.rowsz;
+    if (tid < nw) L.mapc[tid] = mreg;
+    for (int k = tid + nt; k < nw; k += nt) L.mapc[k] = obs_map_word(e, b0, nenv, k);
+}
+
+__device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0, int nenv) {
+    const int tid = threadIdx.x, nt = blockDim.x, N = e.N, K = nenv * N;
+    for (int k = tid; k < K; k += nt) {
+        L.spos[k] = e.pos[(size_t)b0 * N + k];
+        L.sgoal[k] = e.goal[(size_t)b0 * N + k];
+    }
+    for (int k = tid; k < nenv; k += nt) {
+        const int b = b0 + k;
+        L.shn[k] = human_next(e, b);
+        int cnt = 0;
+        if (e.use_hp && e.C >= 6) {
+            const int cur = e.hcur[b];
+            const int len = e.hlen[b * 2 + cur];
+            const uint32_t *path = human_path(e, b, cur);
+            for (int q = 1; q <= e.k_predict && q < len; ++q) L.shp[k * e.k_predict + cnt++] = path[q];
+        }
+        L.shpn[k] = cnt;
+    }
+}
+
+// Phases 1-4.  Every thread of the workgroup calls it after a __syncthreads()
+// that follows obs_init and the agents' staging.
+__device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restrict__ obs, float *__restrict__ vec,
+                                int E, int b0, int nenv) {
+    using namespace obsd;
+    const int N = e.N, F = e.F, C = e.C, FF = F * F, CFF = C * FF;
+    const int K = nenv * N;
+    const int rowsz = L.rowsz;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    uint32_t *stream = L.stream;
+
+    // ---- phase 1: worldWithAgents as a padded bitmap per env ----
+    for (int k = tid; k < K; k += nt) {
+        const int le = k / N;
+        const int rr = prow(L.spos[k]) + e.P, cc = pcol(L.spos[k]) + e.P;
+        atomicOr(&L.occ[le * rowsz + rr * e.WW + (cc >> 5)], 1u << (cc & 31));
+    }
+    __syncthreads();
+
+    // ---- phase 2: (agent, FOV row) ----
+    const int half = F / 2;
+    const int R2 = e.R * e.R;
+    for (int task = tid; task < K * F; task += nt) {
+        const int k = task / F, y = task - k * F;
+        const int le = k / N;
+        const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
+        const int tr = pr - half, tc = pc - half;
+        const int rr = tr + y;                       // map row of this FOV row
+        const int prow_idx = rr + e.P;               // padded row (always inside)
+        const uint32_t *mrow = L.mapc + (e.shared_map ? 0 : le * rowsz) + prow_idx * e.WW;
+        const uint32_t *orow = L.occ + le * rowsz + prow_idx * e.WW;
+        uint32_t seg0 = seg_at(mrow, e.WW, tc + e.P, F);
+        uint32_t segA = seg_at(orow, e.WW, tc + e.P, F);
+        const uint32_t self = (y == half) ? (1u << half) : 0u;
+        const int base = k * CFF + y * F;
+        or_bits(stream, base, seg0 | self, F);
+        or_bits(stream, base + FF, segA & ~self, F);
+        if (e.use_da && rr >= 0 && rr < e.H) {      // ch4 danger area (mapf_gym.py:289-290)
+            const uint32_t hn = L.shn[le];
+            const int dy = prow(hn) - rr;
+            if (dy * dy <= R2) {
+                const int w = isqrt_floor(R2 - dy * dy);
+                int c0 = max(max(pcol(hn) - w, 0), tc), c1 = min(min(pcol(hn) + w, e.W - 1), tc + F - 1);
+                if (c0 <= c1) {
+                    const uint32_t m = ((1u << (c1 - c0 + 1)) - 1u) << (c0 - tc);
+                    or_bits(stream, base + 4 * FF, m, F);
+                }
+            }
+        }
+        if (C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
+            const size_t ai = (size_t)b0 * N + k;
+            const int16_t *bm = e.bfs + ai * e.H * e.W;
+            const int own = bm[pr * e.W + pc];
+            uint32_t m = 0;
+            if (own >= 0)
+                for (int x = 0; x < F; ++x) {
+                    const int cc = tc + x;
+                    if (cc < 0 || cc >= e.W) continue;
+                    const int v = bm[rr * e.W + cc];
+                    if (v >= 0 && v < own) m |= 1u << x;
+                }
+            or_bits(stream, base + 6 * FF, m, F);
+        }
+    }
+
+    // ---- phase 3: per agent ----
+    for (int k = tid; k < K; k += nt) {
+        const int le = k / N;
+        const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
+        const int tr = pr - half, tc = pc - half;
+        const int base = k * CFF;
+        const int gr = prow(L.sgoal[k]), gc = pcol(L.sgoal[k]);
+        if (tr <= gr && gr < tr + F && tc <= gc && gc < tc + F) set_bit(stream, base + 2 * FF + (gr - tr) * F + (gc - tc));
+        for (int j = 0; j < N; ++j) {               // visibleAgents -> clamped goals (:302-308)
+            const int kj = le * N + j;
+            if (kj == k) continue;
+            const int rj = prow(L.spos[kj]), cj = pcol(L.spos[kj]);
+            if (rj < tr || rj >= tr + F || cj < tc || cj >= tc + F) continue;
+            const int xr = min(max(prow(L.sgoal[kj]), tr), tr + F - 1);
+            const int xc = min(max(pcol(L.sgoal[kj]), tc), tc + F - 1);
+            set_bit(stream, base + 3 * FF + (xr - tr) * F + (xc - tc));
+        }
+        const uint32_t hn = L.shn[le];
+        const int hr = prow(hn), hc = pcol(hn);
+        if (tr <= hr && hr < tr + F && tc <= hc && hc < tc + F) set_bit(stream, base + 4 * FF + (hr - tr) * F + (hc - tc));
+        for (int q = 0; q < L.shpn[le]; ++q) {         // ch5 (:293-297): in-map cells inside the FOV
+            const uint32_t cell = L.shp[le * e.k_predict + q];
+            const int r = prow(cell), c = pcol(cell);
+            if (tr <= r && r < tr + F && tc <= c && c < tc + F) set_bit(stream, base + 5 * FF + (r - tr) * F + (c - tc));
+        }
+        // vector (:316-323)
+        const int dx = gr - pr, dy = gc - pc;
+        const int d2 = dx * dx + dy * dy;
+        float4 v;
+        if (d2 == 0) {
+            v = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            const double d = e.dist_lut[d2];
+            v = make_float4((float)((double)dx / d), (float)((double)dy / d), (float)d, 0.f);
+        }
+        reinterpret_cast<float4 *>(vec)[(size_t)b0 * N + k] = v;
+    }
+    __syncthreads();
+
+    // ---- phase 4: bit-stream -> float stores ----
+    const size_t total = (size_t)K * CFF;
+    float *dst = obs + (size_t)b0 * N * CFF;
+    if (((E * N * CFF) & 3) == 0) {
+        const size_t n4 = total >> 2;
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        for (size_t q = tid; q < n4; q += nt) {
+            const uint32_t bitpos = (uint32_t)(q << 2);
+            const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
+            d4[q] = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
+                                (float)((nib >> 3) & 1u));
+        }
+        for (size_t q = (n4 << 2) + tid; q < total; q += nt)
+            dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
+    } else {
+        for (size_t q = tid; q < total; q += nt) dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
+    }
+}
+
+}  // namespace mapf

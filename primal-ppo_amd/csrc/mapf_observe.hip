@@ -1,58 +1,11 @@
-// primal-ppo_amd/csrc/mapf_observe.hip -- getAllObservations for B envs.
-//
-// Reference: observe (mapf_gym.py:246-325), getAllObservations (:327-336),
-// worldWithAgents (:192-198).  Per agent: C x F x F float32 channels
-//   0 obstacle / off-map / self        3 visible agents' goals (clamped to FOV)
-//   1 other agents                     4 human next position (+ danger disc if use_da)
-//   2 own goal                         5 human.path[1:K+1] cells (use_hp)
-//   6 (C = 7, this build's extension) BFS descent: bfsMap >= 0 and < own value
-// and the vector [dx/d, dy/d, d, 0], d = (dx^2 + dy^2) ** .5 in float64.
-//
-// Every channel value is 0/1, so a workgroup first builds its agents'
-// observations as ONE contiguous bit-stream in LDS (bit k of the stream =
-// float k of the workgroup's slice of obs[B][N][C][F][F]) and then expands
-// it with one float4 store per 4 bits: the kernel's HBM traffic is the
-// C*F*F*4 bytes per agent it must write plus ~16 B of state per agent.
-//
-//  phase 0  zero stream / occupancy, stage the padded obstacle rows in LDS
-//  phase 1  agent occupancy bitmap of each env (worldWithAgents)
-//  phase 2  (agent, FOV row) tasks: 11-bit row segments of ch0/ch1 (+ DA, BFS)
-//  phase 3  per agent: own goal, visible agents' goals, human, HP, vector
-//  phase 4  stream -> float4 stores (coalesced, 1 KiB per wave instruction)
+// primal-ppo_amd/csrc/mapf_observe.hip -- getAllObservations for B envs
+// (mapf_gym.py:246-336); the per-workgroup work is in mapf_observe.h.
 #include "mapf_common.h"
 #include "mapf_kernels.h"
+#include "mapf_observe.h"
 #include "mapf_search.h"
 
 namespace mapf {
-
-namespace {
-
-__device__ inline uint32_t seg_at(const uint32_t *row, int WW, int off, int F) {
-    const int w = off >> 5, s = off & 31;
-    const uint64_t a = (uint64_t)row[w] | ((w + 1 < WW) ? ((uint64_t)row[w + 1] << 32) : 0ull);
-    return (uint32_t)(a >> s) & ((1u << F) - 1u);
-}
-
-__device__ inline void or_bits(uint32_t *stream, int off, uint32_t seg, int F) {
-    if (!seg) return;
-    const int w = off >> 5, s = off & 31;
-    atomicOr(&stream[w], seg << s);
-    if (s + F > 32) {
-        const uint32_t hi = seg >> (32 - s);
-        if (hi) atomicOr(&stream[w + 1], hi);
-    }
-}
-
-__device__ inline void set_bit(uint32_t *stream, int off) { atomicOr(&stream[off >> 5], 1u << (off & 31)); }
-
-__device__ inline int isqrt_floor(int x) {
-    int r = (int)sqrtf((float)x);
-    while (r * r > x) --r;
-    while ((r + 1) * (r + 1) <= x) ++r;
-    return r;
-}
-
-}  // namespace
 
 // The first `nsearch` workgroups run the step's search work (agent BFS maps,
 // humans' next paths -- mapf_search.h), the rest write observations: the
@@ -75,170 +28,17 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     } else {
         nsearch = 0;
     }
-    const int E = e.obs_envs, N = e.N, F = e.F, C = e.C, FF = F * F, CFF = C * FF;
+    const int E = e.obs_envs;
     const int b0 = ((int)blockIdx.x - nsearch) * E;
     const int nenv = min(E, e.B - b0);
-    const int K = nenv * N;                       // agents in this workgroup
-    const int rowsz = e.Hp * e.WW;
-    const int nmap = e.shared_map ? 1 : E;
-    const int stream_words = (E * N * CFF + 31) / 32 + 1;
-    uint32_t *stream = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *occ = stream + ((stream_words + 3) & ~3);
-    uint32_t *mapc = occ + E * rowsz;
-    uint32_t *spos = mapc + nmap * rowsz;
-    uint32_t *sgoal = spos + E * N;
-    uint32_t *shn = sgoal + E * N;                 // [E] human next
-    uint32_t *shp = shn + E;                       // [E][k_predict] human.path[1..K]
-    int32_t *shpn = reinterpret_cast<int32_t *>(shp + E * e.k_predict);   // [E] count
-    const int tid = threadIdx.x, nt = blockDim.x;
-
-    // ---- phase 0 ----
-    for (int k = tid; k < stream_words; k += nt) stream[k] = 0u;
-    for (int k = tid; k < E * rowsz; k += nt) occ[k] = 0u;
-    if (e.shared_map) {
-        for (int k = tid; k < rowsz; k += nt) mapc[k] = e.map_bits[k];
-    } else {
-        for (int k = tid; k < nenv * rowsz; k += nt) mapc[k] = e.map_bits[(size_t)b0 * rowsz + k];
-    }
-    for (int k = tid; k < K; k += nt) {
-        spos[k] = e.pos[(size_t)b0 * N + k];
-        sgoal[k] = e.goal[(size_t)b0 * N + k];
-    }
-    for (int k = tid; k < nenv; k += nt) {
-        const int b = b0 + k;
-        shn[k] = human_next(e, b);
-        int cnt = 0;
-        if (e.use_hp && C >= 6) {
-            const int cur = e.hcur[b];
-            const int len = e.hlen[b * 2 + cur];
-            const uint32_t *path = human_path(e, b, cur);
-            for (int q = 1; q <= e.k_predict && q < len; ++q) shp[k * e.k_predict + cnt++] = path[q];
-        }
-        shpn[k] = cnt;
-    }
+    const ObsLds L = obs_layout(e, E, smem);
+    obs_init(e, L, E, b0, nenv, obs_map_word(e, b0, nenv, threadIdx.x));
+    obs_load_agents(e, L, b0, nenv);
     __syncthreads();
-
-    // ---- phase 1: worldWithAgents as a padded bitmap per env ----
-    for (int k = tid; k < K; k += nt) {
-        const int le = k / N;
-        const int rr = prow(spos[k]) + e.P, cc = pcol(spos[k]) + e.P;
-        atomicOr(&occ[le * rowsz + rr * e.WW + (cc >> 5)], 1u << (cc & 31));
-    }
-    __syncthreads();
-
-    // ---- phase 2: (agent, FOV row) ----
-    const int half = F / 2;
-    const int R2 = e.R * e.R;
-    for (int task = tid; task < K * F; task += nt) {
-        const int k = task / F, y = task - k * F;
-        const int le = k / N;
-        const int pr = prow(spos[k]), pc = pcol(spos[k]);
-        const int tr = pr - half, tc = pc - half;
-        const int rr = tr + y;                       // map row of this FOV row
-        const int prow_idx = rr + e.P;               // padded row (always inside)
-        const uint32_t *mrow = mapc + (e.shared_map ? 0 : le * rowsz) + prow_idx * e.WW;
-        const uint32_t *orow = occ + le * rowsz + prow_idx * e.WW;
-        uint32_t seg0 = seg_at(mrow, e.WW, tc + e.P, F);
-        uint32_t segA = seg_at(orow, e.WW, tc + e.P, F);
-        const uint32_t self = (y == half) ? (1u << half) : 0u;
-        const int base = k * CFF + y * F;
-        or_bits(stream, base, seg0 | self, F);
-        or_bits(stream, base + FF, segA & ~self, F);
-        if (e.use_da && rr >= 0 && rr < e.H) {      // ch4 danger area (mapf_gym.py:289-290)
-            const uint32_t hn = shn[le];
-            const int dy = prow(hn) - rr;
-            if (dy * dy <= R2) {
-                const int w = isqrt_floor(R2 - dy * dy);
-                int c0 = max(max(pcol(hn) - w, 0), tc), c1 = min(min(pcol(hn) + w, e.W - 1), tc + F - 1);
-                if (c0 <= c1) {
-                    const uint32_t m = ((1u << (c1 - c0 + 1)) - 1u) << (c0 - tc);
-                    or_bits(stream, base + 4 * FF, m, F);
-                }
-            }
-        }
-        if (C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
-            const size_t ai = (size_t)b0 * N + k;
-            const int16_t *bm = e.bfs + ai * e.H * e.W;
-            const int own = bm[pr * e.W + pc];
-            uint32_t m = 0;
-            if (own >= 0)
-                for (int x = 0; x < F; ++x) {
-                    const int cc = tc + x;
-                    if (cc < 0 || cc >= e.W) continue;
-                    const int v = bm[rr * e.W + cc];
-                    if (v >= 0 && v < own) m |= 1u << x;
-                }
-            or_bits(stream, base + 6 * FF, m, F);
-        }
-    }
-
-    // ---- phase 3: per agent ----
-    for (int k = tid; k < K; k += nt) {
-        const int le = k / N;
-        const int pr = prow(spos[k]), pc = pcol(spos[k]);
-        const int tr = pr - half, tc = pc - half;
-        const int base = k * CFF;
-        const int gr = prow(sgoal[k]), gc = pcol(sgoal[k]);
-        if (tr <= gr && gr < tr + F && tc <= gc && gc < tc + F) set_bit(stream, base + 2 * FF + (gr - tr) * F + (gc - tc));
-        for (int j = 0; j < N; ++j) {               // visibleAgents -> clamped goals (:302-308)
-            const int kj = le * N + j;
-            if (kj == k) continue;
-            const int rj = prow(spos[kj]), cj = pcol(spos[kj]);
-            if (rj < tr || rj >= tr + F || cj < tc || cj >= tc + F) continue;
-            const int xr = min(max(prow(sgoal[kj]), tr), tr + F - 1);
-            const int xc = min(max(pcol(sgoal[kj]), tc), tc + F - 1);
-            set_bit(stream, base + 3 * FF + (xr - tr) * F + (xc - tc));
-        }
-        const uint32_t hn = shn[le];
-        const int hr = prow(hn), hc = pcol(hn);
-        if (tr <= hr && hr < tr + F && tc <= hc && hc < tc + F) set_bit(stream, base + 4 * FF + (hr - tr) * F + (hc - tc));
-        for (int q = 0; q < shpn[le]; ++q) {         // ch5 (:293-297): in-map cells inside the FOV
-            const uint32_t cell = shp[le * e.k_predict + q];
-            const int r = prow(cell), c = pcol(cell);
-            if (tr <= r && r < tr + F && tc <= c && c < tc + F) set_bit(stream, base + 5 * FF + (r - tr) * F + (c - tc));
-        }
-        // vector (:316-323)
-        const int dx = gr - pr, dy = gc - pc;
-        const int d2 = dx * dx + dy * dy;
-        float4 v;
-        if (d2 == 0) {
-            v = make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {
-            const double d = e.dist_lut[d2];
-            v = make_float4((float)((double)dx / d), (float)((double)dy / d), (float)d, 0.f);
-        }
-        reinterpret_cast<float4 *>(vec)[(size_t)b0 * N + k] = v;
-    }
-    __syncthreads();
-
-    // ---- phase 4: bit-stream -> float stores ----
-    const size_t total = (size_t)K * CFF;
-    float *dst = obs + (size_t)b0 * N * CFF;
-    if (((E * N * CFF) & 3) == 0) {
-        const size_t n4 = total >> 2;
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (size_t q = tid; q < n4; q += nt) {
-            const uint32_t bitpos = (uint32_t)(q << 2);
-            const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
-            d4[q] = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
-                                (float)((nib >> 3) & 1u));
-        }
-        for (size_t q = (n4 << 2) + tid; q < total; q += nt)
-            dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
-    } else {
-        for (size_t q = tid; q < total; q += nt) dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
-    }
+    obs_emit(e, L, obs, vec, E, b0, nenv);
 }
 
-size_t observe_lds(const DevEnv &e) {
-    const int E = e.obs_envs;
-    const int stream_words = (E * e.N * e.C * e.F * e.F + 31) / 32 + 1;
-    const int rowsz = e.Hp * e.WW;
-    const int nmap = e.shared_map ? 1 : E;
-    size_t words = ((stream_words + 3) & ~3) + (size_t)E * rowsz + (size_t)nmap * rowsz + 2 * E * e.N + E +
-                   (size_t)E * e.k_predict + E;
-    return words * 4;
-}
+size_t observe_lds(const DevEnv &e) { return obs_lds_bytes(e, e.obs_envs); }
 
 bool observe_hosts_search(const DevEnv &e) { return e.W <= 32 && e.H <= 64; }
 

@@ -1,0 +1,379 @@
+// primal-ppo_amd/csrc/mapf_step_pairs.h -- the step for N <= 8 agents per env.
+//
+// Same semantics as step_kernel (mapf_step.hip, which documents the reference
+// lines), different mapping: one lane per ORDERED PAIR (i, j) of agents, NP*NP
+// lanes per env (NP = next pow2 >= N), i.e. one env per wave at N = 8.  The
+// pairwise part of getRestrictedActions / getTrainValid (mapf_gym.py:363-402,
+// :535-550) is one lane's work instead of a loop over j; per-agent results are
+// OR-reduced across the NP lanes of agent i's row.  Serial parts
+// (getActionStatus's scan, fixActions' worklist) run on per-env uniform
+// values.  8x the waves of the agent-per-lane kernel at N = 8: the latency of
+// each wave's short dependent chains hides behind the others.
+//
+// Lane roles: row i = agent i (its NP lanes hold agent i's values, replicated),
+// lane j of the row also holds agent j's values ("column" copies).  Outputs
+// and state are written by lane j == 0 of each row.
+#pragma once
+#include "mapf_group.h"
+#include "mapf_kernels.h"
+#include "mapf_observe.h"
+
+namespace mapf {
+
+namespace pairs {
+
+// bit of the action whose move is (dr, dc), 0 if none (|dr| + |dc| > 1)
+__device__ inline unsigned abit(int r, int c) {
+    if (r == 0 && c == 0) return 1u;
+    if (r == 0 && c == 1) return 1u << 1;
+    if (r == 1 && c == 0) return 1u << 2;
+    if (r == 0 && c == -1) return 1u << 3;
+    if (r == -1 && c == 0) return 1u << 4;
+    return 0u;
+}
+// actions t of agent i with |p_i + d(t) - p_j|_1 <= 1, for p_j - p_i = (r, c)
+__device__ inline unsigned keys_of(int r, int c) {
+    unsigned m = 0;
+#pragma unroll
+    for (int t = 0; t < NA; ++t)
+        if (abs(dr(t) - r) + abs(dc(t) - c) <= 1) m |= 1u << t;
+    return m;
+}
+
+template <int NP>
+__device__ inline uint32_t row_or(uint32_t v) {
+#pragma unroll
+    for (int s = 1; s < NP; s <<= 1) v |= (uint32_t)__shfl_xor((int)v, s, 64);
+    return v;
+}
+
+}  // namespace pairs
+
+// One env's step on its NP*NP lanes; `gt` = the lane's index among the step
+// lanes of the launch (env = gt / (NP*NP)).  FEED: also hand the post-step
+// cells, goals and human state to the workgroup's observation (LDS `ob`,
+// whose first env is b0) -- the fused step+observe kernel; needs COMMIT.
+template <int NP, bool FEED>
+__device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out,
+                                               uint32_t flags, int slot, int gt, const ObsLds &ob, int b0) {
+    using namespace pairs;
+    constexpr int L = NP * NP;
+    constexpr uint32_t ROW = (1u << NP) - 1u;
+    const int N = e.N;
+    const int b = gt / L;
+    if (gt == 0 && (flags & 1u)) {
+        e.counters[C_REPLAN_COUNT + (slot + 1) % 3] = 0;
+        e.counters[C_BFS_COUNT + (slot + 1) % 3] = 0;
+    }
+    if (b >= e.B) return;
+    STAMP_BEGIN();
+    const int lane = lane_id();
+    const int base = lane & ~(L - 1), li = lane - base;
+    const int i = li / NP, j = li % NP;
+    const uint64_t emask = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << base);
+    auto eballot = [&](bool p) -> uint64_t { return (__ballot(p) & emask) >> base; };   // bit (k*NP + m)
+    auto agents_of = [&](uint64_t m) -> uint32_t {   // stride-NP row-0 bits -> compact agent mask
+        uint32_t a = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) a |= (uint32_t)((m >> (k * NP)) & 1ull) << k;
+        return a;
+    };
+    const bool vi = i < N, vj = j < N;
+    const bool head = j == 0;               // lane that writes agent i's outputs
+    const size_t ai = (size_t)b * N + i, aj = (size_t)b * N + j;
+    const uint32_t env_id = e.env_offset + (uint32_t)b;
+    // ---- every per-env / per-agent load is issued here, in two dependent rounds
+    const uint32_t clock = e.clock[b];
+    const uint32_t hp = e.hpos[b], hn = e.hnext[b];
+    const int hs = e.hstep[b], hcur = e.hcur[b];
+    const int2 hlen2 = *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
+    const uint32_t hng = e.human_mode == 1 ? e.hnext_goal[b] : NO_CELL;
+    const int hsi = e.human_mode == 2 ? e.hseq_idx[b] : 0, hsl = e.human_mode == 2 ? e.hseq_len[b] : 0;
+
+    const uint32_t pi = vi ? e.pos[ai] : 0u, pj = vj ? e.pos[aj] : 0u;
+    const int ri = prow(pi), ci = pcol(pi), rj = prow(pj), cj = pcol(pj);
+    const uint32_t gi = vi ? e.goal[ai] : 0u;
+    const int la = vi ? (int)e.last_act[ai] : -1;
+    int a_i, a_j;
+    if (flags & 2u) {                       // random policy: lane (k, 0) draws agent k's action
+        int mine = 0;
+        if (vi && head) {
+            mine = (int)__umulhi(philox(env_id, P_ACT | ((uint32_t)i << 8), clock, 0u, e.seed).x, (uint32_t)NA);
+            actions[ai] = mine;
+        }
+        a_i = (int)shfl32((uint32_t)mine, base + i * NP);
+        a_j = (int)shfl32((uint32_t)mine, base + j * NP);
+    } else {
+        a_i = vi ? actions[ai] : 0;
+        a_j = vj ? actions[aj] : 0;
+        if (vi && head && (a_i < 0 || a_i >= NA)) atomicAdd(&e.counters[C_BAD_ACTION], 1u);
+        if (a_i < 0 || a_i >= NA) a_i = 0;
+        if (a_j < 0 || a_j >= NA) a_j = 0;
+    }
+    // human.nextStep does not depend on the agents: decide it now, issue its path loads in round 2
+    const int Lc = hcur ? hlen2.y : hlen2.x;
+    int cur2 = hcur, hs2 = hs + 1, seq_idx = 0;
+    bool swapped = false, at_end = hs >= Lc - 1;
+    if (at_end) {
+        hs2 = 0;
+        if (e.human_mode == 1) {
+            if (hng != NO_CELL) { cur2 = hcur ^ 1; swapped = true; }
+        } else if (e.human_mode == 2) {
+            seq_idx = hsi + 1;
+            if (seq_idx < hsl) { cur2 = hcur ^ 1; swapped = true; }
+        }
+    }
+    const int L2 = cur2 ? hlen2.y : hlen2.x;
+    const uint32_t *p2 = human_path(e, b, cur2);
+    const uint32_t hp_new = p2[hs2];
+    const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
+    const unsigned st_mask = vi ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + ri * e.W + ci] : 0x1Fu;
+    unsigned hu_mask = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        if ((st_mask >> k) & 1u) continue;
+        const uint32_t x = pack(ri + dr(k), ci + dc(k));
+        if (x == hn || (pi == hn && x == hp)) hu_mask |= 1u << k;
+    }
+    const unsigned rep_mask = la >= 0 ? 1u << opp(la) : 0u;
+    STAMP(0);
+
+    // ---- the pair (i, j): restricted-action keys and conflicts with j's actual action
+    unsigned kij = 0, cij = 0;
+    if (vi && vj && i != j) {
+        const int r = rj - ri, c = cj - ci;
+        if (abs(r) + abs(c) <= 2) {
+            kij = keys_of(r, c);
+            const int er = r + dr(a_j), ec = c + dc(a_j);        // Y_j - p_i
+            cij = abit(er, ec);                                   // vertex: p_i + d(t) == Y_j
+            if (er == 0 && ec == 0) cij |= abit(r, c);            // swap: p_i + d(t) == p_j, Y_j == p_i
+        }
+    }
+    const uint64_t Mb = eballot((cij >> a_i) & 1u);                 // M_i = bits [i*NP, i*NP+NP)
+    const uint32_t kc = row_or<NP>(kij | (cij << 8));
+    const unsigned keys = kc & 0x1Fu, conf = (kc >> 8) & 0x1Fu;
+    const unsigned good = ~(st_mask | hu_mask | rep_mask | keys) & 0x1Fu;
+    const uint32_t Mi = (uint32_t)(Mb >> (i * NP)) & ROW;
+    STAMP(1);
+
+    // ---- getActionStatus
+    int s0;
+    bool cb = false;
+    if ((st_mask >> a_i) & 1u) s0 = -1;
+    else if ((hu_mask >> a_i) & 1u) s0 = -2;
+    else if ((good >> a_i) & 1u) s0 = 1;
+    else if (Mi) { s0 = -3; cb = true; }
+    else s0 = ((rep_mask >> a_i) & 1u) ? -4 : 1;
+    const uint32_t cbm = agents_of(eballot(head && vi && cb));
+    uint32_t T = 0;
+    for (uint32_t rem = cbm; rem; rem &= rem - 1) {
+        const int k = __builtin_ctz(rem);
+        if (!((T >> k) & 1u)) T |= ((uint32_t)(Mb >> (k * NP)) & ROW) | (1u << k);
+    }
+    const int st = ((T >> i) & 1u) ? -3 : s0;
+
+    float rw;
+    switch (st) {
+        case -1: rw = e.collision_cost; break;
+        case -2: rw = e.human_collision_cost; break;
+        case -3: rw = e.collision_cost; break;
+        case -4: rw = e.repeat_cost; break;
+        default: rw = e.action_cost; break;
+    }
+    const int Xr = ri + dr(a_i), Xc = ci + dc(a_i);
+    const uint32_t shadow = agents_of(eballot(head && vi && st == 1 && Xr == prow(gi) && Xc == pcol(gi)));
+    float cost = 0.f;
+    {   // max(R - ||h - x||, 0) / R in float64, then float32 (mapf_gym.py:513-526)
+        const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
+        const int d2 = d0 * d0 + d1 * d1;
+        if (d2 < e.R * e.R) cost = (float)(((double)e.R - sqrt((double)d2)) / (double)e.R);
+    }
+    if (vi) {
+        if (head) {
+            if (out.status) out.status[ai] = (int8_t)st;
+            if (out.reward) out.reward[ai] = rw;
+            if (out.cost) out.cost[ai] = cost;
+        }
+        if (out.train_valid) {
+            float *tv = out.train_valid + ai * NA;
+            for (int t = j; t < NA; t += NP)
+                tv[t] = (((good >> t) & 1u) || (((keys >> t) & 1u) && !((conf >> t) & 1u))) ? 1.f : 0.f;
+        }
+    }
+    if (li == 0 && out.shadow_goals) out.shadow_goals[b] = __popc(shadow);
+    STAMP(2);
+    if (!(flags & 1u)) return;
+
+    // ---- fixActions (worklist; agent values row-replicated, j's copies in column)
+    int fixed = a_i;
+    const uint32_t need = agents_of(eballot(head && vi && (st == -1 || st == -2 || st == -3)));
+    if (need) {
+        const int st_j = (int)shfl32((uint32_t)st, base + j * NP);
+        int asg_i = (vi && st == 1) ? a_i : -1;
+        int asg_j = (vj && st_j == 1) ? a_j : -1;
+        const uint32_t qm = agents_of(eballot(head && vi && st < 0));
+        int q = (vi && st < 0) ? __popc(qm & ((1u << i) - 1u)) : -1;
+        int next_q = __popc(qm), hd = 0, rounds = 0, iters = 0;
+        const unsigned viable_i = ~(st_mask | hu_mask) & 0x1Fu;
+        while (hd < next_q) {
+            if (++iters > 64 * N) {
+                if (li == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
+                break;
+            }
+            const int idx = __builtin_ctz(agents_of(eballot(head && vi && q == hd)));
+            ++hd;
+            const unsigned good_idx = shfl32(good, base + idx * NP);
+            int newa = -1;
+            uint32_t ev = 0;
+            if (good_idx) {
+                newa = __builtin_ctz(good_idx);
+            } else {
+                const unsigned viable = shfl32(viable_i, base + idx * NP);
+                unsigned cjm = 0;          // in row idx: idx's actions colliding with agent j's assignment
+                if (i == idx && vj && j != idx && asg_j >= 0) {
+                    const int r = rj - ri, c = cj - ci;
+                    if (abs(r) + abs(c) <= 2) {
+                        const int er = r + dr(asg_j), ec = c + dc(asg_j);
+                        cjm = abit(er, ec);
+                        if (er == 0 && ec == 0) cjm |= abit(r, c);
+                    }
+                }
+                unsigned U = 0;
+#pragma unroll
+                for (int t = 0; t < NA; ++t)
+                    if (eballot((cjm >> t) & 1u)) U |= 1u << t;
+                const unsigned fr = viable & ~U;
+                if (fr) {
+                    newa = __builtin_ctz(fr);
+                } else {
+                    const int nv = __popc(viable);
+                    newa = 0;
+                    if (nv == 0) {
+                        if (li == 0) atomicAdd(&e.counters[C_EMPTY_VIABLE], 1u);
+                    } else {
+                        int pick;
+                        if (e.fix_choice == 0) pick = rounds % nv;
+                        else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)rounds,
+                                                         e.seed).x, (uint32_t)nv);
+                        ++rounds;
+                        newa = nth_bit(viable, pick);
+                        ev = (uint32_t)(eballot((cjm >> newa) & 1u) >> (idx * NP)) & ROW;   // evicted agents
+                    }
+                }
+            }
+            if ((ev >> i) & 1u) { asg_i = -1; q = next_q + __popc(ev & ((1u << i) - 1u)); }
+            if ((ev >> j) & 1u) asg_j = -1;
+            next_q += __popc(ev);
+            if (i == idx) { asg_i = newa; q = -1; }
+            if (j == idx) asg_j = newa;
+        }
+        fixed = asg_i >= 0 ? asg_i : 0;
+    }
+    STAMP(3);
+
+    // ---- takeStep + lifelong goals
+    const int nr = ri + dr(fixed), nc = ci + dc(fixed);
+    const uint32_t np = vi ? pack(nr, nc) : 0xFFFFFFFFu;
+    const bool reached = vi && e.lifelong && np == gi;
+    uint32_t ng = gi;
+    if (e.goal_mode == 0) {
+        if (reached && head) {
+            int cur = e.seq_cur[ai];
+            const int len = e.seq_len[ai];
+            const uint32_t *s = e.seq + ai * e.S;
+            if (cur >= len) ng = s[len - 1];
+            else ng = s[cur++];
+            e.seq_cur[ai] = cur;
+        }
+    } else {
+        // getNextGoal(worldWithAgentsAndGoals()) in agent order (mapf_gym.py:620-627)
+        for (uint32_t rem = agents_of(eballot(head && reached)); rem; rem &= rem - 1) {
+            const int k = __builtin_ctz(rem);
+            const uint32_t mypos = (i <= k) ? np : pi;
+            const uint32_t mygoal = ng;
+            const uint32_t *bits = env_map(e, b);
+            auto ok = [&](int r, int c) -> bool {
+                if (obstacle_at(e, bits, r, c)) return false;
+                const uint32_t cell = pack(r, c);
+                return eballot(head && vi && (mypos == cell || mygoal == cell)) == 0ull;
+            };
+            int r, c;
+            if (!group_free_cell(e, env_id, P_GOAL, k, clock, ok, r, c)) {
+                if (li == 0) atomicAdd(&e.counters[C_FREECELL], 1u);
+                const uint32_t npk = shfl32(np, base + k * NP);
+                r = prow(npk); c = pcol(npk);
+            }
+            if (i == k) ng = pack(r, c);
+        }
+    }
+    if (vi && head) {
+        e.pos[ai] = np;
+        e.goal[ai] = ng;
+        e.last_act[ai] = (int8_t)fixed;
+        if (reached && e.keep_bfs) {
+            const uint32_t sl = atomicAdd(&e.counters[C_BFS_COUNT + slot], 1u);
+            e.bfs_list[(size_t)slot * e.B * N + sl] = (uint32_t)ai;
+        }
+    }
+    STAMP(4);
+
+    // ---- human.nextStep (see step_kernel): side effects of the advance decided above
+    if (at_end) {
+        if (e.human_mode == 1) {
+            if (swapped && li == 0) { e.hgoal[b] = hng; e.hreplans[b] += 1u; }
+        } else if (e.human_mode == 2) {
+            if (li == 0) {
+                e.hgoal[b] = e.hseq[(size_t)b * e.HS + (seq_idx < hsl ? seq_idx : hsl - 1)];
+                e.hseq_idx[b] = seq_idx;
+            }
+        }
+    }
+    if (swapped) {
+        uint32_t ns, ngl;
+        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0);
+        if (li == 0) {
+            e.hnext_start[b] = ns;
+            e.hnext_goal[b] = ngl;
+            if (ngl != NO_CELL) {
+                const uint32_t sl = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], 1u);
+                e.replan_list[(size_t)slot * e.B + sl] = (uint32_t)b;
+            }
+        }
+    }
+    if (li == 0) {
+        e.hcur[b] = cur2;
+        e.hstep[b] = hs2;
+        e.hpos[b] = hp_new;
+        e.hnext[b] = hn_new;
+        e.clock[b] = clock + 1u;
+    }
+    STAMP(5);
+
+    if (vi && head) {
+        const int d0 = prow(hp_new) - nr, d1 = pcol(hp_new) - nc;
+        const float cv = (d0 * d0 + d1 * d1 <= e.constr_d2) ? 1.f : 0.f;
+        if (out.actions_fixed) out.actions_fixed[ai] = fixed;
+        if (out.goals_reached) out.goals_reached[ai] = reached ? 1.f : 0.f;
+        if (out.constraints) out.constraints[ai] = cv;
+        if (out.reward_total) out.reward_total[ai] = reached ? rw + e.goal_reward : rw;
+    }
+    STAMP(6);
+    if constexpr (FEED) {
+        const int le = b - b0;
+        if (vi && head) {
+            ob.spos[le * N + i] = np;
+            ob.sgoal[le * N + i] = ng;
+        }
+        if (li == 0) ob.shn[le] = hn_new;
+        if (e.use_hp && e.C >= 6) {       // human.path[1..K] of the path it walks after the step
+            const int kp = e.k_predict;
+            for (int q = 1 + li; q <= kp && q < L2; q += L) ob.shp[le * kp + q - 1] = p2[q];
+            if (li == 0) ob.shpn[le] = min(kp, L2 - 1);
+        } else if (li == 0) {
+            ob.shpn[le] = 0;
+        }
+    }
+    STAMP_END();
+}
+
+}  // namespace mapf

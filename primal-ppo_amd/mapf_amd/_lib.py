@@ -43,11 +43,14 @@ SIGNATURES = {
     "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_step_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_observe": (ctypes.c_int, [P, P, P, P]),
+    "mapf_step_observe": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), P, P, P]),
+    "mapf_step_observe_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), P, P, P]),
     "mapf_flush": (ctypes.c_int, [P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),
     "mapf_get_counters": (ctypes.c_int, [P, P, P]),
     "mapf_get_profile": (ctypes.c_int, [P, P, ctypes.c_int, P]),
+    "mapf_get_timeline": (ctypes.c_int, [P, P, ctypes.c_int32, P]),
     "mapf_get_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
     "mapf_set_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
     "mapf_gae": (ctypes.c_int, [P, P, P, P, P, I32, I32, ctypes.c_double, ctypes.c_double, P]),

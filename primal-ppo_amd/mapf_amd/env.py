@@ -170,6 +170,22 @@ class BatchedMapfGym:
         _lib.check(_lib.lib().mapf_observe(self.h, _ptr(obs), _ptr(vec), _stream(self.device)))
         return obs, vec
 
+    def step_observe(self, actions=None, obs=None, vec=None, random_policy=False):
+        """Committed step + getAllObservations in one launch (mapf_step_observe): the same
+        outputs as step() followed by observe().  random_policy: draw the actions on device
+        into `actions` first (mapf_step_observe_random).  Returns (out, obs, vec)."""
+        if actions is None:
+            actions = self.actions
+        obs = self.obs if obs is None else obs
+        vec = self.vec if vec is None else vec
+        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
+        assert obs.is_contiguous() and vec.is_contiguous()
+        assert obs.numel() == self.B * self.N * self.C * self.F * self.F and vec.numel() == self.B * self.N * 4
+        fn = _lib.lib().mapf_step_observe_random if random_policy else _lib.lib().mapf_step_observe
+        _lib.check(fn(self.h, _ptr(actions), ctypes.byref(self._stepout), _ptr(obs), _ptr(vec),
+                      _stream(self.device)))
+        return self.out, obs, vec
+
     def flush(self):
         """Run pending search work (BFS maps, next human paths) now, in its own launch."""
         _lib.check(_lib.lib().mapf_flush(self.h, _stream(self.device)))
@@ -195,6 +211,14 @@ class BatchedMapfGym:
         _lib.check(_lib.lib().mapf_get_profile(self.h, ctypes.c_void_p(c.ctypes.data), int(reset),
                                                _stream(self.device)))
         return c
+
+    def timeline(self, nblocks):
+        """Diagnostic (stamps) build: per-workgroup timeline of the last fused launch,
+        uint64 [nblocks, 8] (realtime stamps 0-3 at 100 MHz, HW_ID, XCC_ID)."""
+        out = np.zeros((nblocks, 8), dtype=np.uint64)
+        _lib.check(_lib.lib().mapf_get_timeline(self.h, out.ctypes.data_as(ctypes.c_void_p), nblocks,
+                                                 _stream(self.device)))
+        return out
 
     def get_state(self):
         B, N, L = self.B, self.N, self.path_capacity

@@ -39,6 +39,9 @@ for s in $STEPS; do
     stamps)
       timeout -k 10 200 python3 tools/stamps.py > "$OUT/stamps.log" 2>&1
       rc=$?; echo "stamps rc=$rc"; cat "$OUT/stamps.log" | grep -v amdgpu.ids; stop_if_fatal $rc stamps ;;
+    timeline)
+      timeout -k 10 200 python3 tools/timeline.py > "$OUT/timeline.log" 2>&1
+      rc=$?; echo "timeline rc=$rc"; grep -v amdgpu.ids "$OUT/timeline.log"; stop_if_fatal $rc timeline ;;
     rollout)
       timeout -k 10 600 python3 tools/bench_rollout.py --train ${ROLLOUT_ARGS:-} > "$OUT/rollout.log" 2>&1
       rc=$?; echo "rollout rc=$rc"; grep phase "$OUT/rollout.log"; tail -2 "$OUT/rollout.log"; stop_if_fatal $rc rollout ;;
@@ -49,6 +52,14 @@ for s in $STEPS; do
         rc=$?; echo "pmc $ctr rc=$rc"; stop_if_fatal $rc pmc
       done
       find "$OUT" -path "*pmc_*" -name "*.csv" | head ;;
+    sq)   # instruction mix of every kernel (SQ counters), one pass per counter group
+      i=0
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_INSTS_BRANCH" ${SQ_EXTRA:-}; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+          -d "$OUT/sq_$i" -o run -- python3 "$ROOT/bench.py" --steps 30 --warmup 10 --no-cpu --graph-steps 0) > "$OUT/sq_$i.log" 2>&1
+        rc=$?; echo "sq $i ($grp) rc=$rc"; stop_if_fatal $rc sq
+      done ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 20 --no-cpu) > "$OUT/prof.log" 2>&1

@@ -27,15 +27,21 @@ def main():
     env = BatchedMapfGym(make_config(B, 20, 20, num_agents=8, fov=11, num_channel=6, human_mode="random",
                                      goal_mode="random", fix_choice=1, seed=1234))
     env.reset_seeded(generate_warehouse(20, 20))
+    split = os.environ.get("SPLIT", "0") == "1"     # default: the fused step+observe launch
+
+    def one():
+        if split:
+            env.step_random()
+            env.observe()
+        else:
+            env.step_observe(random_policy=True)
     for _ in range(50):
-        env.step_random()
-        env.observe()
+        one()
     torch.cuda.synchronize()
     env.profile(reset=True)
     n = 200
     for _ in range(n):
-        env.step_random()
-        env.observe()
+        one()
     torch.cuda.synchronize()
     p = env.profile(reset=True)      # sums over the waves of the last step launch
     waves = max(int(p[15]), 1)
