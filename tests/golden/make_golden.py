@@ -441,7 +441,72 @@ def g5_net():
     print("g5_net: stats", out["train_stats"])
 
 
+def g6_episodes():
+    """The reference's own fixed-episode files (evaluate.py:50-123, generated and
+    written by its generateFixedEpisodeInfos / saveFixedEpisodeInfos) plus the
+    OneEpPerformance sums of its evaluate() loop (evaluate.py:210-256) on them,
+    with recorded uniform actions in place of the policy: LoopingHuman episodes
+    without DA/HP, and FixedPathHuman episodes with DA+HP."""
+    import evaluate as ev
+    folder = os.path.join(OUT, "g6_episodes")
+    alg.EvalParameters.EPISODES = 4
+    alg.EvalParameters.N_AGENTS = 2
+    alg.EvalParameters.MAX_STEPS = 30
+    alg.EvalParameters.FIXED_EPISODE_INFOS_PATH = folder
+    alg.EnvParameters.WORLD_SIZE = (10, 14)
+    set_params(2, 9)
+    np.random.seed(61)
+    ev.saveFixedEpisodeInfos(ev.generateFixedEpisodeInfos())
+    rng = np.random.default_rng(62)
+    steps = 80
+    out = {}
+    for mtype, da, hp in [(0, False, False), (1, True, True)]:
+        infos = ev.loadFixedEpisodeInfos()
+        acts = np.zeros((4, steps, 2), np.int64)
+        metrics = np.zeros((4, 8), np.float64)
+        for e in range(4):
+            hseq = infos["humanSequence"][e] if mtype == 1 else None
+            env = mg.FixedMapfGym(infos["obstacleMap"][e], infos["agentsSequence"][e], infos["humanStart"][e],
+                                  infos["humanGoal"][e], numChannel=6, useDA=da, useHP=hp, humanSequence=hseq)
+            orig_fix = env.fixActions
+
+            def fix_wrap(actions, st, orig_fix=orig_fix):
+                ROUND[0] = 0
+                return orig_fix(actions, st)
+            env.fixActions = fix_wrap
+            perf = util.OneEpPerformance()
+            env.getAllObservations()
+            for t in range(steps):
+                actions = greedy_actions(rng, env, 2, 0.7).astype(np.float64)
+                acts[e, t] = actions
+                st = env.getActionStatus(actions)
+                perf.staticCollide += int(np.sum(st == -1))
+                perf.humanCollide += int(np.sum(st == -2))
+                perf.agentCollide += int(np.sum(st == -3))
+                rewards, shadow = env.calculateActionReward(actions, st)
+                cost = env.calculateCostReward(actions)
+                perf.shadowGoals += shadow
+                goals, constr = env.jointStep(actions, st)
+                for i, v in enumerate(goals):
+                    if v == 1:
+                        rewards[0, i] += alg.EnvParameters.GOAL_REWARD
+                perf.episodeReward += np.sum(rewards)
+                perf.totalGoals += np.sum(goals)
+                perf.episodeCostReward += np.sum(cost)
+                perf.constraintViolations += np.sum(constr)
+                env.getAllObservations()
+            metrics[e] = [perf.episodeReward, perf.episodeCostReward, perf.humanCollide, perf.staticCollide,
+                          perf.agentCollide, perf.totalGoals, perf.shadowGoals, perf.constraintViolations]
+        out[f"actions_type{mtype}"] = acts.astype(np.int32)
+        out[f"metrics_type{mtype}"] = metrics
+        print(f"g6 type {mtype}: metrics\n{metrics}")
+    np.savez_compressed(os.path.join(folder, "expected.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["g6"]:
+        g6_episodes()
+        sys.exit(0)
     if sys.argv[1:] == ["g4"]:
         g4_gae()
         sys.exit(0)
@@ -459,3 +524,4 @@ if __name__ == "__main__":
     g2_fuzz(3000, 21)
     g3_search(31)
     g4_gae()
+    g6_episodes()
