@@ -47,11 +47,11 @@ def fused_bytes_per_agent(C, F, H, W, N):
     return C * F * F * 4 + 16 + 9 + 9 + 4 + 45 + (-(-H * W // 8) + 64) / N
 
 
-def cpu_baseline(H, W, N, F, C, seconds):
-    """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host, one thread."""
+def cpu_baseline(world, H, W, N, F, C, seconds):
+    """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host, one thread,
+    on a bounded sample: 32 envs sharing the workload's first map, stepped for ~`seconds`."""
     from oracle import oracle as O
-    from mapf_amd.maps import generate_warehouse
-    world = generate_warehouse(H, W)
+    world = world if world.ndim == 2 else world[0]
     B = 32
     cfg = O.make_config(H, W, N, F, C, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
     batch = O.OracleBatch(cfg, world, B)
@@ -62,9 +62,31 @@ def cpu_baseline(H, W, N, F, C, seconds):
         steps += 10
     dt = time.perf_counter() - t0
     return {"value": round(B * N * steps / dt, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{B} envs x {N} agents, {H}x{W}, FOV {F}, random policy, {steps} lockstep steps "
-                      f"(step+observe) in {dt:.1f}s, single thread; reference Python measured 3,442 "
-                      f"agent-steps/s/core on this shape (BASELINE.md)"}
+            "sample": f"{B} envs x {N} agents, {H}x{W}, FOV {F}, {C} channels, random policy, {steps} lockstep "
+                      f"steps (step+observe) in {dt:.1f}s, single thread; reference Python measured 3,442 "
+                      f"agent-steps/s/core on the c2 shape (BASELINE.md)"}
+
+
+# BASELINE.json configs as env-only workloads; envs are PER GPU.
+#   c1  1 env x 4 agents, 10x10 warehouse, FOV 11           (the reference's CPU case)
+#   c2  4096 x 8, 20x20 warehouse, FOV 11                   (headline: the default)
+#   c4  8192 x 16 over 8 GPUs = 1024 per GPU, 40x40, FOV 9  (env part of the c4 training config)
+#   c5  16384 x 64 over 8 GPUs = 2048 per GPU, 80x80 random maps p=0.3 (one per env, largest
+#       4-connected component), FOV 11, 7 channels (BFS heuristic channel)
+PRESETS = {
+    "c1": dict(envs=1, agents=4, size=10, fov=11, channels=6, maps="warehouse"),
+    "c2": dict(envs=4096, agents=8, size=20, fov=11, channels=6, maps="warehouse"),
+    "c4": dict(envs=1024, agents=16, size=40, fov=9, channels=6, maps="warehouse"),
+    "c5": dict(envs=2048, agents=64, size=80, fov=11, channels=7, maps="random"),
+}
+
+
+def make_maps(kind, B, H, W, rank):
+    from mapf_amd.maps import generate_warehouse, keep_largest_component, random_map
+    if kind == "warehouse":
+        return generate_warehouse(H, W), True
+    rng = np.random.default_rng(1234 + rank)
+    return np.stack([keep_largest_component(random_map(rng, H, W, 0.3)) for _ in range(B)]), False
 
 
 PMC_REPORTS = {"observe_kernel": os.path.join(ROOT, "profiles", "r01_pmc_observe_c2.json"),
@@ -85,19 +107,25 @@ def pmc_traffic(B, N, H, W, F, C, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(PRESETS),
+                    help="BASELINE.json workload preset (c2 = the headline metric); explicit flags override")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--agents", type=int, default=8)
-    ap.add_argument("--size", type=int, default=20)
-    ap.add_argument("--fov", type=int, default=11)
-    ap.add_argument("--channels", type=int, default=6)
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=None)
+    ap.add_argument("--size", type=int, default=None)
+    ap.add_argument("--fov", type=int, default=None)
+    ap.add_argument("--channels", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--split", action="store_true", help="step and observe as two launches")
     ap.add_argument("--graph-steps", type=int, default=24,
                     help="steps per captured hipGraph, a multiple of 3 (work-list slots rotate mod 3); 0 = direct")
     args = ap.parse_args()
+    preset = PRESETS[args.config]
+    for k in ("envs", "agents", "size", "fov", "channels"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,12 +139,12 @@ def main():
 
     from mapf_amd.config import make_config
     from mapf_amd.env import BatchedMapfGym
-    from mapf_amd.maps import generate_warehouse
 
     B, N, H, W, F, C = args.envs, args.agents, args.size, args.size, args.fov, args.channels
-    world = generate_warehouse(H, W)
+    world, shared = make_maps(preset["maps"], B, H, W, rank)
     env = BatchedMapfGym(make_config(B, H, W, num_agents=N, fov=F, num_channel=C, human_mode="random",
-                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B), device=dev)
+                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B,
+                                     shared_map=shared), device=dev)
     env.reset_seeded(world)
     obs, vec, acts = env.obs, env.vec, env.actions
 
@@ -195,7 +223,7 @@ def main():
     if rank == 0:
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
-        if args.split:
+        if args.split or not env.fused:      # two launches per step: the observe kernel is the roofline one
             kname, bpa, kms = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms
         else:
             kname, bpa, kms = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms
@@ -205,17 +233,18 @@ def main():
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (seeded warehouse episodes on device, uniform random policy)",
-            "config": {"workload": f"c2: {B} envs x {N} agents per GPU, {H}x{W} warehouse, FOV {F}, {C} channels, "
-                                   f"random policy, env.step+observe",
+            "config": {"workload": f"{args.config}: {B} envs x {N} agents per GPU, {H}x{W} "
+                                   f"{'warehouse' if shared else 'random p=0.3 maps (one per env)'}, FOV {F}, "
+                                   f"{C} channels, random policy, env.step+observe",
                        "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
                        "parallelism": f"env-shards x{world_size}"},
-            "breakdown_ms": {"step_observe_kernel": round(fused_ms, 4),
+            "breakdown_ms": {"step_observe": round(fused_ms, 4),
                              "split": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
                                        "observe_kernel": round(obs_ms, 4)},
                              "timing": f"HIP events around {KT} direct launches of each path (split: search "
                                        f"flushed alone); value from hipGraph replays of {G} steps"
-                                       f" ({'split' if args.split else 'fused'} path)"},
+                                       f" ({'fused' if env.fused and not args.split else 'split'} path)"},
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, N, H, W, F, C, kname), "traffic_unit": "MB/launch (PMC)",
@@ -224,7 +253,7 @@ def main():
             "device_counters": [int(x) for x in counters[:8]],
         }
         if world_size == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(H, W, N, F, C, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(world, H, W, N, F, C, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

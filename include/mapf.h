@@ -133,6 +133,9 @@ int mapf_abi_version(void);
 int mapf_create(const mapf_config *cfg, int device, mapf_env **out);
 int mapf_destroy(mapf_env *env);
 int mapf_path_capacity(const mapf_env *env);       /* human path capacity per env */
+/* 1 if mapf_step_observe runs as ONE launch for this configuration (N <= 8,
+ * no BFS channel, no scripted human), 0 if it runs as step + observe. */
+int mapf_step_observe_fused(const mapf_env *env);
 
 int mapf_reset(mapf_env *env, const mapf_reset_spec *spec, void *stream);
 

@@ -180,6 +180,7 @@ int mapf_destroy(mapf_env *e) {
 }
 
 int mapf_path_capacity(const mapf_env *e) { return e ? e->d.Lmax : 0; }
+int mapf_step_observe_fused(const mapf_env *e) { return e && step_observe_fusable(e->d) ? 1 : 0; }
 
 int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     if (!e || !spec || !spec->maps) return fail(MAPF_EINVAL, "null argument");

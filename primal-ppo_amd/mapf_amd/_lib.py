@@ -39,6 +39,7 @@ SIGNATURES = {
     "mapf_create": (ctypes.c_int, [ctypes.POINTER(MapfConfig), ctypes.c_int, ctypes.POINTER(P)]),
     "mapf_destroy": (ctypes.c_int, [P]),
     "mapf_path_capacity": (ctypes.c_int, [P]),
+    "mapf_step_observe_fused": (ctypes.c_int, [P]),
     "mapf_reset": (ctypes.c_int, [P, ctypes.POINTER(ResetSpec), P]),
     "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_step_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),

@@ -39,6 +39,7 @@ class BatchedMapfGym:
             _lib.check(_lib.lib().mapf_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
         self.h = h
         self.path_capacity = _lib.lib().mapf_path_capacity(self.h)
+        self.fused = bool(_lib.lib().mapf_step_observe_fused(self.h))   # step_observe = one launch
         dev = self.device
         B, N = self.B, self.N
         self.out = dict(
