@@ -71,6 +71,7 @@ struct DevEnv {
     const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
     const uint8_t *smask;     // [nmaps][H*W]: static-invalid action mask of each cell (getInvalidActions[0])
     int search_blocks;        // workgroups of the observe launch that run search work
+    int band_blocks;          // workgroups of the fused launch that write the zero band (0 = none)
 };
 
 constexpr uint32_t NO_CELL = 0xFFFFFFFFu;

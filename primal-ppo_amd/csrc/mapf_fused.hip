@@ -8,7 +8,16 @@
 // observation stores; the step's latency-bound chains of one workgroup overlap
 // the float4 store streams of the others.
 //
-// The first nsearch workgroups run the search work of the PREVIOUS committed
+// Workgroup roles, in grid order:
+//  [0, nband)           the zero band (channel 5 while use_hp is off, all 0 by
+//                       construction) of every agent's observation: HBM writes
+//                       that need nothing from the step, issued while the step
+//                       workgroups run their latency-bound chains; the step
+//                       workgroups' float4 expansion skips exactly those float4s
+//  [nband, +nsearch)    search work (below)
+//  the rest             step + observe of E envs each
+//
+// The nsearch search workgroups run the search work of the PREVIOUS committed
 // step (work-list slot `sslot`): humans' next paths (needed no earlier than
 // two steps after they are queued -- a Human path start->goal->start has >= 3
 // cells, mapf_gym.py:33-38) and agents' BFS maps (read only by mapf_bfs and
@@ -22,15 +31,23 @@ namespace mapf {
 template <int NP, bool HOST>
 __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__restrict__ actions, StepOut out,
                                                            uint32_t flags, int slot, float *__restrict__ obs,
-                                                           float *__restrict__ vec, int nsearch, int sslot) {
+                                                           float *__restrict__ vec, int nsearch, int sslot, int nband) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TL_STAMP(0);
     TL_HWID();
+    if ((int)blockIdx.x < nband) {          // the zero band of every agent's observation
+        const size_t K = (size_t)e.B * e.N;
+        const size_t k0 = K * blockIdx.x / nband, k1 = K * (blockIdx.x + 1) / nband;
+        obs_zero_band_store(e, obs, k0, k1, threadIdx.x, blockDim.x);
+        TL_STAMP(1);
+        return;
+    }
+    const int bx = (int)blockIdx.x - nband;
     if constexpr (HOST) {
-        if ((int)blockIdx.x < nsearch) {
+        if (bx < nsearch) {
             const int wave = threadIdx.x >> 6;
             char *lds = smem + (size_t)wave * srch::wave_lds<uint32_t, 1>(e.H, e.W);
-            srch::search_items<uint32_t, 1>(e, sslot, 0, lds, blockIdx.x * (blockDim.x >> 6) + wave,
+            srch::search_items<uint32_t, 1>(e, sslot, 0, lds, bx * (blockDim.x >> 6) + wave,
                                             nsearch * (blockDim.x >> 6));
             TL_STAMP(1);
             return;
@@ -39,7 +56,7 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
         nsearch = 0;
     }
     constexpr int E = 256 / (NP * NP);
-    const int blk = (int)blockIdx.x - nsearch;
+    const int blk = bx - nsearch;
     const int b0 = blk * E;
     const int nenv = min(E, e.B - b0);
     const ObsLds L = obs_layout(e, E, smem);
@@ -49,7 +66,7 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     obs_init(e, L, E, b0, nenv, mreg);
     __syncthreads();
     TL_STAMP(2);
-    obs_emit(e, L, obs, vec, E, b0, nenv);
+    obs_emit(e, L, obs, vec, E, b0, nenv, nband > 0);
     TL_STAMP(3);
 }
 
@@ -63,16 +80,22 @@ template <int NP>
 static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot, float *obs,
                       float *vec, int nsearch, int sslot, hipStream_t s) {
     constexpr int E = 256 / (NP * NP);
-    const int grid = (e.B + E - 1) / E + nsearch;
+    // zero-band workgroups: whole float4s only, so the step workgroups' slices
+    // and the buffer must be 16-B aligned
+    int z0, z1, nband = 0;
+    const size_t slice = (size_t)E * e.N * e.C * e.F * e.F;
+    if (e.band_blocks > 0 && obs_zero_band(e, z0, z1) && (slice & 3) == 0 && ((uintptr_t)obs & 15) == 0)
+        nband = e.band_blocks;
+    const int grid = (e.B + E - 1) / E + nsearch + nband;
     size_t lds = obs_lds_bytes(e, E);
     if (nsearch > 0) {
         const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
         if (sl > lds) lds = sl;
         hipLaunchKernelGGL((step_observe_kernel<NP, true>), dim3(grid), dim3(256), lds, s, e, actions, out, flags,
-                           slot, obs, vec, nsearch, sslot);
+                           slot, obs, vec, nsearch, sslot, nband);
     } else {
         hipLaunchKernelGGL((step_observe_kernel<NP, false>), dim3(grid), dim3(256), lds, s, e, actions, out, flags,
-                           slot, obs, vec, 0, 0);
+                           slot, obs, vec, 0, 0, nband);
     }
 }
 

@@ -130,10 +130,41 @@ __device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0,
     }
 }
 
+// The config-static zero band of an agent's [C][F][F] block: channel 5
+// (human.path[1:K+1], mapf_gym.py:293-297) is written only when use_hp is on,
+// so with use_hp off every one of its floats is 0 at every step.  Returns the
+// band's float offsets [z0, z1) inside the block, or false if there is none.
+__host__ __device__ inline bool obs_zero_band(const DevEnv &e, int &z0, int &z1) {
+    if (e.use_hp || e.C < 6 || e.F * e.F > 124) return false;    // <= 31 whole float4s (32 lanes per agent)
+    z0 = 5 * e.F * e.F;
+    z1 = 6 * e.F * e.F;
+    return true;
+}
+
+// The band's whole float4s of agents [k0, k1) of `obs` (16-B aligned), written
+// as zeros by `nt` threads numbered `t`: float4 q of the buffer belongs to the
+// band iff 4q >= k*CFF + z0 and 4q + 4 <= k*CFF + z1 for its agent k.  The fused
+// launch runs this in workgroups of their own while the step's latency-bound
+// chains run in the others; obs_emit(skip_band) then skips exactly these float4s.
+__device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ obs, size_t k0, size_t k1, size_t t,
+                                           size_t nt) {
+    int z0, z1;
+    if (!obs_zero_band(e, z0, z1)) return;
+    const size_t CFF = (size_t)e.C * e.F * e.F;
+    float4 *o4 = reinterpret_cast<float4 *>(obs);
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (size_t idx = k0 * 32 + t; idx < k1 * 32; idx += nt) {      // 32 lanes per agent (a band has <= 31 float4s)
+        const size_t k = idx >> 5, j = idx & 31;
+        const size_t qa = (k * CFF + z0 + 3) >> 2, qb = (k * CFF + z1) >> 2;
+        if (qa + j < qb) o4[qa + j] = zero;
+    }
+}
+
 // Phases 1-4.  Every thread of the workgroup calls it after a __syncthreads()
-// that follows obs_init and the agents' staging.
+// that follows obs_init and the agents' staging.  skip_band: the zero band's
+// whole float4s were written by obs_zero_band_store in this launch.
 __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restrict__ obs, float *__restrict__ vec,
-                                int E, int b0, int nenv) {
+                                int E, int b0, int nenv, bool skip_band = false) {
     using namespace obsd;
     const int N = e.N, F = e.F, C = e.C, FF = F * F, CFF = C * FF;
     const int K = nenv * N;
@@ -240,11 +271,19 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     if (((E * N * CFF) & 3) == 0) {
         const size_t n4 = total >> 2;
         float4 *d4 = reinterpret_cast<float4 *>(dst);
+        int z0 = 0, z1 = 0;
+        if (!(skip_band && obs_zero_band(e, z0, z1))) z0 = z1 = 0;
+        int off = (tid * 4) % CFF;                  // float offset of float4 q inside its agent's block
+        const int step = (nt * 4) % CFF;
         for (size_t q = tid; q < n4; q += nt) {
-            const uint32_t bitpos = (uint32_t)(q << 2);
-            const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
-            d4[q] = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
-                                (float)((nib >> 3) & 1u));
+            if (!(off >= z0 && off + 4 <= z1)) {
+                const uint32_t bitpos = (uint32_t)(q << 2);
+                const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
+                d4[q] = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
+                                    (float)((nib >> 3) & 1u));
+            }
+            off += step;
+            if (off >= CFF) off -= CFF;
         }
         for (size_t q = (n4 << 2) + tid; q < total; q += nt)
             dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);

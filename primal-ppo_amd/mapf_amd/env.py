@@ -171,10 +171,13 @@ class BatchedMapfGym:
         _lib.check(_lib.lib().mapf_observe(self.h, _ptr(obs), _ptr(vec), _stream(self.device)))
         return obs, vec
 
-    def step_observe(self, actions=None, obs=None, vec=None, random_policy=False):
+    def step_observe(self, actions=None, obs=None, vec=None, random_policy=False, out=None):
         """Committed step + getAllObservations in one launch (mapf_step_observe): the same
         outputs as step() followed by observe().  random_policy: draw the actions on device
-        into `actions` first (mapf_step_observe_random).  Returns (out, obs, vec)."""
+        into `actions` first (mapf_step_observe_random).  out: optional dict of output
+        tensors (the keys of self.out, any subset; missing = not written) to write the step's
+        outputs into instead of self.out, e.g. slices of rollout buffers.
+        Returns (out, obs, vec)."""
         if actions is None:
             actions = self.actions
         obs = self.obs if obs is None else obs
@@ -183,9 +186,15 @@ class BatchedMapfGym:
         assert obs.is_contiguous() and vec.is_contiguous()
         assert obs.numel() == self.B * self.N * self.C * self.F * self.F and vec.numel() == self.B * self.N * 4
         fn = _lib.lib().mapf_step_observe_random if random_policy else _lib.lib().mapf_step_observe
-        _lib.check(fn(self.h, _ptr(actions), ctypes.byref(self._stepout), _ptr(obs), _ptr(vec),
-                      _stream(self.device)))
-        return self.out, obs, vec
+        so = self._stepout if out is None else self._make_stepout(self._check_out(out))
+        _lib.check(fn(self.h, _ptr(actions), ctypes.byref(so), _ptr(obs), _ptr(vec), _stream(self.device)))
+        return (self.out if out is None else out), obs, vec
+
+    def _check_out(self, out):
+        for k, t in out.items():
+            ref = self.out[k]
+            assert t.dtype == ref.dtype and t.is_contiguous() and t.numel() == ref.numel() and t.device == self.device, k
+        return out
 
     def flush(self):
         """Run pending search work (BFS maps, next human paths) now, in its own launch."""

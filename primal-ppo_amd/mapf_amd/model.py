@@ -93,16 +93,17 @@ class Model:
 
     # ------------------------------------------------------------ acting
     @torch.no_grad()
-    def step(self, observation, vector, input_state=None, seed=0, step=0, actions_out=None):
+    def step(self, observation, vector, input_state=None, seed=0, step=0, actions_out=None, actions32_out=None):
         """model.py:26-41 on device: returns (actions int64, ps, v, block, output_state, cv) as tensors.
-        Sampling: inverse CDF with a Philox uniform (mapf_sample_actions)."""
+        Sampling: inverse CDF with a Philox uniform (mapf_sample_actions); actions32_out: also
+        write the actions as int32 (the env's action format) in the same launch."""
         ps, v, block, _, out_state, _, cv = self.network(observation, vector, input_state)
         ps32 = ps.float().contiguous()
         if self.device.type == "cuda":
             from .env import sample_actions
             a = actions_out if actions_out is not None else torch.empty(ps32.shape[:-1], dtype=torch.int64,
                                                                          device=self.device)
-            sample_actions(ps32, seed, step, out64=a)
+            sample_actions(ps32, seed, step, out32=actions32_out, out64=a)
         else:
             a = torch.multinomial(ps32.reshape(-1, ps32.shape[-1]), 1).reshape(ps32.shape[:-1])
         return a, ps32, v.float(), block.float(), out_state, cv.float()

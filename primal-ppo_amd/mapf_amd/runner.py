@@ -4,10 +4,11 @@ The reference runs one env per Ray actor on a CPU and pickles ~3 MB per
 rollout back to the driver.  Here B environments live in HBM; every buffer of
 the rollout is a device tensor written in place:
 
+  obs[0], vec[0] <- mapf_observe
   for t in range(T):                       (runner.py:43-100)
-      obs[t], vec[t] <- mapf_observe        written straight into the buffer slice
       actions, ps, values, cost values <- policy forward + mapf_sample_actions
-      status/reward/cost/trainValid/goals/constraints <- mapf_step (COMMIT)
+      mapf_step_observe: status/reward/cost/trainValid/goals/constraints written
+      straight into the slices [t] of the buffers, obs[t+1]/vec[t+1] likewise
   last values <- policy value head on obs[T]   (:117-118)
   advantages / returns <- mapf_gae for reward and cost (:121-149)
 
@@ -81,20 +82,15 @@ class DeviceRunner:
         env.observe(self.obs[0], self.vec[0])
         for t in range(T):
             a, ps, v, _, _, cv = self.model.step(self.obs[t], self.vec[t], None, seed=self.seed,
-                                                 step=self.rollouts * T + t, actions_out=self.actions[t])
+                                                 step=self.rollouts * T + t, actions_out=self.actions[t],
+                                                 actions32_out=self.actions32)
             self.ps[t].copy_(ps.reshape(self.ps[t].shape))
             self.values[t].copy_(v.reshape(self.values[t].shape))
             self.cost_values[t].copy_(cv.reshape(self.cost_values[t].shape))
-            self.actions32.copy_(self.actions[t])
-            out = env.step(self.actions32)
-            self.rewards[t].copy_(out["reward_total"])          # reward + GOAL_REWARD (runner.py:89-91)
-            self.cost_rewards[t].copy_(out["cost"])
-            self.train_valid[t].copy_(out["train_valid"])
-            self.status[t].copy_(out["status"])
-            self.goals[t].copy_(out["goals_reached"])
-            self.constraints[t].copy_(out["constraints"])
-            self.shadow[t].copy_(out["shadow_goals"])
-            env.observe(self.obs[t + 1], self.vec[t + 1])
+            env.step_observe(self.actions32, self.obs[t + 1], self.vec[t + 1], out={
+                "reward_total": self.rewards[t],            # reward + GOAL_REWARD (runner.py:89-91)
+                "cost": self.cost_rewards[t], "train_valid": self.train_valid[t], "status": self.status[t],
+                "goals_reached": self.goals[t], "constraints": self.constraints[t], "shadow_goals": self.shadow[t]})
         last_v, last_cv = self.model.value(self.obs[T], self.vec[T], None)
         self.last_v = last_v.reshape(self.values[0].shape).contiguous()
         self.last_cv = last_cv.reshape(self.values[0].shape).contiguous()

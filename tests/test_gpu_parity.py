@@ -250,6 +250,8 @@ def run_random_case(name, case, path):
     for t in range(case["steps"]):
         if path == "fused":
             acts = env.actions
+            env.obs.fill_(float("nan"))     # every float of the observation must be written by the launch
+            env.vec.fill_(float("nan"))
             out, obs, vec = env.step_observe(acts, random_policy=True)
             out = host(out)
             a_host = acts.cpu().numpy()
@@ -357,6 +359,7 @@ def test_c2_full_size_fused_equals_two_launches():
         envs.append(e)
     fz, pl = envs
     for t in range(90):
+        fz.obs.fill_(float("nan"))          # the fused launch (incl. its zero-band workgroups) writes every float
         out_f, obs_f, vec_f = fz.step_observe(fz.actions, random_policy=True)
         out_f = host(out_f)
         out_p = host(pl.step_random(pl.actions))

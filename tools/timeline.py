@@ -31,6 +31,7 @@ def q(x):
 def main():
     B = int(os.environ.get("ENVS", "4096"))
     nsearch = int(os.environ.get("MAPF_SEARCH_BLOCKS", "64"))
+    nband = int(os.environ.get("MAPF_BAND_BLOCKS", "256"))
     env = BatchedMapfGym(make_config(B, 20, 20, num_agents=8, fov=11, num_channel=6, human_mode="random",
                                      goal_mode="random", fix_choice=1, seed=1234))
     env.reset_seeded(generate_warehouse(20, 20))
@@ -41,21 +42,24 @@ def main():
     for rep in range(3):
         env.step_observe(random_policy=True)
         torch.cuda.synchronize()
-        tl = env.timeline(nsearch + nstep).astype(np.int64)
+        tl = env.timeline(nband + nsearch + nstep).astype(np.int64)
         t0 = tl[:, 0].min()
-        s, st = tl[:nsearch], tl[nsearch:]
-        end = max(st[:, 3].max(), s[:, 1].max())
+        bd, s, st = tl[:nband], tl[nband:nband + nsearch], tl[nband + nsearch:]
+        end = max(st[:, 3].max(), s[:, 1].max(), bd[:, 1].max() if nband else 0)
         print(f"--- launch {rep}: span {(end - t0) / 100:.2f} us (first start -> last stamp)")
         print("  step starts      ", q(st[:, 0] - t0))
         print("  step (wave 0)    ", q(st[:, 1] - st[:, 0]))
         print("  barrier wait     ", q(st[:, 2] - st[:, 1]))
         print("  observe issue    ", q(st[:, 3] - st[:, 2]))
         print("  block ends       ", q(st[:, 3] - t0))
+        if nband:
+            print("  band starts      ", q(bd[:, 0] - t0))
+            print("  band blocks      ", q(bd[:, 1] - bd[:, 0]))
         print("  search starts    ", q(s[:, 0] - t0))
         print("  search blocks    ", q(s[:, 1] - s[:, 0]))
         xcc = tl[:, 7] & 0xF
         for x in np.unique(xcc):
-            m = xcc[nsearch:] == x
+            m = xcc[nband + nsearch:] == x
             print(f"  xcc {x}: {m.sum():4d} step blocks, start {(st[m, 0].min() - t0) / 100:5.2f}.."
                   f"{(st[m, 0].max() - t0) / 100:5.2f} us, end max {(st[m, 3].max() - t0) / 100:6.2f} us")
 
