@@ -753,13 +753,16 @@ void oc_debug_set(oc_env *e, int hstep, const int *prev) {
     get_good_actions(e);
 }
 
-/* Random policy used by the env-only benchmark: uniform action in {0..4}
- * from Philox (P_ACT, agent, clock, 0) -- shared spec with the device. */
+/* Random policy used by the env-only benchmark: uniform action in {0..4}.
+ * One Philox draw (P_ACT | (agent >> 3) << 8, clock, 0) per 8 agents; agent i
+ * takes 16-bit half-word i & 7 of the draw, scaled by 5 >> 16 -- shared spec
+ * with the device (mapf_common.h: random_action). */
 void oc_random_actions(const oc_env *e, int *act) {
+    uint32_t o[4];
     for (int i = 0; i < e->N; ++i) {
-        uint32_t o[4];
-        philox(e->env_id, P_ACT | ((uint32_t)i << 8), e->clock, 0, e->cfg.seed, o);
-        act[i] = (int)mulhi32(o[0], OC_NA);
+        if ((i & 7) == 0) philox(e->env_id, P_ACT | ((uint32_t)(i >> 3) << 8), e->clock, 0, e->cfg.seed, o);
+        const int k = i & 7;
+        act[i] = (int)((((o[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu) * (uint32_t)OC_NA) >> 16);
     }
 }
 

@@ -104,7 +104,6 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.repeat_cost = c.repeat_cost; d.goal_reward = c.goal_reward;
     d.env_offset = (uint32_t)c.env_offset;
     d.seed = c.seed;
-    d.maxd2 = (d.H - 1) * (d.H - 1) + (d.W - 1) * (d.W - 1);
     d.obs_envs = 64 / d.N > 1 ? 64 / d.N : 1;
     d.step_block = 256;
     d.search_blocks = 64;
@@ -116,7 +115,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     if (const char *v = std::getenv("MAPF_AGENT_LANES")) d.force_agent_lanes = std::atoi(v) != 0;
     if (d.obs_envs > d.B) d.obs_envs = d.B;
 
-    // fp64 lookup tables, computed exactly like the reference (numpy sqrt / python pow)
+    // fp64 lookup table, computed exactly like the reference (numpy sqrt)
     const double R = (double)c.penalty_radius;
     std::vector<float> cost_lut(d.R * d.R + 1);
     d.constr_d2 = -1;
@@ -126,15 +125,12 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
         cost_lut[k] = (float)(v / R);
         if (v / R >= 0.01) d.constr_d2 = k;       // monotone in k (mapf_gym.py:633)
     }
-    std::vector<double> dist_lut(d.maxd2 + 1);
-    for (int k = 0; k <= d.maxd2; ++k) dist_lut[k] = std::pow((double)k, 0.5);   // (...) ** .5 (:320)
 
     const size_t BN = (size_t)d.B * d.N;
     const size_t nmaps = d.shared_map ? 1 : (size_t)d.B;
     int rc = 0;
     uint32_t *map_bits = nullptr;
     float *cl = nullptr;
-    double *dl = nullptr;
     rc |= e->alloc(map_bits, nmaps * d.Hp * d.WW);
     rc |= e->alloc(d.pos, BN); rc |= e->alloc(d.goal, BN); rc |= e->alloc(d.last_act, BN);
     rc |= e->alloc(d.seq, BN * d.S); rc |= e->alloc(d.seq_len, BN); rc |= e->alloc(d.seq_cur, BN);
@@ -152,7 +148,6 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     uint8_t *smask = nullptr;
     rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
-    rc |= e->alloc(dl, dist_lut.size());
     if (rc) {
         std::string m = g_err;
         mapf_destroy(e);
@@ -161,9 +156,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.map_bits = map_bits;
     d.smask = smask;
     d.cost_lut = cl;
-    d.dist_lut = dl;
     if (hipMemcpy(cl, cost_lut.data(), cost_lut.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(dl, dist_lut.data(), dist_lut.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(d.counters, 0, C_NUM * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(d.prof, 0, PROF_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         mapf_destroy(e);

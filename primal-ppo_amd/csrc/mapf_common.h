@@ -46,7 +46,6 @@ struct DevEnv {
     float action_cost, collision_cost, human_collision_cost, repeat_cost, goal_reward;
     uint32_t env_offset;
     uint64_t seed;
-    int maxd2;
     int constr_d2;            // largest d2 with (R - sqrt(d2)) / R >= 0.01 in fp64 (mapf_gym.py:633)
     int obs_envs;             // envs per observe workgroup
     int step_block;           // threads per step workgroup (64..256)
@@ -68,7 +67,6 @@ struct DevEnv {
     uint32_t *counters, *replan_list, *bfs_list;
     unsigned long long *prof;  // [65536][8] per-wave phase cycles of the MAPF_STAMPS diagnostic build
     const float *cost_lut;    // [R*R+1]: float32(max(R - sqrt(d2), 0) / R) (fp64 like the reference)
-    const double *dist_lut;   // [maxd2+1]: (double)d2 ** .5 (the reference's pow, mapf_gym.py:320)
     const uint8_t *smask;     // [nmaps][H*W]: static-invalid action mask of each cell (getInvalidActions[0])
     int search_blocks;        // workgroups of the observe launch that run search work
     int band_blocks;          // workgroups of the fused launch that write the zero band (0 = none)
@@ -90,13 +88,25 @@ __device__ inline u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one v_mad_u64_u32 per product (hi and lo together), not mul_hi + mul_lo
+        const uint64_t m0 = (uint64_t)0xD2511F53u * c0, m1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(m0 >> 32), lo0 = (uint32_t)m0;
+        uint32_t hi1 = (uint32_t)(m1 >> 32), lo1 = (uint32_t)m1;
         uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
     return {c0, c1, c2, c3};
+}
+
+// Uniform random policy (the env-only benchmark's actions): one Philox draw
+// (env, P_ACT | (agent >> 3) << 8, clock, 0) serves 8 agents, agent i taking
+// 16-bit half-word i & 7 of it, scaled to 0..4.  Shared spec with
+// oracle/mapf_oracle.c: oc_random_actions().
+__host__ __device__ inline int random_action(const u32x4 &o, int i) {
+    const int k = i & 7;
+    const uint32_t w = (k >> 1) == 0 ? o.x : (k >> 1) == 1 ? o.y : (k >> 1) == 2 ? o.z : o.w;
+    return (int)((((w >> ((k & 1) * 16)) & 0xFFFFu) * (uint32_t)NA) >> 16);
 }
 
 // Obstacle test on the padded bitmap (off-map cells read as 1 within P cells).
@@ -160,5 +170,23 @@ __device__ inline uint64_t shfl64(uint64_t v, int src) {
     uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
     return ((uint64_t)hi << 32) | lo;
 }
+
+// The padded obstacle bitmap of a shared map held in registers: lane k of the
+// wave holds word k (needs Hp*WW <= 64).  Tests are ds_bpermute reads of
+// another lane, not HBM loads -- a step running while the chip streams
+// observation stores would wait microseconds per loaded word.  Call only with
+// every lane of the wave active (the source lanes must execute the permute).
+struct RegMap {
+    uint32_t w;
+    bool on;
+    __device__ bool obstacle(const DevEnv &e, const uint32_t *bits, int r, int c) const {
+        if (!on) return obstacle_at(e, bits, r, c);
+        const bool off = r < -e.P || r >= e.H + e.P || c < -e.P || c >= e.W + e.P;
+        const int rr = off ? 0 : r + e.P, cc = off ? 0 : c + e.P;
+        const uint32_t word = shfl32(w, rr * e.WW + (cc >> 5));     // every lane permutes
+        return off || ((word >> (cc & 31)) & 1u);
+    }
+};
+__host__ __device__ inline bool regmap_fits(const DevEnv &e) { return e.shared_map && e.Hp * e.WW <= 64; }
 
 }  // namespace mapf

@@ -60,13 +60,23 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     const int b0 = blk * E;
     const int nenv = min(E, e.B - b0);
     const ObsLds L = obs_layout(e, E, smem);
-    const uint32_t mreg = obs_map_word(e, b0, nenv, threadIdx.x);     // issued before the step's loads
-    step_pairs_env<NP, true>(e, actions, out, flags, slot, blk * 256 + (int)threadIdx.x, L, b0);
+    // the map words are loaded before the step's loads; at NP = 8 every wave holds
+    // the whole shared map (lane k = word k) and the step reads it from registers
+    const bool regmap = NP == 8 && regmap_fits(e);
+    const uint32_t mreg = obs_map_word(e, b0, nenv, regmap ? (int)(threadIdx.x & 63) : (int)threadIdx.x);
+    PairsDeferred dfr;
+#ifdef MAPF_DIAG_NOSTEP   // timing diagnostic only (make diag): observe the pre-step state, no step
+    obs_load_agents(e, L, b0, nenv);
+#else
+    step_pairs_env<NP, true>(e, actions, out, flags, slot, blk * 256 + (int)threadIdx.x, L, b0,
+                             RegMap{mreg, regmap}, dfr);
+#endif
     TL_STAMP(1);
     obs_init(e, L, E, b0, nenv, mreg);
     __syncthreads();
     TL_STAMP(2);
     obs_emit(e, L, obs, vec, E, b0, nenv, nband > 0);
+    step_pairs_finish(e, dfr, slot);
     TL_STAMP(3);
 }
 

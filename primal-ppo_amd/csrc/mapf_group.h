@@ -76,13 +76,13 @@ __device__ bool group_free_cell(const DevEnv &e, uint32_t env_id, uint32_t purpo
 // human's world (entrance marked) from the entrance; mode 2: the next scripted
 // pose from the current one; mode 0 (LoopingHuman) never switches.
 __device__ inline void plan_next_path(const DevEnv &e, int b, uint32_t env_id, uint32_t epoch, int seq_idx,
-                                      uint32_t &nstart, uint32_t &ngoal, bool leader) {
+                                      uint32_t &nstart, uint32_t &ngoal, bool leader, RegMap rm = RegMap{0u, false}) {
     nstart = NO_CELL;
     ngoal = NO_CELL;
     if (e.human_mode == 1) {
         const uint32_t ent = e.hentr[b];
         const uint32_t *bits = env_map(e, b);
-        auto ok = [&](int r, int c) -> bool { return !obstacle_at(e, bits, r, c) && pack(r, c) != ent; };
+        auto ok = [&](int r, int c) -> bool { return !rm.obstacle(e, bits, r, c) && pack(r, c) != ent; };
         int r, c;
         if (group_free_cell(e, env_id, P_HGOAL, 0, epoch, ok, r, c)) { nstart = ent; ngoal = pack(r, c); }
         else if (leader) atomicAdd(&e.counters[C_FREECELL], 1u);

@@ -226,23 +226,27 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         }
     }
 
-    // ---- phase 3: per agent ----
-    for (int k = tid; k < K; k += nt) {
-        const int le = k / N;
+    // ---- phase 3: (agent k, agent j of its env) pairs, one lane each ----
+    // j != k: visibleAgents -> agent j's goal clamped to k's FOV (ch3, :302-308);
+    // j == k: own goal (ch2), human next position (ch4), HP cells (ch5), vector.
+    for (int task = tid; task < K * N; task += nt) {
+        const int k = task / N, j = task - k * N;
+        const int le = k / N, i = k - le * N;
         const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
         const int tr = pr - half, tc = pc - half;
         const int base = k * CFF;
+        if (j != i) {
+            const int kj = le * N + j;
+            const int rj = prow(L.spos[kj]), cj = pcol(L.spos[kj]);
+            if (rj >= tr && rj < tr + F && cj >= tc && cj < tc + F) {
+                const int xr = min(max(prow(L.sgoal[kj]), tr), tr + F - 1);
+                const int xc = min(max(pcol(L.sgoal[kj]), tc), tc + F - 1);
+                set_bit(stream, base + 3 * FF + (xr - tr) * F + (xc - tc));
+            }
+            continue;
+        }
         const int gr = prow(L.sgoal[k]), gc = pcol(L.sgoal[k]);
         if (tr <= gr && gr < tr + F && tc <= gc && gc < tc + F) set_bit(stream, base + 2 * FF + (gr - tr) * F + (gc - tc));
-        for (int j = 0; j < N; ++j) {               // visibleAgents -> clamped goals (:302-308)
-            const int kj = le * N + j;
-            if (kj == k) continue;
-            const int rj = prow(L.spos[kj]), cj = pcol(L.spos[kj]);
-            if (rj < tr || rj >= tr + F || cj < tc || cj >= tc + F) continue;
-            const int xr = min(max(prow(L.sgoal[kj]), tr), tr + F - 1);
-            const int xc = min(max(pcol(L.sgoal[kj]), tc), tc + F - 1);
-            set_bit(stream, base + 3 * FF + (xr - tr) * F + (xc - tc));
-        }
         const uint32_t hn = L.shn[le];
         const int hr = prow(hn), hc = pcol(hn);
         if (tr <= hr && hr < tr + F && tc <= hc && hc < tc + F) set_bit(stream, base + 4 * FF + (hr - tr) * F + (hc - tc));
@@ -251,19 +255,21 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             const int r = prow(cell), c = pcol(cell);
             if (tr <= r && r < tr + F && tc <= c && c < tc + F) set_bit(stream, base + 5 * FF + (r - tr) * F + (c - tc));
         }
-        // vector (:316-323)
+        // vector (:316-323): d = (dx^2 + dy^2) ** .5 in float64 -- the correctly
+        // rounded sqrt equals Python's pow(x, .5) for every x >= 0 (no table load)
         const int dx = gr - pr, dy = gc - pc;
         const int d2 = dx * dx + dy * dy;
         float4 v;
         if (d2 == 0) {
             v = make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-            const double d = e.dist_lut[d2];
+            const double d = __builtin_sqrt((double)d2);
             v = make_float4((float)((double)dx / d), (float)((double)dy / d), (float)d, 0.f);
         }
         reinterpret_cast<float4 *>(vec)[(size_t)b0 * N + k] = v;
     }
     __syncthreads();
+    TL_STAMP(4);
 
     // ---- phase 4: bit-stream -> float stores ----
     const size_t total = (size_t)K * CFF;

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     int a = 0;
     if (flags & 2u) {          // random policy fused in: same stream as random_actions_kernel
         if (act) {
-            a = (int)__umulhi(philox(env_id, P_ACT | ((uint32_t)i << 8), clock, 0u, e.seed).x, (uint32_t)NA);
+            a = random_action(philox(env_id, P_ACT | ((uint32_t)(i >> 3) << 8), clock, 0u, e.seed), i);
             actions[ai] = a;
         }
     } else if (act) {
@@ -335,13 +335,13 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
     STAMP_END();
 }
 
-// Uniform random policy: counter (env, P_ACT | agent << 8, clock, 0).
+// Uniform random policy (random_action(): one Philox draw per 8 agents).
 __global__ __launch_bounds__(256) void random_actions_kernel(DevEnv e, int32_t *__restrict__ actions) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= e.B * e.N) return;
     const int b = t / e.N, i = t - b * e.N;
-    const u32x4 o = philox(e.env_offset + (uint32_t)b, P_ACT | ((uint32_t)i << 8), e.clock[b], 0u, e.seed);
-    actions[t] = (int32_t)__umulhi(o.x, (uint32_t)NA);
+    const u32x4 o = philox(e.env_offset + (uint32_t)b, P_ACT | ((uint32_t)(i >> 3) << 8), e.clock[b], 0u, e.seed);
+    actions[t] = (int32_t)random_action(o, i);
 }
 
 void launch_step(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int parity, hipStream_t s) {

@@ -49,18 +49,48 @@ __device__ inline uint32_t row_or(uint32_t v) {
 
 }  // namespace pairs
 
+// Work-list appends whose slot comes from a returning atomic (one wave-aggregated
+// atomicAdd per list).  The step only issues the atomic; step_pairs_finish()
+// reads its result and stores the items as late as the caller can (the fused
+// kernel: after the observation stores), so no wave waits on the round trip.
+struct PairsDeferred {
+    uint64_t bmask = 0, rmask = 0;     // lanes appending to bfs_list / replan_list
+    uint32_t bret = 0, rret = 0;       // the leader lane's atomicAdd result
+    uint32_t bitem = 0, ritem = 0;
+};
+
+__device__ inline void step_pairs_finish(const DevEnv &e, const PairsDeferred &d, int slot) {
+    const int lane = lane_id();
+    if (d.bmask) {
+        const uint32_t base = __builtin_amdgcn_readlane(d.bret, __builtin_ctzll(d.bmask));
+        if ((d.bmask >> lane) & 1ull)
+            e.bfs_list[(size_t)slot * e.B * e.N + base + __popcll(d.bmask & ((1ull << lane) - 1ull))] = d.bitem;
+    }
+    if (d.rmask) {
+        const uint32_t base = __builtin_amdgcn_readlane(d.rret, __builtin_ctzll(d.rmask));
+        if ((d.rmask >> lane) & 1ull)
+            e.replan_list[(size_t)slot * e.B + base + __popcll(d.rmask & ((1ull << lane) - 1ull))] = d.ritem;
+    }
+}
+
 // One env's step on its NP*NP lanes; `gt` = the lane's index among the step
 // lanes of the launch (env = gt / (NP*NP)).  FEED: also hand the post-step
 // cells, goals and human state to the workgroup's observation (LDS `ob`,
 // whose first env is b0) -- the fused step+observe kernel; needs COMMIT.
+//
+// rm: the shared map in registers (NP = 8 only: one env per wave, so every
+// lane takes part in each map read); dfr: the deferred list appends.
 template <int NP, bool FEED>
 __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out,
-                                               uint32_t flags, int slot, int gt, const ObsLds &ob, int b0) {
+                                               uint32_t flags, int slot, int gt, const ObsLds &ob, int b0,
+                                               RegMap rm, PairsDeferred &dfr) {
     using namespace pairs;
     constexpr int L = NP * NP;
     constexpr uint32_t ROW = (1u << NP) - 1u;
     const int N = e.N;
-    const int b = gt / L;
+    // one env per wave at NP = 8: make the env index (and everything derived from
+    // per-env loads) wave-uniform, i.e. scalar registers / SALU, not 64 VALU lanes
+    const int b = (L == 64) ? __builtin_amdgcn_readfirstlane(gt / L) : gt / L;
     if (gt == 0 && (flags & 1u)) {
         e.counters[C_REPLAN_COUNT + (slot + 1) % 3] = 0;
         e.counters[C_BFS_COUNT + (slot + 1) % 3] = 0;
@@ -84,6 +114,11 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t env_id = e.env_offset + (uint32_t)b;
     // ---- every per-env / per-agent load is issued here, in two dependent rounds
     const uint32_t clock = e.clock[b];
+    // calculateCostReward's table (cost_lut[d2], d2 <= R*R) in lanes: lane k holds
+    // entry k, read with one permute instead of an fp64 sqrt + divide per lane
+    const int RR = e.R * e.R;
+    const bool lutreg = L == 64 && RR < 64;      // one env per wave: every lane is active
+    const float creg = lutreg ? e.cost_lut[lane_id() <= RR ? lane_id() : 0] : 0.f;
     const uint32_t hp = e.hpos[b], hn = e.hnext[b];
     const int hs = e.hstep[b], hcur = e.hcur[b];
     const int2 hlen2 = *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
@@ -95,14 +130,15 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t gi = vi ? e.goal[ai] : 0u;
     const int la = vi ? (int)e.last_act[ai] : -1;
     int a_i, a_j;
-    if (flags & 2u) {                       // random policy: lane (k, 0) draws agent k's action
-        int mine = 0;
-        if (vi && head) {
-            mine = (int)__umulhi(philox(env_id, P_ACT | ((uint32_t)i << 8), clock, 0u, e.seed).x, (uint32_t)NA);
-            actions[ai] = mine;
-        }
-        a_i = (int)shfl32((uint32_t)mine, base + i * NP);
-        a_j = (int)shfl32((uint32_t)mine, base + j * NP);
+    if (flags & 2u) {                       // random policy: one env-uniform Philox draw for all N <= 8 agents
+#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 1)    // timing diagnostic only
+        const u32x4 o = {clock * 0x9E3779B9u + env_id, clock ^ env_id, clock + 7u, env_id * 3u};
+#else
+        const u32x4 o = philox(env_id, P_ACT, clock, 0u, e.seed);
+#endif
+        a_i = random_action(o, i);
+        a_j = random_action(o, j);
+        if (vi && head) actions[ai] = a_i;
     } else {
         a_i = vi ? actions[ai] : 0;
         a_j = vj ? actions[aj] : 0;
@@ -127,7 +163,15 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t *p2 = human_path(e, b, cur2);
     const uint32_t hp_new = p2[hs2];
     const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
-    const unsigned st_mask = vi ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + ri * e.W + ci] : 0x1Fu;
+    unsigned st_mask = 0x1Fu;
+    if (rm.on) {                            // getInvalidActions' static list from the register map
+        unsigned m = 0;
+#pragma unroll
+        for (int k = 1; k < NA; ++k) m |= (unsigned)rm.obstacle(e, nullptr, ri + dr(k), ci + dc(k)) << k;
+        if (vi) st_mask = m;
+    } else if (vi) {
+        st_mask = (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + ri * e.W + ci];
+    }
     unsigned hu_mask = 0;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
@@ -186,7 +230,12 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     {   // max(R - ||h - x||, 0) / R in float64, then float32 (mapf_gym.py:513-526)
         const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
         const int d2 = d0 * d0 + d1 * d1;
-        if (d2 < e.R * e.R) cost = (float)(((double)e.R - sqrt((double)d2)) / (double)e.R);
+        if (lutreg) {
+            const float c = __shfl(creg, d2 < RR ? d2 : 0, 64);    // every lane permutes
+            cost = d2 < RR ? c : 0.f;
+        } else if (d2 < RR) {
+            cost = (float)(((double)e.R - sqrt((double)d2)) / (double)e.R);
+        }
     }
     if (vi) {
         if (head) {
@@ -206,7 +255,11 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
 
     // ---- fixActions (worklist; agent values row-replicated, j's copies in column)
     int fixed = a_i;
+#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 2)    // timing diagnostic only
+    const uint32_t need = 0;
+#else
     const uint32_t need = agents_of(eballot(head && vi && (st == -1 || st == -2 || st == -3)));
+#endif
     if (need) {
         const int st_j = (int)shfl32((uint32_t)st, base + j * NP);
         int asg_i = (vi && st == 1) ? a_i : -1;
@@ -276,6 +329,10 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t np = vi ? pack(nr, nc) : 0xFFFFFFFFu;
     const bool reached = vi && e.lifelong && np == gi;
     uint32_t ng = gi;
+#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 4)    // timing diagnostic only
+    if (true) {
+    } else
+#endif
     if (e.goal_mode == 0) {
         if (reached && head) {
             int cur = e.seq_cur[ai];
@@ -293,7 +350,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
             const uint32_t mygoal = ng;
             const uint32_t *bits = env_map(e, b);
             auto ok = [&](int r, int c) -> bool {
-                if (obstacle_at(e, bits, r, c)) return false;
+                if (rm.obstacle(e, bits, r, c)) return false;
                 const uint32_t cell = pack(r, c);
                 return eballot(head && vi && (mypos == cell || mygoal == cell)) == 0ull;
             };
@@ -310,9 +367,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
         e.pos[ai] = np;
         e.goal[ai] = ng;
         e.last_act[ai] = (int8_t)fixed;
-        if (reached && e.keep_bfs) {
-            const uint32_t sl = atomicAdd(&e.counters[C_BFS_COUNT + slot], 1u);
-            e.bfs_list[(size_t)slot * e.B * N + sl] = (uint32_t)ai;
+    }
+    if (e.keep_bfs) {                       // agent.bfsMap recompute (makeBfsMap on goal change, :627)
+        const uint64_t bm = __ballot(vi && head && reached);
+        if (bm) {
+            if (lane == __builtin_ctzll(bm)) dfr.bret = atomicAdd(&e.counters[C_BFS_COUNT + slot], (uint32_t)__popcll(bm));
+            dfr.bmask = bm;
+            dfr.bitem = (uint32_t)ai;
         }
     }
     STAMP(4);
@@ -330,14 +391,16 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     }
     if (swapped) {
         uint32_t ns, ngl;
-        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0);
+        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0, rm);
         if (li == 0) {
             e.hnext_start[b] = ns;
             e.hnext_goal[b] = ngl;
-            if (ngl != NO_CELL) {
-                const uint32_t sl = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], 1u);
-                e.replan_list[(size_t)slot * e.B + sl] = (uint32_t)b;
-            }
+        }
+        const uint64_t rmk = __ballot(li == 0 && ngl != NO_CELL);
+        if (rmk) {
+            if (lane == __builtin_ctzll(rmk)) dfr.rret = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], (uint32_t)__popcll(rmk));
+            dfr.rmask = rmk;
+            dfr.ritem = (uint32_t)b;
         }
     }
     if (li == 0) {

@@ -7,7 +7,10 @@ namespace mapf {
 template <int NP>
 __global__ __launch_bounds__(256) void step_pairs_kernel(DevEnv e, int32_t *__restrict__ actions, StepOut out,
                                                          uint32_t flags, int slot) {
-    step_pairs_env<NP, false>(e, actions, out, flags, slot, blockIdx.x * blockDim.x + threadIdx.x, ObsLds{}, 0);
+    PairsDeferred dfr;
+    step_pairs_env<NP, false>(e, actions, out, flags, slot, blockIdx.x * blockDim.x + threadIdx.x, ObsLds{}, 0,
+                              RegMap{0u, false}, dfr);
+    step_pairs_finish(e, dfr, slot);
 }
 
 bool launch_step_pairs(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,

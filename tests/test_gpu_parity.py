@@ -426,3 +426,28 @@ def test_sample_actions_distribution():
     b = torch.zeros(M, dtype=torch.int64, device="cuda")
     sample_actions(p, 99, 3, out64=b)
     assert torch.equal(a.long(), b)
+
+
+def test_vector_every_offset_on_80x80():
+    """observe's vector [dx/d, dy/d, d, 0], d = (dx^2 + dy^2) ** .5 in float64
+    (mapf_gym.py:316-323), for EVERY goal offset (dx, dy) in [0, 79]^2 of an
+    80x80 grid: the device's fp64 sqrt + divides must equal Python's pow / divide
+    bit for bit (the kernel has no distance table)."""
+    B, N, H = 100, 64, 80
+    env = mk_env(B=B, H=H, W=H, num_agents=N, fov=11, num_channel=6, human_mode="looping", goal_mode="random",
+                 fix_choice=1, shared_map=True, seed=3, keep_bfs=False)
+    env.reset_seeded(np.zeros((H, H), np.int8))
+    idx = np.arange(B * N)
+    dx, dy = idx // H, idx % H
+    pos = np.zeros((B, N, 2), np.int32)
+    goal = np.stack([dx, dy], -1).reshape(B, N, 2).astype(np.int32)
+    env.set_state(pos=pos, goal=goal)
+    _, vec = env.observe()
+    got = vec.cpu().numpy().reshape(-1, 4)
+    want = np.zeros_like(got)
+    for k in range(B * N):
+        d2 = int(dx[k]) ** 2 + int(dy[k]) ** 2
+        if d2:
+            d = d2 ** .5
+            want[k] = [np.float32(dx[k] / d), np.float32(dy[k] / d), np.float32(d), 0.0]
+    np.testing.assert_array_equal(got, want)

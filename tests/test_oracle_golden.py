@@ -136,3 +136,25 @@ def test_runner_buffer_contract():
     assert tuple(z["valid_shape"]) == (256, 2, 5)
     assert tuple(z["ps_shape"]) == (256, 2, 5)
     assert str(z["actions_dtype"]) == "int64"
+
+
+def test_random_policy_stream_is_uniform():
+    """The env-only benchmark's random policy (oracle oc_random_actions == device
+    random_action: one Philox draw per 8 agents, 16-bit half-words scaled by 5):
+    frequencies of the 5 actions over 2,000 steps x 12 agents are ~0.2 each and
+    agents 0..7 / 8..11 (two draws) are not identical streams."""
+    from mapf_amd.maps import generate_warehouse
+    world = generate_warehouse(20, 20)
+    cfg = O.make_config(20, 20, 12, 11, 6, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
+    oe = O.OracleEnv(cfg, env_id=3)
+    oe.reset_random(world)
+    acts = []
+    for _ in range(2000):
+        a = oe.random_actions()
+        acts.append(a)
+        oe.step(a)
+    acts = np.array(acts)
+    freq = np.bincount(acts.ravel(), minlength=5) / acts.size
+    assert acts.min() >= 0 and acts.max() <= 4
+    np.testing.assert_allclose(freq, 0.2, atol=0.015)
+    assert not np.array_equal(acts[:, 0], acts[:, 8])

@@ -39,8 +39,10 @@ def main():
         env.step_observe(random_policy=True)
     torch.cuda.synchronize()
     nstep = (B + 3) // 4
+    b2b = int(os.environ.get("BACK2BACK", "1"))    # launches back to back; the last one is recorded
     for rep in range(3):
-        env.step_observe(random_policy=True)
+        for _ in range(b2b):
+            env.step_observe(random_policy=True)
         torch.cuda.synchronize()
         tl = env.timeline(nband + nsearch + nstep).astype(np.int64)
         t0 = tl[:, 0].min()
@@ -50,7 +52,8 @@ def main():
         print("  step starts      ", q(st[:, 0] - t0))
         print("  step (wave 0)    ", q(st[:, 1] - st[:, 0]))
         print("  barrier wait     ", q(st[:, 2] - st[:, 1]))
-        print("  observe issue    ", q(st[:, 3] - st[:, 2]))
+        print("  obs phases 1-3   ", q(st[:, 4] - st[:, 2]))
+        print("  obs stores issue ", q(st[:, 3] - st[:, 4]))
         print("  block ends       ", q(st[:, 3] - t0))
         if nband:
             print("  band starts      ", q(bd[:, 0] - t0))
