@@ -32,6 +32,7 @@ namespace mapf {
 struct ObsLds {
     uint32_t *stream, *occ, *mapc, *spos, *sgoal, *shn, *shp;
     int32_t *shpn;
+    uint8_t *idg;               // [E][H*W] agent index at each occupied cell (read only where occ is set)
     int stream_words, rowsz;
 };
 
@@ -42,7 +43,7 @@ __host__ __device__ inline size_t obs_lds_bytes(const DevEnv &e, int E) {
     const int nmap = e.shared_map ? 1 : E;
     const size_t words = ((obs_stream_words(e, E) + 3) & ~3) + (size_t)E * rowsz + (size_t)nmap * rowsz +
                          2 * (size_t)E * e.N + E + (size_t)E * e.k_predict + E;
-    return words * 4;
+    return words * 4 + (((size_t)E * e.H * e.W + 3) & ~(size_t)3);
 }
 
 __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
@@ -58,6 +59,7 @@ __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
     L.shn = L.sgoal + E * e.N;                  // [E] human next
     L.shp = L.shn + E;                          // [E][k_predict] human.path[1..K]
     L.shpn = reinterpret_cast<int32_t *>(L.shp + E * e.k_predict);   // [E] count
+    L.idg = reinterpret_cast<uint8_t *>(L.shpn + E);
     return L;
 }
 
@@ -172,11 +174,14 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     const int tid = threadIdx.x, nt = blockDim.x;
     uint32_t *stream = L.stream;
 
-    // ---- phase 1: worldWithAgents as a padded bitmap per env ----
+    // ---- phase 1: worldWithAgents as a padded bitmap per env + agent index grid ----
+    const int HW = e.H * e.W;
     for (int k = tid; k < K; k += nt) {
         const int le = k / N;
-        const int rr = prow(L.spos[k]) + e.P, cc = pcol(L.spos[k]) + e.P;
+        const int r = prow(L.spos[k]), c = pcol(L.spos[k]);
+        const int rr = r + e.P, cc = c + e.P;
         atomicOr(&L.occ[le * rowsz + rr * e.WW + (cc >> 5)], 1u << (cc & 31));
+        L.idg[le * HW + r * e.W + c] = (uint8_t)(k - le * N);
     }
     __syncthreads();
 
@@ -198,6 +203,14 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         const int base = k * CFF + y * F;
         or_bits(stream, base, seg0 | self, F);
         or_bits(stream, base + FF, segA & ~self, F);
+        // visibleAgents (the agents of this FOV row) -> their goals clamped to the FOV (ch3, :302-308)
+        for (uint32_t others = segA & ~self; others; others &= others - 1u) {
+            const int cc = tc + __builtin_ctz(others);
+            const int kj = le * N + L.idg[le * HW + rr * e.W + cc];
+            const int xr = min(max(prow(L.sgoal[kj]), tr), tr + F - 1);
+            const int xc = min(max(pcol(L.sgoal[kj]), tc), tc + F - 1);
+            set_bit(stream, k * CFF + 3 * FF + (xr - tr) * F + (xc - tc));
+        }
         if (e.use_da && rr >= 0 && rr < e.H) {      // ch4 danger area (mapf_gym.py:289-290)
             const uint32_t hn = L.shn[le];
             const int dy = prow(hn) - rr;
@@ -213,38 +226,35 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         if (C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
             const size_t ai = (size_t)b0 * N + k;
             const int16_t *bm = e.bfs + ai * e.H * e.W;
+            const int16_t *row = bm + rr * e.W;
             const int own = bm[pr * e.W + pc];
+            // the row's loads all issued before any is used (one HBM latency, not F)
+            int16_t v[16];
+#pragma unroll
+            for (int x = 0; x < 16; ++x) v[x] = x < F ? row[min(max(tc + x, 0), e.W - 1)] : (int16_t)-1;
             uint32_t m = 0;
-            if (own >= 0)
-                for (int x = 0; x < F; ++x) {
-                    const int cc = tc + x;
-                    if (cc < 0 || cc >= e.W) continue;
-                    const int v = bm[rr * e.W + cc];
-                    if (v >= 0 && v < own) m |= 1u << x;
-                }
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = tc + x;
+                if (x < F && cc >= 0 && cc < e.W && v[x] >= 0 && v[x] < own) m |= 1u << x;
+            }
+            for (int x = 16; x < F; ++x) {
+                const int cc = tc + x;
+                if (cc < 0 || cc >= e.W) continue;
+                const int w = row[cc];
+                if (w >= 0 && w < own) m |= 1u << x;
+            }
+            if (own < 0) m = 0;
             or_bits(stream, base + 6 * FF, m, F);
         }
     }
 
-    // ---- phase 3: (agent k, agent j of its env) pairs, one lane each ----
-    // j != k: visibleAgents -> agent j's goal clamped to k's FOV (ch3, :302-308);
-    // j == k: own goal (ch2), human next position (ch4), HP cells (ch5), vector.
-    for (int task = tid; task < K * N; task += nt) {
-        const int k = task / N, j = task - k * N;
-        const int le = k / N, i = k - le * N;
+    // ---- phase 3: per agent: own goal (ch2), human next position (ch4), HP cells (ch5), vector ----
+    for (int k = tid; k < K; k += nt) {
+        const int le = k / N;
         const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
         const int tr = pr - half, tc = pc - half;
         const int base = k * CFF;
-        if (j != i) {
-            const int kj = le * N + j;
-            const int rj = prow(L.spos[kj]), cj = pcol(L.spos[kj]);
-            if (rj >= tr && rj < tr + F && cj >= tc && cj < tc + F) {
-                const int xr = min(max(prow(L.sgoal[kj]), tr), tr + F - 1);
-                const int xc = min(max(pcol(L.sgoal[kj]), tc), tc + F - 1);
-                set_bit(stream, base + 3 * FF + (xr - tr) * F + (xc - tc));
-            }
-            continue;
-        }
         const int gr = prow(L.sgoal[k]), gc = pcol(L.sgoal[k]);
         if (tr <= gr && gr < tr + F && tc <= gc && gc < tc + F) set_bit(stream, base + 2 * FF + (gr - tr) * F + (gc - tc));
         const uint32_t hn = L.shn[le];

@@ -24,11 +24,12 @@
 // Register-only BFS.  Grid rows live on the lanes (row r = lane + 64k, k < RW),
 // each row a W-bit mask (u32 / u64 / 2 x u64).  One BFS level = one frontier
 // dilation: horizontal neighbours by shifting the row, vertical neighbours by
-// DPP wave_shr:1 / wave_shl:1.  Distances are accumulated as K bit planes
-// (plane k holds bit k of every visited cell's distance) -- no memory traffic
-// inside the loop.  The walk-back needs only d mod 4: the grid graph is
-// bipartite, so two adjacent reachable cells differ by exactly one level and
-// "d(p) == d(c) - 1" <=> p visited and d(p) = d(c) - 1 (mod 4).
+// DPP wave_shr:1 / wave_shl:1.  A BFS map is written level by level into a
+// per-wave LDS image (each lane stores the few cells its row gains at that
+// level), then swept out coalesced.  The A* walk-back needs only d mod 4, kept
+// as 2 bit planes in registers: the grid graph is bipartite, so two adjacent
+// reachable cells differ by exactly one level and "d(p) == d(c) - 1" <=> p
+// visited and d(p) = d(c) - 1 (mod 4).
 #pragma once
 #include "mapf_common.h"
 
@@ -70,6 +71,13 @@ template <> __device__ inline uint32_t r_bit<uint32_t>(int c) { return 1u << c; 
 template <> __device__ inline uint64_t r_bit<uint64_t>(int c) { return 1ull << c; }
 template <> __device__ inline Row2 r_bit<Row2>(int c) { return c < 64 ? Row2{1ull << c, 0} : Row2{0, 1ull << (c - 64)}; }
 template <class T> __device__ inline T r_zero() { return T{}; }
+// lowest set column / clear it
+__device__ inline int r_ctz(uint32_t a) { return __builtin_ctz(a); }
+__device__ inline int r_ctz(uint64_t a) { return __builtin_ctzll(a); }
+__device__ inline int r_ctz(Row2 a) { return a.lo ? __builtin_ctzll(a.lo) : 64 + __builtin_ctzll(a.hi); }
+__device__ inline uint32_t r_pop(uint32_t a) { return a & (a - 1u); }
+__device__ inline uint64_t r_pop(uint64_t a) { return a & (a - 1ull); }
+__device__ inline Row2 r_pop(Row2 a) { return a.lo ? Row2{a.lo & (a.lo - 1ull), a.hi} : Row2{0ull, a.hi & (a.hi - 1ull)}; }
 
 // lane i <- lane i-1 (DPP wave_shr:1) / lane i <- lane i+1 (wave_shl:1); edge lanes read 0
 __device__ inline uint32_t from_below(uint32_t x) {
@@ -115,11 +123,6 @@ template <> __device__ inline Row2 free_row<Row2>(const DevEnv &e, const uint32_
     if (e.W < 128) f.hi &= (1ull << (e.W - 64)) - 1;
     return f;
 }
-
-template <class T> struct Kbits;   // distance bit planes: max distance < cells <= 64*RW*width
-template <> struct Kbits<uint32_t> { static constexpr int v = 12; };
-template <> struct Kbits<uint64_t> { static constexpr int v = 13; };
-template <> struct Kbits<Row2> { static constexpr int v = 14; };
 
 // Level-synchronous BFS over free cells from (sr, sc).  V = visited rows,
 // D[k] = bit k of each visited cell's distance.  Stops after the level that
@@ -167,6 +170,50 @@ __device__ int bfs_planes(const T (&fre)[RW], int sr, int sc, int stop_r, int st
     }
 }
 
+// makeBfsMap straight into an LDS image: `img` holds the map's -1 / -2 cells
+// (obstacle / free); the start cell gets 0 and every cell reached at level d gets
+// d, written by the lane holding its row as the level is found (a frontier row
+// has few cells) -- no distance bit planes to maintain or decode.
+template <class T, int RW>
+__device__ void bfs_to_img(const T (&fre)[RW], int sr, int sc, int16_t *img, int W) {
+    const int lane = lane_id();
+    T fr[RW], V[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        fr[k] = (lane + 64 * k == sr) ? r_bit<T>(sc) : r_zero<T>();
+        V[k] = fr[k];
+    }
+    if ((sr & 63) == lane) img[sr * W + sc] = 0;
+    for (int d = 1;; ++d) {
+        T up[RW], dn[RW], nw[RW];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) { up[k] = from_below(fr[k]); dn[k] = from_above(fr[k]); }
+        if (RW == 2) {
+            const T a = rdlane(fr[0], 63), b = rdlane(fr[RW - 1], 0);
+            if (lane == 0) up[RW - 1] = a;      // row 64 <- row 63
+            if (lane == 63) dn[0] = b;          // row 63 <- row 64
+        }
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            nw[k] = r_andn(r_and(r_or(r_or(r_nb(fr[k]), up[k]), dn[k]), fre[k]), V[k]);
+            any |= r_any(nw[k]);
+        }
+        if (__ballot(any) == 0ull) return;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            V[k] = r_or(V[k], nw[k]);
+            fr[k] = nw[k];
+            const int r = lane + 64 * k;
+            for (T m = nw[k]; r_any(m); m = r_pop(m)) img[r * W + r_ctz(m)] = (int16_t)d;
+        }
+    }
+}
+
+// distance bit planes of the narrow-row BFS map (W <= 32: 12 planes cover any
+// distance < 64 * 32 cells)
+constexpr int KNARROW = 12;
+
 // bit c of the row held by lane `ln` in slot `sl` (ln, sl, c wave-uniform): a v_readlane
 __device__ inline uint32_t word_of(uint32_t x, int) { return x; }
 __device__ inline uint32_t word_of(uint64_t x, int w) { return w ? (uint32_t)(x >> 32) : (uint32_t)x; }
@@ -193,7 +240,6 @@ __host__ __device__ inline size_t wave_lds(int H, int W) {
 //   agent's BFS map; 2: every env's next path only.
 template <class T, int RW>
 __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, uint32_t wave_id, uint32_t nwaves) {
-    constexpr int K = Kbits<T>::v;
     const int lane = lane_id();
     const int W = e.W, H = e.H, cells = H * W;
     const uint32_t n_replan = all ? (uint32_t)e.B : e.counters[C_REPLAN_COUNT + parity];
@@ -215,31 +261,46 @@ __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, ui
             sr_cell = e.goal[ai];
         }
         const uint32_t *bits = env_map(e, b);
-        T fre[RW], V[RW], D[K][RW];
+        T fre[RW];
 #pragma unroll
         for (int k = 0; k < RW; ++k) fre[k] = free_row<T>(e, bits, lane + 64 * k);
         const int sr = prow(sr_cell), sc = pcol(sr_cell);
         if (!replan) {
-            const int maxd = bfs_planes<T, RW, K>(fre, sr, sc, -1, -1, V, D);
-            const int kq = 32 - __builtin_clz((unsigned)maxd | 1u);   // planes in use
-            // decode each row's distances into the LDS image, then one coalesced sweep out
+            // the map copy (-1 obstacle / -2 free), then the BFS levels on top, then one
+            // coalesced sweep out
             int16_t *img = reinterpret_cast<int16_t *>(lds);
+            if constexpr (sizeof(T) == 4) {
+                // narrow rows (shallow BFS): distances as bit planes in registers, decoded per row
+                T V[RW], D[KNARROW][RW];
+                const int maxd = bfs_planes<T, RW, KNARROW>(fre, sr, sc, -1, -1, V, D);
+                const int kq = 32 - __builtin_clz((unsigned)maxd | 1u);   // planes in use
 #pragma unroll
-            for (int k = 0; k < RW; ++k) {
-                const int r = lane + 64 * k;
-                if (r < H)
-                    for (int c = 0; c < W; ++c) {
-                        int v;
-                        if (r_get(V[k], c)) {
-                            v = 0;
+                for (int k = 0; k < RW; ++k) {
+                    const int r = lane + 64 * k;
+                    if (r < H)
+                        for (int c = 0; c < W; ++c) {
+                            int v;
+                            if (r_get(V[k], c)) {
+                                v = 0;
 #pragma unroll
-                            for (int q = 0; q < K; ++q)
-                                if (q < kq) v |= (int)r_get(D[q][k], c) << q;
-                        } else {
-                            v = r_get(fre[k], c) ? -2 : -1;
+                                for (int q = 0; q < KNARROW; ++q)
+                                    if (q < kq) v |= (int)r_get(D[q][k], c) << q;
+                            } else {
+                                v = r_get(fre[k], c) ? -2 : -1;
+                            }
+                            img[r * W + c] = (int16_t)v;
                         }
-                        img[r * W + c] = (int16_t)v;
-                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < RW; ++k) {
+                    const int r = lane + 64 * k;
+                    if (r < H)
+                        for (int c = 0; c < W; ++c) img[r * W + c] = r_get(fre[k], c) ? (int16_t)-2 : (int16_t)-1;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                bfs_to_img<T, RW>(fre, sr, sc, img, W);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
