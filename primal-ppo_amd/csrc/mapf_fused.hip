@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     obs_init(e, L, E, b0, nenv, mreg);
     __syncthreads();
     TL_STAMP(2);
-    obs_emit(e, L, obs, vec, E, b0, nenv, nband > 0);
+    obs_emit<false>(e, L, obs, vec, E, b0, nenv, nband > 0);
     step_pairs_finish(e, dfr, slot);
     TL_STAMP(3);
 }

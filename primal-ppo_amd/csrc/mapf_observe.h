@@ -33,17 +33,23 @@ struct ObsLds {
     uint32_t *stream, *occ, *mapc, *spos, *sgoal, *shn, *shp;
     int32_t *shpn;
     uint8_t *idg;               // [E][H*W] agent index at each occupied cell (read only where occ is set)
+    uint32_t *bfsw;             // BFS channel: [E*N][F][WD] dwords = 2*WD int16 cells of each FOV row's
+    int32_t *bfsown;            //   bfsMap window, from column (tc & ~1); [E*N] bfsMap at the agent's cell
     int stream_words, rowsz;
 };
 
 __host__ __device__ inline int obs_stream_words(const DevEnv &e, int E) { return (E * e.N * e.C * e.F * e.F + 31) / 32 + 1; }
+
+__host__ __device__ inline bool obs_bfs_windows(const DevEnv &e) { return e.C >= 7 && e.keep_bfs && (e.W & 1) == 0; }
+__host__ __device__ inline int obs_bfs_wd(const DevEnv &e) { return (e.F + 2) >> 1; }   // dwords per window row
 
 __host__ __device__ inline size_t obs_lds_bytes(const DevEnv &e, int E) {
     const int rowsz = e.Hp * e.WW;
     const int nmap = e.shared_map ? 1 : E;
     const size_t words = ((obs_stream_words(e, E) + 3) & ~3) + (size_t)E * rowsz + (size_t)nmap * rowsz +
                          2 * (size_t)E * e.N + E + (size_t)E * e.k_predict + E;
-    return words * 4 + (((size_t)E * e.H * e.W + 3) & ~(size_t)3);
+    const size_t bfs_words = obs_bfs_windows(e) ? (size_t)E * e.N * (e.F * obs_bfs_wd(e) + 1) : 0;
+    return (words + bfs_words) * 4 + (((size_t)E * e.H * e.W + 3) & ~(size_t)3);
 }
 
 __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
@@ -59,7 +65,9 @@ __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
     L.shn = L.sgoal + E * e.N;                  // [E] human next
     L.shp = L.shn + E;                          // [E][k_predict] human.path[1..K]
     L.shpn = reinterpret_cast<int32_t *>(L.shp + E * e.k_predict);   // [E] count
-    L.idg = reinterpret_cast<uint8_t *>(L.shpn + E);
+    L.bfsw = reinterpret_cast<uint32_t *>(L.shpn + E);
+    L.bfsown = reinterpret_cast<int32_t *>(L.bfsw + (obs_bfs_windows(e) ? (size_t)E * e.N * e.F * obs_bfs_wd(e) : 0));
+    L.idg = reinterpret_cast<uint8_t *>(L.bfsown + (obs_bfs_windows(e) ? E * e.N : 0));
     return L;
 }
 
@@ -165,6 +173,9 @@ __device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ 
 // Phases 1-4.  Every thread of the workgroup calls it after a __syncthreads()
 // that follows obs_init and the agents' staging.  skip_band: the zero band's
 // whole float4s were written by obs_zero_band_store in this launch.
+// BFSCH = false compiles the BFS channel (C = 7) out (the fused launch never
+// has it: step_observe_fusable).
+template <bool BFSCH = true>
 __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restrict__ obs, float *__restrict__ vec,
                                 int E, int b0, int nenv, bool skip_band = false) {
     using namespace obsd;
@@ -183,10 +194,25 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         atomicOr(&L.occ[le * rowsz + rr * e.WW + (cc >> 5)], 1u << (cc & 31));
         L.idg[le * HW + r * e.W + c] = (uint8_t)(k - le * N);
     }
+    const int half = F / 2;
+    if (BFSCH && obs_bfs_windows(e)) {
+        // the BFS channel's bfsMap windows: every load of the workgroup issued here
+        // at once (one HBM latency, not one per FOV-row task), as aligned dwords
+        const int WD = obs_bfs_wd(e);
+        for (int idx = tid; idx < K * F * WD; idx += nt) {
+            const int task = idx / WD, w = idx - task * WD;
+            const int k = task / F, y = task - k * F;
+            const int rr = min(max(prow(L.spos[k]) - half + y, 0), e.H - 1);
+            const int col = min(max(((pcol(L.spos[k]) - half) & ~1) + 2 * w, 0), e.W - 2);
+            const int16_t *bm = e.bfs + ((size_t)b0 * N + k) * HW;
+            L.bfsw[idx] = *reinterpret_cast<const uint32_t *>(bm + rr * e.W + col);
+        }
+        for (int k = tid; k < K; k += nt)
+            L.bfsown[k] = e.bfs[((size_t)b0 * N + k) * HW + prow(L.spos[k]) * e.W + pcol(L.spos[k])];
+    }
     __syncthreads();
 
     // ---- phase 2: (agent, FOV row) ----
-    const int half = F / 2;
     const int R2 = e.R * e.R;
     for (int task = tid; task < K * F; task += nt) {
         const int k = task / F, y = task - k * F;
@@ -223,7 +249,19 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
                 }
             }
         }
-        if (C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
+        if (BFSCH && obs_bfs_windows(e) && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension), from LDS
+            const int own = L.bfsown[k];
+            const uint32_t *win = L.bfsw + (size_t)task * obs_bfs_wd(e);
+            const int c0 = tc & ~1;
+            uint32_t m = 0;
+            for (int x = 0; x < F; ++x) {
+                const int cc = tc + x, wi = cc - c0;
+                const int v = (int16_t)(win[wi >> 1] >> ((wi & 1) * 16));
+                if (cc >= 0 && cc < e.W && v >= 0 && v < own) m |= 1u << x;
+            }
+            if (own < 0) m = 0;
+            or_bits(stream, base + 6 * FF, m, F);
+        } else if (BFSCH && C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
             const size_t ai = (size_t)b0 * N + k;
             const int16_t *bm = e.bfs + ai * e.H * e.W;
             const int16_t *row = bm + rr * e.W;

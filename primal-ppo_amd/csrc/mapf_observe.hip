@@ -17,6 +17,8 @@ template <bool HOST>
 __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restrict__ obs, float *__restrict__ vec,
                                                       int nsearch, int parity) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    TL_STAMP(0);
+    TL_HWID();
     if constexpr (HOST) {
         if ((int)blockIdx.x < nsearch) {
             const int wave = threadIdx.x >> 6;
@@ -34,8 +36,11 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     const ObsLds L = obs_layout(e, E, smem);
     obs_init(e, L, E, b0, nenv, obs_map_word(e, b0, nenv, threadIdx.x));
     obs_load_agents(e, L, b0, nenv);
+    TL_STAMP(1);
     __syncthreads();
+    TL_STAMP(2);
     obs_emit(e, L, obs, vec, E, b0, nenv);
+    TL_STAMP(3);
 }
 
 size_t observe_lds(const DevEnv &e) { return obs_lds_bytes(e, e.obs_envs); }
