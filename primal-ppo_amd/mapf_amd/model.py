@@ -84,6 +84,8 @@ class Model:
         self.ID = env_id
         self.device = torch.device(device)
         self.network = SCRIMPNet(numChannel=numChannel, num_agents=num_agents, fov=fov).to(self.device)
+        if self.device.type == "cuda":     # NHWC convolutions: no layout transposes around MIOpen's kernels
+            self.network = self.network.to(memory_format=torch.channels_last)
         self.num_agents = num_agents or EnvParameters.N_AGENTS
         self._flat = None
         if global_model:
