@@ -55,6 +55,10 @@ class _PreNorm(nn.Module):
     def forward(self, x):
         return self.fn.fn(self.fn.norm(x)) + x
 
+    def forward_first(self, x):
+        """Token 0 of forward(x) only (x: [b, n, d] -> [b, 1, d])."""
+        return self.fn.fn.forward_first(self.fn.norm(x)) + x[:, :1]
+
 
 class _SelfAttention(nn.Module):
     """transformer.py:48-85: fused qkv projection, softmax(q k^T / sqrt(dim)) v, output projection.
@@ -81,6 +85,16 @@ class _SelfAttention(nn.Module):
         qkv = self.to_qkv(x).view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
         q, k, v = qkv[0], qkv[1], qkv[2]
         out = F.scaled_dot_product_attention(q, k, v, scale=self.scale).transpose(1, 2).reshape(b, n, d)
+        return self.do1(self.nn1(out))
+
+    def forward_first(self, x):
+        """Token 0 of forward(x) only: keys and values of every token, the query of token 0."""
+        b, n, d = x.shape
+        h = self.heads
+        w, bias = self.to_qkv.weight, self.to_qkv.bias
+        q = F.linear(x[:, :1], w[:d], bias[:d]).view(b, 1, h, d // h).transpose(1, 2)          # b, h, 1, dh
+        kv = F.linear(x, w[d:], bias[d:]).view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)      # 2, b, h, n, dh
+        out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=self.scale).transpose(1, 2).reshape(b, 1, d)
         return self.do1(self.nn1(out))
 
 
@@ -111,8 +125,13 @@ class _Encoder(nn.Module):
                            _PreNorm(dim, _FeedForward(dim, mlp_dim, dropout))])
             for _ in range(depth)])
 
-    def forward(self, x):
-        for att, ff in self.layers:
+    def forward(self, x, first_only=False):
+        """first_only: return token 0 of the last block's output only ([b, 1, d]).  SCRIMPNet reads
+        nothing else (net.py:140-141 takes x[:, 0]), so the last block's queries, output
+        projection and MLP of tokens 1..16 are skipped; keys/values still see every token."""
+        for li, (att, ff) in enumerate(self.layers):
+            if first_only and li == len(self.layers) - 1:
+                return ff(att.forward_first(x))
             x = ff(att(x))
         return x
 
@@ -186,7 +205,7 @@ class SCRIMPNet(nn.Module):
             VV = torch.matmul(h, self.token_wV.sum(0))                        # [b, 1, 512]
             T = A * VV                       # [b, 16, 512]: matmul(A, VV) over a length-1 axis
             x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
-            x = self.transformer(self.dropout(x))
+            x = self.transformer(self.dropout(x), first_only=True)
             x = self.nn_same(self.nn_same(x[:, 0]))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)
