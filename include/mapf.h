@@ -184,6 +184,9 @@ int mapf_get_profile(mapf_env *env, uint64_t *host16, int reset, void *stream);
 /* Diagnostic builds only: the fused kernel's per-workgroup timeline of its last
  * launch, host [nblocks][8] u64 (100 MHz realtime stamps 0-3, HW_ID, XCC_ID). */
 int mapf_get_timeline(mapf_env *env, uint64_t *host, int32_t nblocks, void *stream);
+/* Diagnostic build: per-wave phase cycles of the last step launch, uint64 [nwaves][8]
+ * (slots 0-6 phases, 7 = 1 if the wave recorded). */
+int mapf_get_wave_profile(mapf_env *env, uint64_t *host, int32_t nwaves, void *stream);
 
 int mapf_get_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */
 int mapf_set_state(mapf_env *env, const mapf_state *host, void *stream);   /* synchronises */

@@ -462,6 +462,15 @@ int mapf_get_profile(mapf_env *e, uint64_t *host16, int reset, void *stream) {
     return MAPF_OK;
 }
 
+int mapf_get_wave_profile(mapf_env *e, uint64_t *host, int32_t nwaves, void *stream) {
+    if (!e || !host || nwaves < 0 || nwaves > (int)PROF_WAVES) return fail(MAPF_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(host, e->d.prof, (size_t)nwaves * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MAPF_OK;
+}
+
 int mapf_get_timeline(mapf_env *e, uint64_t *host, int32_t nblocks, void *stream) {
     if (!e || !host || nblocks < 0 || nblocks > (int)PROF_TL_BLOCKS) return fail(MAPF_EINVAL, "bad argument");
     HIPCHK(hipSetDevice(e->device));

@@ -28,6 +28,12 @@
 
 namespace mapf {
 
+// one wave per env observes on its own (NP = 8, shared map in registers, every
+// env's observation a whole number of float4s)
+__host__ __device__ inline bool fused_per_wave(const DevEnv &e) {
+    return e.G == 8 && regmap_fits(e) && ((e.N * e.C * e.F * e.F) & 3) == 0;
+}
+
 template <int NP, bool HOST>
 __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__restrict__ actions, StepOut out,
                                                            uint32_t flags, int slot, float *__restrict__ obs,
@@ -59,10 +65,12 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     const int blk = bx - nsearch;
     const int b0 = blk * E;
     const int nenv = min(E, e.B - b0);
-    const ObsLds L = obs_layout(e, E, smem);
     // the map words are loaded before the step's loads; at NP = 8 every wave holds
-    // the whole shared map (lane k = word k) and the step reads it from registers
+    // the whole shared map (lane k = word k) and the step reads it from registers,
+    // and each wave then observes its own env with no workgroup barrier
     const bool regmap = NP == 8 && regmap_fits(e);
+    const bool per_wave = regmap && fused_per_wave(e);
+    const ObsLds L = obs_layout(e, E, smem, per_wave);
     const uint32_t mreg = obs_map_word(e, b0, nenv, regmap ? (int)(threadIdx.x & 63) : (int)threadIdx.x);
     PairsDeferred dfr;
 #ifdef MAPF_DIAG_NOSTEP   // timing diagnostic only (make diag): observe the pre-step state, no step
@@ -72,10 +80,19 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
                              RegMap{mreg, regmap}, dfr);
 #endif
     TL_STAMP(1);
-    obs_init(e, L, E, b0, nenv, mreg);
-    __syncthreads();
-    TL_STAMP(2);
-    obs_emit<false>(e, L, obs, vec, E, b0, nenv, nband > 0);
+    if (per_wave) {
+        const int le = (int)(threadIdx.x >> 6);
+        if (le < nenv) {
+            const ObsGroup g = obs_wave_init(e, L, le, mreg);
+            TL_STAMP(2);
+            obs_emit<false>(e, L, obs, vec, g, b0, nband > 0);
+        }
+    } else {
+        obs_init(e, L, E, b0, nenv, mreg);
+        __syncthreads();
+        TL_STAMP(2);
+        obs_emit<false>(e, L, obs, vec, obs_workgroup(L, nenv), b0, nband > 0);
+    }
     step_pairs_finish(e, dfr, slot);
     TL_STAMP(3);
 }
@@ -83,13 +100,14 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
 bool step_observe_fusable(const DevEnv &e) {
     if (e.G > 8 || e.force_agent_lanes || e.human_mode == 2 || e.C >= 7) return false;
     const int E = 256 / (e.G * e.G);
-    return obs_lds_bytes(e, E) <= 64 * 1024;
+    return obs_lds_bytes(e, E, fused_per_wave(e)) <= 64 * 1024;
 }
 
 template <int NP>
 static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot, float *obs,
                       float *vec, int nsearch, int sslot, hipStream_t s) {
     constexpr int E = 256 / (NP * NP);
+    const bool per_wave = NP == 8 && fused_per_wave(e);
     // zero-band workgroups: whole float4s only, so the step workgroups' slices
     // and the buffer must be 16-B aligned
     int z0, z1, nband = 0;
@@ -97,7 +115,7 @@ static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uin
     if (e.band_blocks > 0 && obs_zero_band(e, z0, z1) && (slice & 3) == 0 && ((uintptr_t)obs & 15) == 0)
         nband = e.band_blocks;
     const int grid = (e.B + E - 1) / E + nsearch + nband;
-    size_t lds = obs_lds_bytes(e, E);
+    size_t lds = obs_lds_bytes(e, E, per_wave);
     if (nsearch > 0) {
         const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
         if (sl > lds) lds = sl;

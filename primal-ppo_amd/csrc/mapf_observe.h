@@ -28,8 +28,11 @@
 
 namespace mapf {
 
-// LDS carve-up of an observing workgroup (E envs).
+// LDS carve-up of an observing workgroup (E envs).  per_env: every env has its
+// own word-aligned bit-stream (stride swe words) and its own copy of the map
+// rows, so one wave can observe its env with no workgroup barrier.
 struct ObsLds {
+    int swe;                    // per-env stream stride in words (0: one stream for the workgroup)
     uint32_t *stream, *occ, *mapc, *spos, *sgoal, *shn, *shp;
     int32_t *shpn;
     uint8_t *idg;               // [E][H*W] agent index at each occupied cell (read only where occ is set)
@@ -43,20 +46,26 @@ __host__ __device__ inline int obs_stream_words(const DevEnv &e, int E) { return
 __host__ __device__ inline bool obs_bfs_windows(const DevEnv &e) { return e.C >= 7 && e.keep_bfs && (e.W & 1) == 0; }
 __host__ __device__ inline int obs_bfs_wd(const DevEnv &e) { return (e.F + 2) >> 1; }   // dwords per window row
 
-__host__ __device__ inline size_t obs_lds_bytes(const DevEnv &e, int E) {
+__host__ __device__ inline int obs_env_stream_words(const DevEnv &e) {
+    return ((e.N * e.C * e.F * e.F + 31) / 32 + 1 + 3) & ~3;
+}
+
+__host__ __device__ inline size_t obs_lds_bytes(const DevEnv &e, int E, bool per_env = false) {
     const int rowsz = e.Hp * e.WW;
-    const int nmap = e.shared_map ? 1 : E;
-    const size_t words = ((obs_stream_words(e, E) + 3) & ~3) + (size_t)E * rowsz + (size_t)nmap * rowsz +
+    const int nmap = (e.shared_map && !per_env) ? 1 : E;
+    const size_t sw = per_env ? (size_t)E * obs_env_stream_words(e) : (size_t)((obs_stream_words(e, E) + 3) & ~3);
+    const size_t words = sw + (size_t)E * rowsz + (size_t)nmap * rowsz +
                          2 * (size_t)E * e.N + E + (size_t)E * e.k_predict + E;
     const size_t bfs_words = obs_bfs_windows(e) ? (size_t)E * e.N * (e.F * obs_bfs_wd(e) + 1) : 0;
     return (words + bfs_words) * 4 + (((size_t)E * e.H * e.W + 3) & ~(size_t)3);
 }
 
-__device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem) {
+__device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem, bool per_env = false) {
     ObsLds L;
-    L.stream_words = obs_stream_words(e, E);
+    L.swe = per_env ? obs_env_stream_words(e) : 0;
+    L.stream_words = per_env ? E * L.swe : obs_stream_words(e, E);
     L.rowsz = e.Hp * e.WW;
-    const int nmap = e.shared_map ? 1 : E;
+    const int nmap = (e.shared_map && !per_env) ? 1 : E;
     L.stream = reinterpret_cast<uint32_t *>(smem);
     L.occ = L.stream + ((L.stream_words + 3) & ~3);
     L.mapc = L.occ + E * L.rowsz;
@@ -175,24 +184,65 @@ __device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ 
 // whole float4s were written by obs_zero_band_store in this launch.
 // BFSCH = false compiles the BFS channel (C = 7) out (the fused launch never
 // has it: step_observe_fusable).
+// The threads that observe a run of the workgroup's envs together: the whole
+// workgroup (workgroup barriers) or one wave observing its own env (per_env
+// layout; wave-level ordering only).
+struct ObsGroup {
+    int tid, nt;                 // thread index in the group, group size
+    int le0, nenv;               // first env (index within the workgroup) and env count
+    uint32_t *stream;            // bit 0 = float 0 of env le0's observation
+    const uint32_t *mapc;        // map rows: the shared map, or per-env maps at (le - le0) * rowsz
+    bool wave;
+};
+
+__device__ inline void obs_sync(const ObsGroup &g) {
+    if (g.wave) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
+__device__ inline ObsGroup obs_workgroup(const ObsLds &L, int nenv) {
+    return ObsGroup{(int)threadIdx.x, (int)blockDim.x, 0, nenv, L.stream, L.mapc, false};
+}
+
+// One wave observes env le of the workgroup (per_env layout): zero its stream
+// and occupancy, copy the map rows it holds in registers (lane k = word k).
+__device__ inline ObsGroup obs_wave_init(const DevEnv &e, const ObsLds &L, int le, uint32_t mreg) {
+    const int lane = lane_id();
+    uint32_t *st = L.stream + (size_t)le * L.swe;
+    for (int k = lane; k < L.swe; k += 64) st[k] = 0u;
+    for (int k = lane; k < L.rowsz; k += 64) L.occ[le * L.rowsz + k] = 0u;
+    uint32_t *mp = L.mapc + le * L.rowsz;
+    if (lane < L.rowsz) mp[lane] = mreg;
+    ObsGroup g{lane, 64, le, 1, st, mp, true};
+    obs_sync(g);
+    return g;
+}
+
 template <bool BFSCH = true>
 __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restrict__ obs, float *__restrict__ vec,
-                                int E, int b0, int nenv, bool skip_band = false) {
+                                const ObsGroup &G, int b0, bool skip_band = false) {
     using namespace obsd;
     const int N = e.N, F = e.F, C = e.C, FF = F * F, CFF = C * FF;
-    const int K = nenv * N;
+    const int K = G.nenv * N;                 // agents of the group; k below is group-relative
+    const int kw = G.le0 * N;                 // first agent of the group within the workgroup
     const int rowsz = L.rowsz;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    uint32_t *stream = L.stream;
+    const int tid = G.tid, nt = G.nt;
+    uint32_t *stream = G.stream;
+    b0 += G.le0;                              // first env of the group
+    const int E = G.nenv;
 
     // ---- phase 1: worldWithAgents as a padded bitmap per env + agent index grid ----
     const int HW = e.H * e.W;
     for (int k = tid; k < K; k += nt) {
-        const int le = k / N;
-        const int r = prow(L.spos[k]), c = pcol(L.spos[k]);
+        const int le = G.le0 + k / N;
+        const int r = prow(L.spos[kw + k]), c = pcol(L.spos[kw + k]);
         const int rr = r + e.P, cc = c + e.P;
         atomicOr(&L.occ[le * rowsz + rr * e.WW + (cc >> 5)], 1u << (cc & 31));
-        L.idg[le * HW + r * e.W + c] = (uint8_t)(k - le * N);
+        L.idg[le * HW + r * e.W + c] = (uint8_t)(k % N);
     }
     const int half = F / 2;
     if (BFSCH && obs_bfs_windows(e)) {
@@ -202,26 +252,26 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         for (int idx = tid; idx < K * F * WD; idx += nt) {
             const int task = idx / WD, w = idx - task * WD;
             const int k = task / F, y = task - k * F;
-            const int rr = min(max(prow(L.spos[k]) - half + y, 0), e.H - 1);
-            const int col = min(max(((pcol(L.spos[k]) - half) & ~1) + 2 * w, 0), e.W - 2);
+            const int rr = min(max(prow(L.spos[kw + k]) - half + y, 0), e.H - 1);
+            const int col = min(max(((pcol(L.spos[kw + k]) - half) & ~1) + 2 * w, 0), e.W - 2);
             const int16_t *bm = e.bfs + ((size_t)b0 * N + k) * HW;
-            L.bfsw[idx] = *reinterpret_cast<const uint32_t *>(bm + rr * e.W + col);
+            L.bfsw[kw * F * WD + idx] = *reinterpret_cast<const uint32_t *>(bm + rr * e.W + col);
         }
         for (int k = tid; k < K; k += nt)
-            L.bfsown[k] = e.bfs[((size_t)b0 * N + k) * HW + prow(L.spos[k]) * e.W + pcol(L.spos[k])];
+            L.bfsown[kw + k] = e.bfs[((size_t)b0 * N + k) * HW + prow(L.spos[kw + k]) * e.W + pcol(L.spos[kw + k])];
     }
-    __syncthreads();
+    obs_sync(G);
 
     // ---- phase 2: (agent, FOV row) ----
     const int R2 = e.R * e.R;
     for (int task = tid; task < K * F; task += nt) {
         const int k = task / F, y = task - k * F;
-        const int le = k / N;
-        const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
+        const int le = G.le0 + k / N;
+        const int pr = prow(L.spos[kw + k]), pc = pcol(L.spos[kw + k]);
         const int tr = pr - half, tc = pc - half;
         const int rr = tr + y;                       // map row of this FOV row
         const int prow_idx = rr + e.P;               // padded row (always inside)
-        const uint32_t *mrow = L.mapc + (e.shared_map ? 0 : le * rowsz) + prow_idx * e.WW;
+        const uint32_t *mrow = G.mapc + (e.shared_map ? 0 : (le - G.le0) * rowsz) + prow_idx * e.WW;
         const uint32_t *orow = L.occ + le * rowsz + prow_idx * e.WW;
         uint32_t seg0 = seg_at(mrow, e.WW, tc + e.P, F);
         uint32_t segA = seg_at(orow, e.WW, tc + e.P, F);
@@ -250,8 +300,8 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             }
         }
         if (BFSCH && obs_bfs_windows(e) && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension), from LDS
-            const int own = L.bfsown[k];
-            const uint32_t *win = L.bfsw + (size_t)task * obs_bfs_wd(e);
+            const int own = L.bfsown[kw + k];
+            const uint32_t *win = L.bfsw + ((size_t)kw * F + task) * obs_bfs_wd(e);
             const int c0 = tc & ~1;
             uint32_t m = 0;
             for (int x = 0; x < F; ++x) {
@@ -289,11 +339,11 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
 
     // ---- phase 3: per agent: own goal (ch2), human next position (ch4), HP cells (ch5), vector ----
     for (int k = tid; k < K; k += nt) {
-        const int le = k / N;
-        const int pr = prow(L.spos[k]), pc = pcol(L.spos[k]);
+        const int le = G.le0 + k / N;
+        const int pr = prow(L.spos[kw + k]), pc = pcol(L.spos[kw + k]);
         const int tr = pr - half, tc = pc - half;
         const int base = k * CFF;
-        const int gr = prow(L.sgoal[k]), gc = pcol(L.sgoal[k]);
+        const int gr = prow(L.sgoal[kw + k]), gc = pcol(L.sgoal[kw + k]);
         if (tr <= gr && gr < tr + F && tc <= gc && gc < tc + F) set_bit(stream, base + 2 * FF + (gr - tr) * F + (gc - tc));
         const uint32_t hn = L.shn[le];
         const int hr = prow(hn), hc = pcol(hn);
@@ -316,7 +366,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         }
         reinterpret_cast<float4 *>(vec)[(size_t)b0 * N + k] = v;
     }
-    __syncthreads();
+    obs_sync(G);
     TL_STAMP(4);
 
     // ---- phase 4: bit-stream -> float stores ----
@@ -333,8 +383,14 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             if (!(off >= z0 && off + 4 <= z1)) {
                 const uint32_t bitpos = (uint32_t)(q << 2);
                 const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
-                d4[q] = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
-                                    (float)((nib >> 3) & 1u));
+                const float4 f = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
+                                             (float)((nib >> 3) & 1u));
+#ifdef MAPF_NT_STORES   // store-policy experiment (make ntstores)
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4f{f.x, f.y, f.z, f.w}, reinterpret_cast<v4f *>(&d4[q]));
+#else
+                d4[q] = f;
+#endif
             }
             off += step;
             if (off >= CFF) off -= CFF;

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     TL_STAMP(1);
     __syncthreads();
     TL_STAMP(2);
-    obs_emit(e, L, obs, vec, E, b0, nenv);
+    obs_emit(e, L, obs, vec, obs_workgroup(L, nenv), b0);
     TL_STAMP(3);
 }
 

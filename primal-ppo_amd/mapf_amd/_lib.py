@@ -52,6 +52,7 @@ SIGNATURES = {
     "mapf_get_counters": (ctypes.c_int, [P, P, P]),
     "mapf_get_profile": (ctypes.c_int, [P, P, ctypes.c_int, P]),
     "mapf_get_timeline": (ctypes.c_int, [P, P, ctypes.c_int32, P]),
+    "mapf_get_wave_profile": (ctypes.c_int, [P, P, ctypes.c_int32, P]),
     "mapf_get_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
     "mapf_set_state": (ctypes.c_int, [P, ctypes.POINTER(State), P]),
     "mapf_gae": (ctypes.c_int, [P, P, P, P, P, I32, I32, ctypes.c_double, ctypes.c_double, P]),

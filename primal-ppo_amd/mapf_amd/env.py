@@ -222,6 +222,13 @@ class BatchedMapfGym:
                                                _stream(self.device)))
         return c
 
+    def wave_profile(self, nwaves):
+        """Diagnostic (stamps) build: per-wave phase cycles of the last step launch, uint64 [nwaves, 8]."""
+        out = np.zeros((nwaves, 8), dtype=np.uint64)
+        _lib.check(_lib.lib().mapf_get_wave_profile(self.h, out.ctypes.data_as(ctypes.c_void_p), nwaves,
+                                                     _stream(self.device)))
+        return out
+
     def timeline(self, nblocks):
         """Diagnostic (stamps) build: per-workgroup timeline of the last fused launch,
         uint64 [nblocks, 8] (realtime stamps 0-3 at 100 MHz, HW_ID, XCC_ID)."""

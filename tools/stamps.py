@@ -43,7 +43,7 @@ def main():
     for _ in range(n):
         one()
     torch.cuda.synchronize()
-    p = env.profile(reset=True)      # sums over the waves of the last step launch
+    p = env.profile(reset=False)     # sums over the waves of the last step launch
     waves = max(int(p[15]), 1)
     n = 1
     tot = sum(int(x) for x in p[:7])
@@ -51,6 +51,21 @@ def main():
     for k, name in enumerate(PHASES):
         print(f"  {name:26s} {int(p[k]) / waves:9.0f} cycles/wave  {100.0 * int(p[k]) / max(tot, 1):5.1f}%")
     print(f"  {'total':26s} {tot / waves:9.0f} cycles/wave")
+    # per-wave distribution of the last launch: percentiles of each phase, and the
+    # mean breakdown of the slowest 5 % of waves
+    import numpy as np
+    wp = env.wave_profile(min(65536, 4096 * 2))
+    wp = wp[wp[:, 7] == 1][:, :7].astype(np.float64)
+    if len(wp):
+        tot_w = wp.sum(1)
+        print("per-wave percentiles (p10 / p50 / p90 / p99 / max cycles):")
+        for k, name in enumerate(PHASES + ["total"]):
+            col = tot_w if k == 7 else wp[:, k]
+            print(f"  {name:26s} " + " / ".join(f"{v:8.0f}" for v in np.percentile(col, [10, 50, 90, 99, 100])))
+        slow = wp[tot_w >= np.percentile(tot_w, 95)]
+        print("slowest 5% of waves, mean cycles per phase:")
+        for k, name in enumerate(PHASES):
+            print(f"  {name:26s} {slow[:, k].mean():9.0f}")
 
 
 if __name__ == "__main__":
