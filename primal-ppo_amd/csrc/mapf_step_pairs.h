@@ -134,14 +134,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
 #if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 1)    // timing diagnostic only
         const u32x4 o = {clock * 0x9E3779B9u + env_id, clock ^ env_id, clock + 7u, env_id * 3u};
 #else
-#if defined(MAPF_VALU_PHILOX)   // experiment: the draw on the vector ALU (inputs moved to VGPRs)
-        uint32_t ev, cv;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(ev) : "s"(env_id));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(cv) : "s"(clock));
-        const u32x4 o = philox(ev, P_ACT, cv, 0u, e.seed);
-#else
         const u32x4 o = philox(env_id, P_ACT, clock, 0u, e.seed);
-#endif
 #endif
         a_i = random_action(o, i);
         a_j = random_action(o, j);
