@@ -26,6 +26,21 @@ def random_warehouse(rng, world_size=(10, 40)):
     return generate_warehouse(length)
 
 
+def random_warehouse_batch(rng, num_envs, world_size=(10, 40)):
+    """One MapfGym() map per env (random length in WORLD_SIZE, mapf_gym.py:166) in ONE
+    [B, Lmax, Wmax] int8 stack: each warehouse at the top-left, padded with obstacle
+    rows/columns at the bottom/right.  Equivalent for the env: off-map and padding
+    cells read alike everywhere (static masks, FOV channel 0, A*/BFS passability,
+    getFreeCell's rejection; the human entrance lies on row 0 / column 0, unpadded);
+    tests/test_gpu_parity.py replays reference episodes on a padded map."""
+    big = generate_warehouse(world_size[1])
+    out = np.full((num_envs,) + big.shape, -1, dtype=np.int8)
+    for b in range(num_envs):
+        w = random_warehouse(rng, world_size)
+        out[b, :w.shape[0], :w.shape[1]] = w
+    return out
+
+
 def random_map(rng, height, width, density):
     return -(rng.random((height, width)) < density).astype(np.int8)
 

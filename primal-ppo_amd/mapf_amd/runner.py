@@ -25,6 +25,20 @@ from .config import EnvParameters, NetParameters, TrainingParameters
 from .env import BatchedMapfGym, gae
 
 
+def reference_maps(env: BatchedMapfGym, world_size=None, seed=0):
+    """new_maps for DeviceRunner: per rollout, every env gets its own MapfGym() warehouse
+    (random length in EnvParameters.WORLD_SIZE) in the padded [B, Lmax, Wmax] stack the
+    env was created with (maps.random_warehouse_batch; create the env with
+    height, width = that stack's shape and shared_map=False)."""
+    import numpy as np
+    from .maps import random_warehouse_batch
+    ws = EnvParameters.WORLD_SIZE if world_size is None else world_size
+
+    def draw(rollout):
+        return random_warehouse_batch(np.random.default_rng((seed, rollout)), env.B, ws)
+    return draw
+
+
 class OneEpPerformance:
     """util.py:56-65 (sums over all B envs of the rollout)."""
 
@@ -47,11 +61,17 @@ class BatchValues:
 
 
 class DeviceRunner:
-    def __init__(self, env: BatchedMapfGym, model, n_steps=None, seed=0):
+    """new_maps: callable(rollout index) -> maps for env.reset_seeded at the start of every
+    run(), i.e. Runner.run's `env = MapfGym()` (runner.py:30: a NEW random-size warehouse
+    and new agents/human every rollout) -- e.g. reference_maps(env) below.  None: the
+    envs continue from where the previous rollout left them (lifelong)."""
+
+    def __init__(self, env: BatchedMapfGym, model, n_steps=None, seed=0, new_maps=None):
         self.env = env
         self.model = model
         self.T = TrainingParameters.N_STEPS if n_steps is None else n_steps
         self.seed = seed
+        self.new_maps = new_maps
         self.rollouts = 0
         B, N, C, F = env.B, env.N, env.C, env.F
         dev = env.device
@@ -79,6 +99,8 @@ class DeviceRunner:
         if weights is not None:
             self.model.set_weights(weights)
         env, T = self.env, self.T
+        if self.new_maps is not None:        # runner.py:30 -- a fresh MapfGym() per rollout
+            env.reset_seeded(self.new_maps(self.rollouts), seed=(self.seed << 20) + self.rollouts + 1)
         env.observe(self.obs[0], self.vec[0])
         for t in range(T):
             a, ps, v, _, _, cv = self.model.step(self.obs[t], self.vec[t], None, seed=self.seed,

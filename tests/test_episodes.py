@@ -58,3 +58,22 @@ def test_generator_follows_reference_protocol():
         for s in infos["agentsSequence"][i]:
             assert sum(abs(a[0] - b[0]) + abs(a[1] - b[1]) for a, b in zip(s, s[1:])) > 40
             assert all(m[c] == 0 for c in s)
+
+
+def test_random_warehouse_batch_pads_with_obstacles():
+    """MapfGym() maps for a batch: random lengths in WORLD_SIZE, each warehouse at the
+    top-left of one [B, 40, 60] stack, the rest obstacles (maps.random_warehouse_batch)."""
+    from mapf_amd.maps import generate_warehouse, random_warehouse_batch
+    m = random_warehouse_batch(np.random.default_rng(0), 64, (10, 40))
+    assert m.shape == (64, 40, 60) and m.dtype == np.int8
+    lengths = set()
+    for b in range(64):
+        free = np.argwhere(m[b] == 0)
+        L = int(free[:, 0].max()) + 1
+        W = int(free[:, 1].max()) + 1
+        w = generate_warehouse(L)
+        assert W == w.shape[1]
+        np.testing.assert_array_equal(m[b, :L, :W], w)
+        assert (m[b, L:, :] == -1).all() and (m[b, :, W:] == -1).all()
+        lengths.add(L)
+    assert len(lengths) > 10 and min(lengths) >= 10 and max(lengths) <= 40

@@ -45,9 +45,25 @@ def assert_no_errors(env, allow=()):
 # --------------------------------------------------------------------------- g1
 @pytest.mark.parametrize("name", G1_NAMES)
 def test_g1_episode_on_device(name):
+    run_g1(name, pad=None)
+
+
+@pytest.mark.parametrize("name", G1_NAMES[:3])
+def test_g1_episode_on_padded_map(name):
+    """The same reference episode on the map padded with obstacle rows/columns at the
+    bottom/right (how a batch of the reference's random-size warehouses shares one
+    H x W, maps.random_warehouse_batch): off-map and padding read alike, so every
+    output and observation is unchanged."""
+    run_g1(name, pad=(6, 5))
+
+
+def run_g1(name, pad):
     z = load(name)
     n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
     world = z["map"]
+    H0, W0 = world.shape
+    if pad is not None:
+        world = np.pad(world, ((0, pad[0]), (0, pad[1])), constant_values=-1)
     H, W = world.shape
     hmode = int(z["human_mode"])
     B = 37   # replicas: partial last workgroup, several envs per wave
@@ -64,7 +80,10 @@ def test_g1_episode_on_device(name):
         np.testing.assert_array_equal(st["pos"][b], z["pos0"])
         L = st["human"][b, 7]
         np.testing.assert_array_equal(st["human_path"][b, :L], z["hpath0"])
-    np.testing.assert_array_equal(env.bfs().cpu().numpy(), np.broadcast_to(z["bfs0"], (B,) + z["bfs0"].shape))
+    bfs = env.bfs().cpu().numpy()
+    np.testing.assert_array_equal(bfs[:, :, :H0, :W0], np.broadcast_to(z["bfs0"], (B,) + z["bfs0"].shape))
+    if pad is not None:
+        assert (bfs[:, :, H0:, :] == -1).all() and (bfs[:, :, :, W0:] == -1).all()
     obs, vec = env.observe()
     ref = unpack_obs(z["obs0"], (n, nch, fov, fov))
     o = obs.cpu().numpy()
@@ -94,7 +113,7 @@ def test_g1_episode_on_device(name):
             np.testing.assert_array_equal(st["goal"][B - 1], z["goal"][t])
             np.testing.assert_array_equal(st["human"][0, 0:2], z["hpos"][t])
             np.testing.assert_array_equal(st["human"][0, 2:4], z["hnext"][t])
-    np.testing.assert_array_equal(env.bfs().cpu().numpy()[B - 1], z["bfs_final"])
+    np.testing.assert_array_equal(env.bfs().cpu().numpy()[B - 1][:, :H0, :W0], z["bfs_final"])
     assert_no_errors(env)
 
 

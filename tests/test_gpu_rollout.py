@@ -139,3 +139,32 @@ def test_policy_forward_on_device_matches_reference():
         got = o.float().cpu().numpy()
         tol = 2e-2 * max(1.0, float(np.abs(want).max()))
         np.testing.assert_allclose(got, want, rtol=0, atol=tol, err_msg=name)
+
+
+def test_device_runner_fresh_reference_envs_each_rollout():
+    """DeviceRunner(new_maps=reference_maps(env)): every run() starts from a fresh
+    MapfGym() per env (runner.py:30) -- its own random-size warehouse in the padded
+    stack, new agents and human -- and every agent stays on its env's real map."""
+    from mapf_amd.config import make_config
+    from mapf_amd.env import BatchedMapfGym
+    from mapf_amd.model import Model
+    from mapf_amd.runner import DeviceRunner, reference_maps
+    B, N, T = 32, 8, 6
+    env = BatchedMapfGym(make_config(B, 40, 60, num_agents=N, fov=9, num_channel=6, human_mode="random",
+                                     goal_mode="random", fix_choice=1, seed=5, shared_map=False))
+    model = Model(0, "cuda", global_model=False, numChannel=6, num_agents=N, fov=9)
+    draw = reference_maps(env, seed=3)
+    runner = DeviceRunner(env, model, n_steps=T, seed=1, new_maps=draw)
+    starts = []
+    for r in range(2):
+        mb, perf = runner.run()
+        assert mb["observations"].shape == (T * B, N, 6, 9, 9)
+        maps = draw(r)
+        st = env.get_state()
+        for b in range(B):
+            cells = maps[b][st["pos"][b][:, 0], st["pos"][b][:, 1]]
+            assert (cells == 0).all(), f"rollout {r} env {b}: agent off its warehouse"
+        starts.append(mb["observations"][:B].cpu().numpy())
+    assert not np.array_equal(starts[0], starts[1])      # a new env each rollout
+    c = env.counters()
+    assert not c[:8].any(), c[:8]

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--train", action="store_true", help="also time PPO minibatch updates")
     ap.add_argument("--minibatch", type=int, default=256, help="rows per PPO minibatch (x N agents)")
     ap.add_argument("--updates", type=int, default=10)
+    ap.add_argument("--reference-maps", action="store_true",
+                    help="runner.py:30 semantics: a fresh MapfGym() (random-size warehouse, padded to 40x60) "
+                         "per env per rollout, instead of --size")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -44,14 +47,18 @@ def main():
     B, N, H, F = args.envs, args.agents, args.size, args.fov
     EnvParameters.N_AGENTS = N
     EnvParameters.FOV_SIZE = F
-    env = BatchedMapfGym(make_config(B, H, H, num_agents=N, fov=F, num_channel=6, human_mode="random",
-                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B), device=dev)
-    env.reset_seeded(generate_warehouse(H, H))
+    from mapf_amd.runner import reference_maps
+    Hh, Ww = (40, 60) if args.reference_maps else (H, H)
+    env = BatchedMapfGym(make_config(B, Hh, Ww, num_agents=N, fov=F, num_channel=6, human_mode="random",
+                                     goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B,
+                                     shared_map=not args.reference_maps), device=dev)
+    new_maps = reference_maps(env, seed=rank) if args.reference_maps else None
+    env.reset_seeded(new_maps(0) if new_maps else generate_warehouse(H, H))
     model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=F)
     if world > 1:
         for p in model.network.parameters():
             torch.distributed.broadcast(p.data, 0)
-    runner = DeviceRunner(env, model, n_steps=args.steps, seed=rank)
+    runner = DeviceRunner(env, model, n_steps=args.steps, seed=rank, new_maps=new_maps)
     runner.run()                       # warm-up (kernels, autotuning)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -60,7 +67,8 @@ def main():
     dt = time.perf_counter() - t0
     out = {"phase": "rollout (policy forward + sampling + env.step + observe + GAE)", "n_gpus": world,
            "agent_steps_per_s": round(world * B * N * args.steps / dt, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
-           "config": {"envs_per_gpu": B, "agents": N, "grid": H, "fov": F, "T": args.steps}}
+           "config": {"envs_per_gpu": B, "agents": N, "grid": "MapfGym() random 10-40 (40x60 padded), new per rollout"
+                      if args.reference_maps else H, "fov": F, "T": args.steps}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if args.train:
