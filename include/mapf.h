@@ -163,6 +163,20 @@ int mapf_step_observe(mapf_env *env, const int32_t *actions, const mapf_step_out
 int mapf_step_observe_random(mapf_env *env, int32_t *actions_out, const mapf_step_out *out, float *obs,
                              float *vec, void *stream);
 
+/* Random-policy rollout: T x (mapf_step_observe_random), i.e. runner.py:64-100
+ * with the uniform random policy T times, in ONE launch where the configuration
+ * allows (mapf_rollout_random_fused; otherwise T launches) -- identical results.
+ * slots = 1: step t writes slot t of [T]-leading DEVICE buffers (actions_out
+ * [T][B][N], every out field [T][...], obs [T][B][N][C][F][F], vec [T][B][N][4]),
+ * i.e. rollout buffers; slots = 0: every step overwrites the same [B]-leading
+ * buffers.  Each wave of the one-launch kernel owns one env and loops step ->
+ * observe -> its own search work, so steps overlap other envs' store drains. */
+int mapf_rollout_random(mapf_env *env, int32_t T, int32_t slots, int32_t *actions_out, const mapf_step_out *out,
+                        float *obs, float *vec, void *stream);
+/* 1 if mapf_rollout_random runs as one launch for this configuration (N in 5..8,
+ * shared map of width <= 30, no BFS channel, no scripted human). */
+int mapf_rollout_random_fused(const mapf_env *env);
+
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the
  * humans' next paths) on its own; mapf_observe otherwise runs it inside the
  * observation launch.  Any later call that needs it flushes implicitly. */

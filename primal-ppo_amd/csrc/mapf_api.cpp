@@ -176,6 +176,8 @@ int mapf_destroy(mapf_env *e) {
 
 int mapf_path_capacity(const mapf_env *e) { return e ? e->d.Lmax : 0; }
 int mapf_step_observe_fused(const mapf_env *e) { return e && step_observe_fusable(e->d) ? 1 : 0; }
+static bool rollout_random_fused(const mapf_env *e) { return e && rollout_random_fusable(e->d); }
+int mapf_rollout_random_fused(const mapf_env *e) { return rollout_random_fused(e) ? 1 : 0; }
 
 int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     if (!e || !spec || !spec->maps) return fail(MAPF_EINVAL, "null argument");
@@ -408,6 +410,46 @@ int mapf_step_observe(mapf_env *e, const int32_t *actions, const mapf_step_out *
 int mapf_step_observe_random(mapf_env *e, int32_t *actions_out, const mapf_step_out *out, float *obs, float *vec,
                              void *stream) {
     return step_observe_impl(e, actions_out, out, 2u, obs, vec, stream);
+}
+
+int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_out, const mapf_step_out *out,
+                        float *obs, float *vec, void *stream) {
+    if (!e || !actions_out || !obs || !vec) return fail(MAPF_EINVAL, "null argument");
+    if (T < 0) return fail(MAPF_EINVAL, "T must be >= 0");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_rollout_random before mapf_reset");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    StepOut o{};
+    if (out) {
+        o.status = out->status; o.reward = out->reward; o.shadow_goals = out->shadow_goals; o.cost = out->cost;
+        o.train_valid = out->train_valid; o.actions_fixed = out->actions_fixed; o.goals_reached = out->goals_reached;
+        o.constraints = out->constraints; o.reward_total = out->reward_total;
+    }
+    if (T == 0) return MAPF_OK;
+    if (rollout_random_fused(e)) {
+        if (int rc = flush_search(e, s)) return rc;     // the kernel searches inline from here on
+        launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s);
+        HIPCHK(hipGetLastError());
+        return MAPF_OK;
+    }
+    // not covered by the one-launch kernel: T step_observe launches, same results
+    const size_t BN = (size_t)e->d.B * e->d.N, obs_t = BN * e->d.C * e->d.F * e->d.F;
+    for (int32_t t = 0; t < T; ++t) {
+        const size_t k = slots ? (size_t)t : 0;
+        mapf_step_out ot{};
+        if (out) {
+            auto adv = [&](auto *p, size_t n) { return p ? p + k * n : p; };
+            ot.status = adv(out->status, BN); ot.reward = adv(out->reward, BN);
+            ot.shadow_goals = adv(out->shadow_goals, (size_t)e->d.B); ot.cost = adv(out->cost, BN);
+            ot.train_valid = adv(out->train_valid, BN * 5); ot.actions_fixed = adv(out->actions_fixed, BN);
+            ot.goals_reached = adv(out->goals_reached, BN); ot.constraints = adv(out->constraints, BN);
+            ot.reward_total = adv(out->reward_total, BN);
+        }
+        if (int rc = step_observe_impl(e, actions_out + k * BN, out ? &ot : nullptr, 2u, obs + k * obs_t,
+                                       vec + k * BN * 4, stream))
+            return rc;
+    }
+    return MAPF_OK;
 }
 
 int mapf_flush(mapf_env *e, void *stream) {

@@ -97,6 +97,96 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     TL_STAMP(3);
 }
 
+// The search work an INLINE step left in `d`, done by the same wave right away:
+// agent.bfsMap of every agent whose goal changed (agent order), then the human's
+// next path.  Same items, same results as the work-list searches.
+__device__ inline void step_pairs_search_inline(const DevEnv &e, const PairsDeferred &d, char *lds) {
+    for (uint64_t m = d.bmask; m; m &= m - 1ull) {
+        const int l = __builtin_ctzll(m);
+        const uint32_t ai = (uint32_t)__builtin_amdgcn_readlane((int)d.bitem, l);
+        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d.bgoal, l);
+        srch::search_one<uint32_t, 1>(e, false, (int)(ai / (uint32_t)e.N), ai, g, NO_CELL, 0, lds);
+    }
+    if (d.rmask) {
+        const int l = __builtin_ctzll(d.rmask);
+        const int b = __builtin_amdgcn_readlane((int)d.ritem, l);
+        srch::search_one<uint32_t, 1>(e, true, b, 0u, (uint32_t)__builtin_amdgcn_readlane((int)d.rstart, l),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)d.rgoal, l),
+                                      __builtin_amdgcn_readlane(d.rbuf, l), lds);
+    }
+}
+
+// T committed random-policy steps + observations in ONE launch
+// (mapf_rollout_random; runner.py:64-100 with the uniform policy, T times).
+// Each wave owns one env for the whole launch and loops
+//     step (pair lanes) -> observe its env (LDS bit-stream -> float4 stores)
+//     -> its own search work (BFS maps, the human's next path)
+// so a wave's latency-bound step runs while the other waves' observation stores
+// drain: no launch boundary, dispatch ramp or state reload per step.  Step t's
+// outputs go to slot t of the buffers when `slots` is set (rollout buffers).
+struct RolloutOut {
+    int32_t *actions;
+    StepOut out;
+    float *obs, *vec;
+    int slots;
+};
+
+__host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
+    return e.G == 8 && e.human_mode != 2 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) && e.W <= 30;
+}
+
+__host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
+    return ((obs_lds_bytes(e, 4, true) + 15) & ~(size_t)15) + 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(DevEnv e, int T, RolloutOut ro) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int E = 4;                     // envs per workgroup, one per wave
+    const int b0 = (int)blockIdx.x * E;
+    const int nenv = min(E, e.B - b0);
+    const int le = (int)(threadIdx.x >> 6);
+    const ObsLds L = obs_layout(e, E, smem, true);
+    char *slds = smem + ((obs_lds_bytes(e, E, true) + 15) & ~(size_t)15) +
+                 (size_t)le * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+    const uint32_t mreg = obs_map_word(e, b0, nenv, (int)(threadIdx.x & 63));
+    const size_t BN = (size_t)e.B * e.N;
+    const size_t obs_t = BN * e.C * e.F * e.F;
+    for (int t = 0; t < T; ++t) {
+        const size_t s = ro.slots ? (size_t)t : 0;
+        StepOut o = ro.out;
+        if (o.status) o.status += s * BN;
+        if (o.reward) o.reward += s * BN;
+        if (o.shadow_goals) o.shadow_goals += s * e.B;
+        if (o.cost) o.cost += s * BN;
+        if (o.train_valid) o.train_valid += s * BN * NA;
+        if (o.actions_fixed) o.actions_fixed += s * BN;
+        if (o.goals_reached) o.goals_reached += s * BN;
+        if (o.constraints) o.constraints += s * BN;
+        if (o.reward_total) o.reward_total += s * BN;
+        PairsDeferred dfr;
+        step_pairs_env<8, true, true>(e, ro.actions + s * BN, o, 3u, 0, (int)(blockIdx.x * 256 + threadIdx.x), L, b0,
+                                      RegMap{mreg, true}, dfr);
+        if (le < nenv) {
+            const ObsGroup g = obs_wave_init(e, L, le, mreg);
+            obs_emit<false>(e, L, ro.obs + s * obs_t, ro.vec + s * BN * 4, g, b0, false);
+            step_pairs_search_inline(e, dfr, slds);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+bool rollout_random_fusable(const DevEnv &e) { return rollout_fusable(e) && rollout_lds_bytes(e) <= 64 * 1024; }
+
+bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                           int slots, hipStream_t s) {
+    if (!rollout_random_fusable(e)) return false;
+    const int grid = (e.B + 3) / 4;
+    hipLaunchKernelGGL(rollout_random_kernel, dim3(grid), dim3(256), rollout_lds_bytes(e), s, e, T,
+                       RolloutOut{actions, out, obs, vec, slots});
+    return true;
+}
+
 bool step_observe_fusable(const DevEnv &e) {
     if (e.G > 8 || e.force_agent_lanes || e.human_mode == 2 || e.C >= 7) return false;
     const int E = 256 / (e.G * e.G);

@@ -34,6 +34,11 @@ bool observe_hosts_search(const DevEnv &e);
 bool step_observe_fusable(const DevEnv &e);
 void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,
                          float *obs, float *vec, int nsearch, int sslot, hipStream_t s);
+// T committed random-policy steps + observations in one launch (mapf_fused.hip);
+// false (nothing launched) if the configuration is not covered
+bool rollout_random_fusable(const DevEnv &e);
+bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                           int slots, hipStream_t s);
 void launch_reset_fixed(const DevEnv &e, hipStream_t s);
 void launch_reset_seeded(const DevEnv &e, hipStream_t s);
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,

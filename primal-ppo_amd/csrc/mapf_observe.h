@@ -169,6 +169,9 @@ __device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ 
                                            size_t nt) {
     int z0, z1;
     if (!obs_zero_band(e, z0, z1)) return;
+#ifdef MAPF_DIAG_NOSTORE   // timing diagnostic only: no observation stores
+    if (k0 != 0x7FFFFFFF) return;
+#endif
     const size_t CFF = (size_t)e.C * e.F * e.F;
     float4 *o4 = reinterpret_cast<float4 *>(obs);
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -370,6 +373,9 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     TL_STAMP(4);
 
     // ---- phase 4: bit-stream -> float stores ----
+#ifdef MAPF_DIAG_NOSTORE   // timing diagnostic only: no observation stores
+    if (stream[0] != 0x12345678u) return;
+#endif
     const size_t total = (size_t)K * CFF;
     float *dst = obs + (size_t)b0 * N * CFF;
     if (((E * N * CFF) & 3) == 0) {

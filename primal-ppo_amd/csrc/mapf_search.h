@@ -235,31 +235,17 @@ __host__ __device__ inline size_t wave_lds(int H, int W) {
     return ((planes > img ? planes : img) + 15) & ~(size_t)15;
 }
 
-// All search items of one step (or of a reset), grid-strided over waves.
-//   all = 0: the step's work lists (parity); 1: every env's next path + every
-//   agent's BFS map; 2: every env's next path only.
+// One search item on one wave (wave-uniform arguments):
+//   replan = false: makeBfsMap of agent ai (env b) from its goal sr_cell into bfs[ai];
+//   replan = true:  env b's human path sr_cell -> stop_cell into path buffer `buf`,
+//                   its length into hlen[b][buf].
+// `lds` = wave_lds<T, RW>(H, W) bytes of this wave's LDS.
 template <class T, int RW>
-__device__ void search_items(const DevEnv &e, int parity, int all, char *lds, uint32_t wave_id, uint32_t nwaves) {
+__device__ void search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
+                           int buf, char *lds) {
     const int lane = lane_id();
     const int W = e.W, H = e.H, cells = H * W;
-    const uint32_t n_replan = all ? (uint32_t)e.B : e.counters[C_REPLAN_COUNT + parity];
-    const uint32_t n_bfs = (!e.keep_bfs || all == 2) ? 0u : (all ? (uint32_t)(e.B * e.N) : e.counters[C_BFS_COUNT + parity]);
-    const uint32_t total = n_replan + n_bfs;
-    for (uint32_t item = wave_id; item < total; item += nwaves) {
-        const bool replan = item < n_replan;
-        uint32_t ai = 0, sr_cell, stop_cell = NO_CELL;
-        int b;
-        if (replan) {
-            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];   // parity = list slot
-            stop_cell = e.hnext_goal[b];
-            if (stop_cell == NO_CELL) continue;
-            sr_cell = e.hnext_start[b];
-        } else {
-            const uint32_t k = item - n_replan;
-            ai = all ? k : e.bfs_list[(size_t)parity * e.B * e.N + k];
-            b = (int)(ai / (uint32_t)e.N);
-            sr_cell = e.goal[ai];
-        }
+    {
         const uint32_t *bits = env_map(e, b);
         T fre[RW];
 #pragma unroll
@@ -350,7 +336,6 @@ __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, ui
                     }
                 }
             }
-            const int buf = e.hcur[b] ^ 1;
             uint32_t *path = human_path(e, b, buf);
             int len;
             if (d <= 0) {
@@ -389,6 +374,34 @@ __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, ui
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// All search items of one step (or of a reset), grid-strided over waves.
+//   all = 0: the step's work lists (parity); 1: every env's next path + every
+//   agent's BFS map; 2: every env's next path only.
+template <class T, int RW>
+__device__ void search_items(const DevEnv &e, int parity, int all, char *lds, uint32_t wave_id, uint32_t nwaves) {
+    const uint32_t n_replan = all ? (uint32_t)e.B : e.counters[C_REPLAN_COUNT + parity];
+    const uint32_t n_bfs = (!e.keep_bfs || all == 2) ? 0u : (all ? (uint32_t)(e.B * e.N) : e.counters[C_BFS_COUNT + parity]);
+    const uint32_t total = n_replan + n_bfs;
+    for (uint32_t item = wave_id; item < total; item += nwaves) {
+        const bool replan = item < n_replan;
+        uint32_t ai = 0, sr_cell, stop_cell = NO_CELL;
+        int b, buf = 0;
+        if (replan) {
+            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];   // parity = list slot
+            stop_cell = e.hnext_goal[b];
+            if (stop_cell == NO_CELL) continue;
+            sr_cell = e.hnext_start[b];
+            buf = e.hcur[b] ^ 1;
+        } else {
+            const uint32_t k = item - n_replan;
+            ai = all ? k : e.bfs_list[(size_t)parity * e.B * e.N + k];
+            b = (int)(ai / (uint32_t)e.N);
+            sr_cell = e.goal[ai];
+        }
+        search_one<T, RW>(e, replan, b, ai, sr_cell, stop_cell, buf, lds);
     }
 }
 

@@ -57,6 +57,10 @@ struct PairsDeferred {
     uint64_t bmask = 0, rmask = 0;     // lanes appending to bfs_list / replan_list
     uint32_t bret = 0, rret = 0;       // the leader lane's atomicAdd result
     uint32_t bitem = 0, ritem = 0;
+    // INLINE steps (the multi-step rollout kernel): no lists, the wave searches itself
+    uint32_t bgoal = 0;                // the new goal of a bmask lane's agent
+    uint32_t rstart = 0, rgoal = 0;    // the human's next path (wave-uniform)
+    int rbuf = 0;                      // ... into this path buffer
 };
 
 __device__ inline void step_pairs_finish(const DevEnv &e, const PairsDeferred &d, int slot) {
@@ -80,7 +84,9 @@ __device__ inline void step_pairs_finish(const DevEnv &e, const PairsDeferred &d
 //
 // rm: the shared map in registers (NP = 8 only: one env per wave, so every
 // lane takes part in each map read); dfr: the deferred list appends.
-template <int NP, bool FEED>
+// INLINE (NP = 8, the multi-step rollout kernel): no work lists -- the search
+// items are left in dfr for step_pairs_search_inline() on the same wave.
+template <int NP, bool FEED, bool INLINE = false>
 __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out,
                                                uint32_t flags, int slot, int gt, const ObsLds &ob, int b0,
                                                RegMap rm, PairsDeferred &dfr) {
@@ -91,7 +97,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     // one env per wave at NP = 8: make the env index (and everything derived from
     // per-env loads) wave-uniform, i.e. scalar registers / SALU, not 64 VALU lanes
     const int b = (L == 64) ? __builtin_amdgcn_readfirstlane(gt / L) : gt / L;
-    if (gt == 0 && (flags & 1u)) {
+    if (!INLINE && gt == 0 && (flags & 1u)) {
         e.counters[C_REPLAN_COUNT + (slot + 1) % 3] = 0;
         e.counters[C_BFS_COUNT + (slot + 1) % 3] = 0;
     }
@@ -371,9 +377,11 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     if (e.keep_bfs) {                       // agent.bfsMap recompute (makeBfsMap on goal change, :627)
         const uint64_t bm = __ballot(vi && head && reached);
         if (bm) {
-            if (lane == __builtin_ctzll(bm)) dfr.bret = atomicAdd(&e.counters[C_BFS_COUNT + slot], (uint32_t)__popcll(bm));
+            if (!INLINE && lane == __builtin_ctzll(bm))
+                dfr.bret = atomicAdd(&e.counters[C_BFS_COUNT + slot], (uint32_t)__popcll(bm));
             dfr.bmask = bm;
             dfr.bitem = (uint32_t)ai;
+            dfr.bgoal = ng;
         }
     }
     STAMP(4);
@@ -398,9 +406,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
         }
         const uint64_t rmk = __ballot(li == 0 && ngl != NO_CELL);
         if (rmk) {
-            if (lane == __builtin_ctzll(rmk)) dfr.rret = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], (uint32_t)__popcll(rmk));
+            if (!INLINE && lane == __builtin_ctzll(rmk))
+                dfr.rret = atomicAdd(&e.counters[C_REPLAN_COUNT + slot], (uint32_t)__popcll(rmk));
             dfr.rmask = rmk;
             dfr.ritem = (uint32_t)b;
+            dfr.rstart = ns;
+            dfr.rgoal = ngl;
+            dfr.rbuf = cur2 ^ 1;
         }
     }
     if (li == 0) {

@@ -46,6 +46,8 @@ SIGNATURES = {
     "mapf_observe": (ctypes.c_int, [P, P, P, P]),
     "mapf_step_observe": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), P, P, P]),
     "mapf_step_observe_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), P, P, P]),
+    "mapf_rollout_random": (ctypes.c_int, [P, I32, I32, P, ctypes.POINTER(StepOut), P, P, P]),
+    "mapf_rollout_random_fused": (ctypes.c_int, [P]),
     "mapf_flush": (ctypes.c_int, [P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),

@@ -40,6 +40,7 @@ class BatchedMapfGym:
         self.h = h
         self.path_capacity = _lib.lib().mapf_path_capacity(self.h)
         self.fused = bool(_lib.lib().mapf_step_observe_fused(self.h))   # step_observe = one launch
+        self.rollout_fused = bool(_lib.lib().mapf_rollout_random_fused(self.h))   # rollout_random = one launch
         dev = self.device
         B, N = self.B, self.N
         self.out = dict(
@@ -189,6 +190,32 @@ class BatchedMapfGym:
         so = self._stepout if out is None else self._make_stepout(self._check_out(out))
         _lib.check(fn(self.h, _ptr(actions), ctypes.byref(so), _ptr(obs), _ptr(vec), _stream(self.device)))
         return (self.out if out is None else out), obs, vec
+
+    def rollout_random(self, T, slots=False, actions=None, obs=None, vec=None, out=None):
+        """T x step_observe(random_policy=True) -- runner.py:64-100 with the uniform random
+        policy, T times -- as ONE launch where mapf_rollout_random_fused (each wave owns an
+        env and loops step -> observe -> its search work).  slots: step t writes slot t of
+        [T]-leading buffers (actions [T, B, N], obs [T, B, N, C, F, F], vec [T, B, N, 4],
+        out[k] [T, ...]); otherwise every step overwrites the [B]-leading buffers.
+        Returns (out, obs, vec)."""
+        k = T if slots else 1
+        actions = self.actions if actions is None else actions
+        obs = self.obs if obs is None else obs
+        vec = self.vec if vec is None else vec
+        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == k * self.B * self.N
+        assert obs.is_contiguous() and obs.numel() == k * self.B * self.N * self.C * self.F * self.F
+        assert vec.is_contiguous() and vec.numel() == k * self.B * self.N * 4
+        if out is None:
+            assert not slots, "slots=True needs [T]-leading output buffers (out=...)"
+            so, out = self._stepout, self.out
+        else:
+            for key, t in out.items():
+                ref = self.out[key]
+                assert t.dtype == ref.dtype and t.is_contiguous() and t.numel() == k * ref.numel(), key
+            so = self._make_stepout(out)
+        _lib.check(_lib.lib().mapf_rollout_random(self.h, int(T), 1 if slots else 0, _ptr(actions), ctypes.byref(so),
+                                                  _ptr(obs), _ptr(vec), _stream(self.device)))
+        return out, obs, vec
 
     def _check_out(self, out):
         for k, t in out.items():

@@ -240,6 +240,15 @@ def test_fused_step_observe_matches_oracle(name):
     run_random_case(name, FUSED_CASES[name], "fused")
 
 
+@pytest.mark.parametrize("name", list(FUSED_CASES) + ["c5_80x80_n64_f11_bfsch"])
+def test_rollout_random_matches_oracle(name):
+    """mapf_rollout_random into [T]-slot rollout buffers, 23 steps per call: one launch
+    where covered (c2 shape, n7/n8 shapes: each wave loops step -> observe -> its own
+    search), T step_observe launches elsewhere -- every slot bit-exact vs the oracle."""
+    case = FUSED_CASES.get(name) or RANDOM_CASES[name]
+    run_random_case(name, case, "rollout")
+
+
 def run_random_case(name, case, path):
     B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
     rng = np.random.default_rng(5)
@@ -266,8 +275,25 @@ def run_random_case(name, case, path):
         hp = oracles[b].human_path()
         np.testing.assert_array_equal(st["human_path"][b, :len(hp)], hp)
     checked_obs = 0
+    RT = 23                                   # rollout path: steps per mapf_rollout_random call
+    roll = None
     for t in range(case["steps"]):
-        if path == "fused":
+        if path == "rollout":
+            if t % RT == 0:
+                T = min(RT, case["steps"] - t)
+                roll = dict(actions=torch.zeros(T, B, n, dtype=torch.int32, device=env.device),
+                            obs=torch.full((T, B, n, nch, fov, fov), float("nan"), device=env.device),
+                            vec=torch.full((T, B, n, 4), float("nan"), device=env.device),
+                            out={k: torch.zeros((T,) + tuple(v.shape), dtype=v.dtype, device=env.device)
+                                 for k, v in env.out.items()})
+                env.rollout_random(T, slots=True, **roll)
+                roll = dict(actions=roll["actions"].cpu().numpy(), obs=roll["obs"], vec=roll["vec"],
+                            out=host(roll["out"]))
+            k = t % RT
+            a_host = roll["actions"][k]
+            out = {key: v[k] for key, v in roll["out"].items()}
+            obs, vec = roll["obs"][k], roll["vec"][k]
+        elif path == "fused":
             acts = env.actions
             env.obs.fill_(float("nan"))     # every float of the observation must be written by the launch
             env.vec.fill_(float("nan"))
@@ -298,7 +324,8 @@ def run_random_case(name, case, path):
                 np.testing.assert_array_equal(obs[b], oo, err_msg=f"{name} t={t} b={b} obs")
                 np.testing.assert_array_equal(vec[b], ov, err_msg=f"{name} t={t} b={b} vec")
                 checked_obs += 1
-        if t % 20 == 19:
+        # device state after the step (rollout path: only at the end of a call's T steps)
+        if (t % 20 == 19) if path != "rollout" else (t % RT == RT - 1 or t == case["steps"] - 1):
             st = env.get_state()
             bfs = env.bfs().cpu().numpy()
             for b in range(B):
@@ -394,6 +421,51 @@ def test_c2_full_size_fused_equals_two_launches():
             assert torch.equal(fz.bfs(), pl.bfs())
     assert_no_errors(fz)
     assert_no_errors(pl)
+
+
+@pytest.mark.parametrize("slots", [True, False])
+def test_c2_full_size_rollout_equals_step_observe(slots):
+    """c2 at full size: mapf_rollout_random (one launch of T steps) and T launches of
+    mapf_step_observe_random on two envs with the same seed give identical actions,
+    outputs, observations, state and BFS maps (slots: every step's; else the last)."""
+    from mapf_amd.maps import generate_warehouse
+    B, n, H, W, fov, C = 4096, 8, 20, 20, 11, 6
+    world = generate_warehouse(H, W)
+    envs = []
+    for _ in range(2):
+        e = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=C, human_mode="random", goal_mode="random",
+                   fix_choice=1, seed=4321)
+        e.reset_seeded(world)
+        envs.append(e)
+    ro, so = envs
+    assert ro.rollout_fused
+    for _ in range(3):                       # a step_observe first: pending search work is flushed
+        ro.step_observe(random_policy=True)
+        so.step_observe(random_policy=True)
+    for T in (1, 31, 45):
+        k = T if slots else 1
+        dev = ro.device
+        acts = torch.zeros(k, B, n, dtype=torch.int32, device=dev)
+        obs = torch.full((k, B, n, C, fov, fov), float("nan"), device=dev)
+        vec = torch.full((k, B, n, 4), float("nan"), device=dev)
+        out = {key: torch.full((k,) + tuple(v.shape), -7, dtype=v.dtype, device=dev) for key, v in ro.out.items()}
+        ro.rollout_random(T, slots=slots, actions=acts, obs=obs, vec=vec, out=out)
+        out = host(out)
+        for t in range(T):
+            o_s, obs_s, vec_s = so.step_observe(random_policy=True)
+            if slots or t == T - 1:
+                j = t if slots else 0
+                np.testing.assert_array_equal(acts[j].cpu().numpy(), so.actions.cpu().numpy(), err_msg=f"T={T} t={t}")
+                o_s = host(o_s)
+                for key in o_s:
+                    np.testing.assert_array_equal(out[key][j], o_s[key], err_msg=f"T={T} t={t} {key}")
+                assert torch.equal(obs[j], obs_s) and torch.equal(vec[j], vec_s), f"T={T} t={t} obs"
+        sr, ss = ro.get_state(), so.get_state()
+        for key in ss:
+            np.testing.assert_array_equal(sr[key], ss[key], err_msg=f"T={T} state {key}")
+        assert torch.equal(ro.bfs(), so.bfs()), f"T={T} bfs"
+    assert_no_errors(ro)
+    assert_no_errors(so)
 
 
 # --------------------------------------------------------------- GAE / normalise
