@@ -3,9 +3,19 @@
 A "step" = one lockstep step of every env on the GPU: the random policy's
 actions (Philox, on device) -> getActionStatus ... jointStep (human replans,
 BFS maps on goal changes) -> getAllObservations (all agents' FOV observations
-+ vectors), i.e. runner.py:64-100 with a random policy, issued as ONE
-mapf_step_observe_random launch per step (--split: mapf_step_random +
-mapf_observe, two launches, same results).
++ vectors), i.e. runner.py:64-100 with a random policy.
+
+Paths (--path):
+  rollout (default)  mapf_rollout_random: a random-policy rollout of T steps per
+                     launch (T = --rollout-steps, default 256 = the reference's
+                     N_STEPS, alg_parameters.py:68); each wave owns one env and
+                     loops step -> observe -> its own search work.  Every step's
+                     actions, outputs and observation are written (to the same
+                     [B]-leading buffers; --slots: to [T]-slot rollout buffers).
+  fused              one mapf_step_observe_random launch per step (the path a
+                     policy-in-the-loop rollout uses), hipGraph replays of 24 steps
+  split              mapf_step_random + mapf_observe, two launches per step
+The breakdown also times the one-launch-per-step path.
 
 Default workload (N=1): BASELINE config c2 -- 4096 envs x 8 agents, 20x20
 generalised warehouse, FOV 11, 6 channels, Human with random goals,
@@ -39,7 +49,7 @@ def observe_bytes_per_agent(C, F, H, W, N):
 
 
 def fused_bytes_per_agent(C, F, H, W, N):
-    """Algorithmic HBM bytes per agent of one step_observe launch:
+    """Algorithmic HBM bytes per agent-step of the fused step+observe:
     obs + vec writes (C*F^2*4 + 16); agent state read (cell, goal, last action: 9)
     and written (9); random action (4) and step outputs (status 1, reward 4, cost 4,
     train_valid 20, fixed 4, goal flag 4, constraint 4, total reward 4: 45);
@@ -89,19 +99,21 @@ def make_maps(kind, B, H, W, rank):
     return np.stack([keep_largest_component(random_map(rng, H, W, 0.3)) for _ in range(B)]), False
 
 
-PMC_REPORTS = {"observe_kernel": os.path.join(ROOT, "profiles", "r01_pmc_observe_c2.json"),
-               "step_observe_kernel": os.path.join(ROOT, "profiles", "r01_pmc_step_observe_c2.json")}
+# committed rocprofv3 --pmc passes (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py) of the c2 workload
+PMC_REPORTS = {"observe_kernel": "r01_pmc_observe_c2.json",
+               "step_observe_kernel": "r01_pmc_step_observe_c2.json",
+               "rollout_random_kernel": "r01_pmc_rollout_c2.json"}
 
 
-def pmc_traffic(B, N, H, W, F, C, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
-    (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py; collected by
-    `STEPS=pmc tools/gpu_check.sh`), for the c2 workload only -- null otherwise."""
-    path = PMC_REPORTS.get(kernel)
-    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or path is None or not os.path.exists(path):
+def pmc_traffic_per_step(B, N, H, W, F, C, kernel):
+    """HBM bytes per lockstep step of `kernel` (MB) from the committed PMC report
+    (per launch / steps per launch), for the c2 workload only -- null otherwise."""
+    path = os.path.join(ROOT, "profiles", PMC_REPORTS.get(kernel, "-"))
+    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or not os.path.exists(path):
         return None
     with open(path) as f:
-        return round(json.load(f)["traffic_bytes"] / 1e6, 3)
+        rep = json.load(f)
+    return rep["traffic_bytes"] / rep.get("steps_per_launch", 1) / 1e6
 
 
 def main():
@@ -109,8 +121,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(PRESETS),
                     help="BASELINE.json workload preset (c2 = the headline metric); explicit flags override")
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=1024)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--size", type=int, default=None)
@@ -118,10 +130,18 @@ def main():
     ap.add_argument("--channels", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--split", action="store_true", help="step and observe as two launches")
+    ap.add_argument("--path", default="rollout", choices=["rollout", "fused", "split"])
+    ap.add_argument("--split", action="store_true", help="= --path split")
+    ap.add_argument("--rollout-steps", type=int, default=256, help="steps per mapf_rollout_random launch")
+    ap.add_argument("--slots", action="store_true",
+                    help="rollout path: write step t to slot t of [T]-leading rollout buffers")
     ap.add_argument("--graph-steps", type=int, default=24,
-                    help="steps per captured hipGraph, a multiple of 3 (work-list slots rotate mod 3); 0 = direct")
+                    help="fused/split paths: steps per captured hipGraph, a multiple of 3; 0 = direct")
+    ap.add_argument("--kernel-launches", type=int, default=None,
+                    help="launches timed with HIP events for the roofline kernel (default: per path)")
     args = ap.parse_args()
+    if args.split:
+        args.path = "split"
     preset = PRESETS[args.config]
     for k in ("envs", "agents", "size", "fov", "channels"):
         if getattr(args, k) is None:
@@ -146,26 +166,47 @@ def main():
                                      goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B,
                                      shared_map=shared), device=dev)
     env.reset_seeded(world)
+    path = args.path
+    if path == "rollout" and not env.rollout_fused:
+        path = "fused"                       # the one-launch rollout does not cover this config
     obs, vec, acts = env.obs, env.vec, env.actions
+    K = args.steps
+    T = max(1, min(args.rollout_steps, K))
+
+    roll = None
+    if path == "rollout" and args.slots:    # [T]-slot rollout buffers (runner.py's per-rollout arrays)
+        roll = dict(actions=torch.zeros(T, B, N, dtype=torch.int32, device=dev),
+                    obs=torch.zeros(T, B, N, C, F, F, device=dev), vec=torch.zeros(T, B, N, 4, device=dev),
+                    out={k: torch.zeros((T,) + tuple(v.shape), dtype=v.dtype, device=dev)
+                         for k, v in env.out.items()})
+
+    def rollout(n):
+        if roll is None:
+            env.rollout_random(n)
+        else:
+            env.rollout_random(n, slots=True, actions=roll["actions"][:n], obs=roll["obs"][:n],
+                               vec=roll["vec"][:n], out={k: v[:n] for k, v in roll["out"].items()})
 
     def one_step():
-        if args.split:
+        if path == "split":
             env.step_random(acts)    # random policy's actions drawn in the step kernel
             env.observe(obs, vec)
         else:
             env.step_observe(acts, obs, vec, random_policy=True)
 
+    # warm-up: the timed path and the per-step path of the breakdown
     for _ in range(args.warmup):
         one_step()
+    if path == "rollout":
+        rollout(max(1, min(T, args.warmup)))
     torch.cuda.synchronize()
 
-    # The K timed steps are replays of a hipGraph holding G consecutive steps
-    # (every kernel of every step runs; the graph only removes host launch cost).
+    # fused/split: the K timed steps are replays of a hipGraph holding G consecutive
+    # steps (every kernel of every step runs; the graph only removes host launch cost)
     G = args.graph_steps
-    assert G % 3 == 0, "--graph-steps must be a multiple of 3"
-    K = args.steps
     graph = None
-    if G > 0:
+    if path != "rollout" and G > 0:
+        assert G % 3 == 0, "--graph-steps must be a multiple of 3"
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for _ in range(G):
@@ -173,16 +214,23 @@ def main():
         torch.cuda.synchronize()
         graph.replay()               # these G steps are warm-up too
         torch.cuda.synchronize()
-    n_replay, n_direct = (K // G, K % G) if G > 0 else (0, K)
 
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(n_replay):
-        graph.replay()
-    for _ in range(n_direct):
-        one_step()
+    if path == "rollout":
+        done = 0
+        while done < K:
+            n = min(T, K - done)
+            rollout(n)
+            done += n
+    else:
+        n_replay, n_direct = (K // G, K % G) if graph is not None else (0, K)
+        for _ in range(n_replay):
+            graph.replay()
+        for _ in range(n_direct):
+            one_step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -194,18 +242,25 @@ def main():
 
     # Per-kernel timing: HIP events around each launch on the launch stream
     # (torch's current stream, which the env launches on), direct launches.
-    # (a) the product path: one step_observe launch per step, the previous
-    #     step's search riding in it -- the roofline kernel;
-    # (b) the split path for the breakdown: step / search flushed alone / observe.
-    KT = min(K, 300)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(KT)]
-    for k in range(KT):
-        ev[k][0].record()
-        env.step_observe(acts, obs, vec, random_policy=True)
-        ev[k][1].record()
+    #  rollout: each mapf_rollout_random launch of T steps -- the roofline kernel;
+    #  fused:   one step_observe launch per step (previous step's search riding in it);
+    #  split:   step / search flushed alone / observe.
+    def event_ms(fn, n):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    KT = args.kernel_launches or (max(1, min(20, K // T)) if path == "rollout" else min(K, 300))
+    KS = min(K, 300)
+    fused_ms = event_ms(lambda: env.step_observe(acts, obs, vec, random_policy=True), KS)
     env.flush()
-    for k in range(KT):
-        e0, e1, e2, e3 = ev[k][2:]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KS)]
+    for k in range(KS):
+        e0, e1, e2, e3 = ev[k]
         e0.record()
         env.step_random(acts)
         e1.record()
@@ -214,20 +269,23 @@ def main():
         env.observe(obs, vec)
         e3.record()
     torch.cuda.synchronize()
-    fused_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KT)]))
-    step_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KT)]))
-    search_ms = float(np.mean([ev[k][3].elapsed_time(ev[k][4]) for k in range(KT)]))
-    obs_ms = float(np.mean([ev[k][4].elapsed_time(ev[k][5]) for k in range(KT)]))
+    step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KS)]))
+    search_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(KS)]))
+    obs_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KS)]))
+    roll_ms = event_ms(lambda: rollout(T), KT) if path == "rollout" else None
     counters = env.counters()
 
     if rank == 0:
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
-        if args.split or not env.fused:      # two launches per step: the observe kernel is the roofline one
-            kname, bpa, kms = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms
+        if path == "rollout":
+            kname, bpa, kms, steps_pl = "rollout_random_kernel", fused_bytes_per_agent(C, F, H, W, N), roll_ms, T
+        elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one
+            kname, bpa, kms, steps_pl = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms, 1
         else:
-            kname, bpa, kms = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms
-        achieved = bpa * B * N / (kms * 1e-3) / 1e9
+            kname, bpa, kms, steps_pl = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms, 1
+        achieved = bpa * B * N * steps_pl / (kms * 1e-3) / 1e9
+        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -238,18 +296,23 @@ def main():
                                    f"{C} channels, random policy, env.step+observe",
                        "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
+                       "path": path + (f" (T={T} steps per launch{', slot buffers' if roll else ''})"
+                                       if path == "rollout" else ""),
                        "parallelism": f"env-shards x{world_size}"},
-            "breakdown_ms": {"step_observe": round(fused_ms, 4),
+            "breakdown_ms": {"rollout_launch": round(roll_ms, 4) if roll_ms else None,
+                             "rollout_per_step": round(roll_ms / T, 5) if roll_ms else None,
+                             "step_observe_launch": round(fused_ms, 4),
                              "split": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
                                        "observe_kernel": round(obs_ms, 4)},
-                             "timing": f"HIP events around {KT} direct launches of each path (split: search "
-                                       f"flushed alone); value from hipGraph replays of {G} steps"
-                                       f" ({'fused' if env.fused and not args.split else 'split'} path)"},
+                             "timing": f"HIP events around direct launches ({KT} rollout launches, {KS} of each "
+                                       f"per-step path; split: search flushed alone); value timed over the {path} "
+                                       f"path" + (f" with hipGraph replays of {G} steps" if graph else "")},
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(B, N, H, W, F, C, kname), "traffic_unit": "MB/launch (PMC)",
-                         "algorithmic_mb": round(bpa * B * N / 1e6, 3), "bytes_per_agent": bpa,
-                         "agents_per_launch": B * N},
+                         "traffic": round(traffic * steps_pl, 3) if traffic is not None else None,
+                         "traffic_unit": "MB/launch (PMC)", "steps_per_launch": steps_pl,
+                         "algorithmic_mb": round(bpa * B * N * steps_pl / 1e6, 3), "bytes_per_agent_step": bpa,
+                         "agents_per_step": B * N},
             "device_counters": [int(x) for x in counters[:8]],
         }
         if world_size == 1 and not args.no_cpu:

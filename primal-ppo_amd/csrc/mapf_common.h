@@ -163,7 +163,11 @@ __device__ inline uint64_t stamp_now() {
 #endif
 
 // Wave-level helpers ---------------------------------------------------------
-__device__ inline int lane_id() { return threadIdx.x & 63; }
+__device__ inline int lane_id() {   // volatile: never hoisted out of a loop (keeps per-lane invariants from pinning VGPRs)
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 __device__ inline uint64_t ballot(bool p) { return __ballot(p); }
 __device__ inline uint32_t shfl32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
 __device__ inline uint64_t shfl64(uint64_t v, int src) {

@@ -23,6 +23,8 @@
 // cells, mapf_gym.py:33-38) and agents' BFS maps (read only by mapf_bfs and
 // the BFS channel, which is not fused).  The step of this launch reads none of
 // what they write (the path buffer it walks is the other one).
+#include <cstdlib>
+
 #include "mapf_step_pairs.h"
 #include "mapf_search.h"
 
@@ -100,19 +102,26 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
 // The search work an INLINE step left in `d`, done by the same wave right away:
 // agent.bfsMap of every agent whose goal changed (agent order), then the human's
 // next path.  Same items, same results as the work-list searches.
-__device__ inline void step_pairs_search_inline(const DevEnv &e, const PairsDeferred &d, char *lds) {
+// map: the env's padded obstacle rows in the wave's LDS; rs: the resident state,
+// whose path lengths take the searched path's.
+__device__ inline void step_pairs_search_inline(const DevEnv &e, const PairsDeferred &d, char *lds,
+                                                const uint32_t *map, EnvRegs &rs) {
     for (uint64_t m = d.bmask; m; m &= m - 1ull) {
         const int l = __builtin_ctzll(m);
         const uint32_t ai = (uint32_t)__builtin_amdgcn_readlane((int)d.bitem, l);
         const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d.bgoal, l);
-        srch::search_one<uint32_t, 1>(e, false, (int)(ai / (uint32_t)e.N), ai, g, NO_CELL, 0, lds);
+        srch::search_one<uint32_t, 1>(e, false, (int)(ai / (uint32_t)e.N), ai, g, NO_CELL, 0, lds, map);
     }
     if (d.rmask) {
         const int l = __builtin_ctzll(d.rmask);
         const int b = __builtin_amdgcn_readlane((int)d.ritem, l);
-        srch::search_one<uint32_t, 1>(e, true, b, 0u, (uint32_t)__builtin_amdgcn_readlane((int)d.rstart, l),
-                                      (uint32_t)__builtin_amdgcn_readlane((int)d.rgoal, l),
-                                      __builtin_amdgcn_readlane(d.rbuf, l), lds);
+        const int buf = __builtin_amdgcn_readlane(d.rbuf, l);
+        const int len = srch::search_one<uint32_t, 1>(e, true, b, 0u,
+                                                      (uint32_t)__builtin_amdgcn_readlane((int)d.rstart, l),
+                                                      (uint32_t)__builtin_amdgcn_readlane((int)d.rgoal, l), buf,
+                                                      lds, map);
+        if (buf) rs.hlen1 = len;
+        else rs.hlen0 = len;
     }
 }
 
@@ -135,8 +144,10 @@ __host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
     return e.G == 8 && e.human_mode != 2 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) && e.W <= 30;
 }
 
+// LDS of a rollout workgroup: observation layout | 4 search scratch | 4 path copies
+__host__ __device__ inline size_t rollout_obs_lds(const DevEnv &e) { return (obs_lds_bytes(e, 4, true) + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
-    return ((obs_lds_bytes(e, 4, true) + 15) & ~(size_t)15) + 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+    return rollout_obs_lds(e) + 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W) + 4 * (size_t)e.Lmax * 4;
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(DevEnv e, int T, RolloutOut ro) {
@@ -146,17 +157,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     const int nenv = min(E, e.B - b0);
     const int le = (int)(threadIdx.x >> 6);
     const ObsLds L = obs_layout(e, E, smem, true);
-    char *slds = smem + ((obs_lds_bytes(e, E, true) + 15) & ~(size_t)15) +
-                 (size_t)le * srch::wave_lds<uint32_t, 1>(e.H, e.W);
+    const size_t swl = srch::wave_lds<uint32_t, 1>(e.H, e.W);
+    char *slds = smem + rollout_obs_lds(e) + (size_t)le * swl;
+    uint32_t *lpath = reinterpret_cast<uint32_t *>(smem + rollout_obs_lds(e) + 4 * swl) + (size_t)le * e.Lmax;
     const uint32_t mreg = obs_map_word(e, b0, nenv, (int)(threadIdx.x & 63));
-    const size_t BN = (size_t)e.B * e.N;
-    const size_t obs_t = BN * e.C * e.F * e.F;
+    EnvRegs rs{};
+    if (le < nenv) env_regs_load<8>(e, b0 + le, rs, lpath);
     for (int t = 0; t < T; ++t) {
-        const size_t s = ro.slots ? (size_t)t : 0;
-        StepOut o = ro.out;
+        const DevEnv &E = e;
+        const RolloutOut &R = ro;
+        const size_t BN = (size_t)E.B * E.N;
+        const size_t s = R.slots ? (size_t)t : 0;
+        StepOut o = R.out;
         if (o.status) o.status += s * BN;
         if (o.reward) o.reward += s * BN;
-        if (o.shadow_goals) o.shadow_goals += s * e.B;
+        if (o.shadow_goals) o.shadow_goals += s * E.B;
         if (o.cost) o.cost += s * BN;
         if (o.train_valid) o.train_valid += s * BN * NA;
         if (o.actions_fixed) o.actions_fixed += s * BN;
@@ -164,16 +179,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
         if (o.constraints) o.constraints += s * BN;
         if (o.reward_total) o.reward_total += s * BN;
         PairsDeferred dfr;
-        step_pairs_env<8, true, true>(e, ro.actions + s * BN, o, 3u, 0, (int)(blockIdx.x * 256 + threadIdx.x), L, b0,
-                                      RegMap{mreg, true}, dfr);
+        step_pairs_env<8, true, true, true>(E, R.actions + s * BN, o, 3u, 0, (int)(blockIdx.x * 256 + threadIdx.x),
+                                            L, b0, RegMap{mreg, true}, dfr, &rs);
         if (le < nenv) {
-            const ObsGroup g = obs_wave_init(e, L, le, mreg);
-            obs_emit<false>(e, L, ro.obs + s * obs_t, ro.vec + s * BN * 4, g, b0, false);
-            step_pairs_search_inline(e, dfr, slds);
+            const ObsGroup g = obs_wave_init(E, L, le, mreg);
+            obs_emit<false>(E, L, R.obs + s * BN * E.C * E.F * E.F, R.vec + s * BN * 4, g, b0, false);
+            step_pairs_search_inline(E, dfr, slds, L.mapc + (size_t)le * L.rowsz, rs);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
+    if (le < nenv) env_regs_store<8>(e, b0 + le, rs);
 }
 
 bool rollout_random_fusable(const DevEnv &e) { return rollout_fusable(e) && rollout_lds_bytes(e) <= 64 * 1024; }
@@ -182,7 +198,22 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
                            int slots, hipStream_t s) {
     if (!rollout_random_fusable(e)) return false;
     const int grid = (e.B + 3) / 4;
-    hipLaunchKernelGGL(rollout_random_kernel, dim3(grid), dim3(256), rollout_lds_bytes(e), s, e, T,
+    // Persistent waves: every CU should hold the same number of workgroups, or the
+    // CUs holding more set the pace of every step.  The LDS request caps the
+    // workgroups per CU at ceil(grid / CUs) (160 KiB of LDS per CU).
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    int occ = (grid + ncu - 1) / ncu;
+    if (const char *v = std::getenv("MAPF_ROLL_OCC")) { const int x = std::atoi(v); if (x >= 1 && x <= 16) occ = x; }
+    size_t lds = rollout_lds_bytes(e);
+    const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
+    if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
+    hipLaunchKernelGGL(rollout_random_kernel, dim3(grid), dim3(256), lds, s, e, T,
                        RolloutOut{actions, out, obs, vec, slots});
     return true;
 }

@@ -238,15 +238,17 @@ __host__ __device__ inline size_t wave_lds(int H, int W) {
 // One search item on one wave (wave-uniform arguments):
 //   replan = false: makeBfsMap of agent ai (env b) from its goal sr_cell into bfs[ai];
 //   replan = true:  env b's human path sr_cell -> stop_cell into path buffer `buf`,
-//                   its length into hlen[b][buf].
-// `lds` = wave_lds<T, RW>(H, W) bytes of this wave's LDS.
+//                   its length into hlen[b][buf]; returns that length (0 for a BFS map).
+// `lds` = wave_lds<T, RW>(H, W) bytes of this wave's LDS; `map` = the env's padded
+// obstacle rows if the caller holds a copy (e.g. in LDS), else read from HBM.
 template <class T, int RW>
-__device__ void search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
-                           int buf, char *lds) {
+__device__ int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
+                          int buf, char *lds, const uint32_t *map = nullptr) {
     const int lane = lane_id();
     const int W = e.W, H = e.H, cells = H * W;
+    int len = 0;
     {
-        const uint32_t *bits = env_map(e, b);
+        const uint32_t *bits = map ? map : env_map(e, b);
         T fre[RW];
 #pragma unroll
         for (int k = 0; k < RW; ++k) fre[k] = free_row<T>(e, bits, lane + 64 * k);
@@ -337,7 +339,6 @@ __device__ void search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uin
                 }
             }
             uint32_t *path = human_path(e, b, buf);
-            int len;
             if (d <= 0) {
                 // start == goal (astar_4 returns []) or unreachable (it returns a ValueError):
                 // the reference crashes right after; the human stays put.
@@ -375,6 +376,7 @@ __device__ void search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uin
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
+    return len;
 }
 
 // All search items of one step (or of a reset), grid-strided over waves.

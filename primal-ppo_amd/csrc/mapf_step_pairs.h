@@ -63,6 +63,73 @@ struct PairsDeferred {
     int rbuf = 0;                      // ... into this path buffer
 };
 
+// The state of one wave's env kept in registers across the steps of the
+// multi-step rollout kernel (RES steps): no state loads at the top of a step, so
+// a step never waits (vmcnt counts loads AND stores on gfx9) behind the previous
+// step's observation stores.  The human's current path is copied into the wave's
+// LDS (lp) whenever it switches, so the per-step path reads are LDS reads.
+struct EnvRegs {
+    uint32_t pi, pj, gi;          // per lane (i, j): cells of agents i and j, agent i's goal
+    int la;                       //                  agent i's last action (-1 = none)
+    uint32_t clock, hp, hn, hng, hgoal, hstart, replans;   // per env (wave-uniform)
+    int hs, hcur, hlen0, hlen1;
+    uint32_t *lp;                 // LDS copy of path buffer hcur (Lmax cells)
+};
+
+// path buffer `buf` of env b (len cells) into the wave's LDS copy
+__device__ inline void env_regs_path_to_lds(const DevEnv &e, int b, int buf, int len, uint32_t *lp) {
+    const uint32_t *p = human_path(e, b, buf);
+    for (int k = lane_id(); k < len; k += 64) lp[k] = p[k];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int NP>
+__device__ inline void env_regs_load(const DevEnv &e, int b, EnvRegs &r, uint32_t *lp) {
+    const int lane = lane_id(), i = lane / NP, j = lane % NP;
+    const bool vi = i < e.N, vj = j < e.N;
+    const size_t ai = (size_t)b * e.N + i, aj = (size_t)b * e.N + j;
+    r.pi = vi ? e.pos[ai] : 0u;
+    r.pj = vj ? e.pos[aj] : 0u;
+    r.gi = vi ? e.goal[ai] : 0u;
+    r.la = vi ? (int)e.last_act[ai] : -1;
+    r.clock = e.clock[b];
+    r.hp = e.hpos[b];
+    r.hn = e.hnext[b];
+    r.hng = e.hnext_goal[b];
+    r.hgoal = e.hgoal[b];
+    r.hstart = e.hnext_start[b];
+    r.replans = 0u;
+    r.hs = e.hstep[b];
+    r.hcur = e.hcur[b];
+    r.hlen0 = e.hlen[(size_t)b * 2];
+    r.hlen1 = e.hlen[(size_t)b * 2 + 1];
+    r.lp = lp;
+    env_regs_path_to_lds(e, b, r.hcur, r.hcur ? r.hlen1 : r.hlen0, lp);
+}
+
+template <int NP>
+__device__ inline void env_regs_store(const DevEnv &e, int b, const EnvRegs &r) {
+    const int lane = lane_id(), i = lane / NP, j = lane % NP;
+    if (i < e.N && j == 0) {
+        const size_t ai = (size_t)b * e.N + i;
+        e.pos[ai] = r.pi;
+        e.goal[ai] = r.gi;
+        e.last_act[ai] = (int8_t)r.la;
+    }
+    if (lane == 0) {
+        e.clock[b] = r.clock;
+        e.hpos[b] = r.hp;
+        e.hnext[b] = r.hn;
+        e.hnext_goal[b] = r.hng;
+        e.hgoal[b] = r.hgoal;
+        e.hnext_start[b] = r.hstart;
+        e.hreplans[b] += r.replans;
+        e.hstep[b] = r.hs;
+        e.hcur[b] = r.hcur;
+    }
+}
+
 __device__ inline void step_pairs_finish(const DevEnv &e, const PairsDeferred &d, int slot) {
     const int lane = lane_id();
     if (d.bmask) {
@@ -86,10 +153,11 @@ __device__ inline void step_pairs_finish(const DevEnv &e, const PairsDeferred &d
 // lane takes part in each map read); dfr: the deferred list appends.
 // INLINE (NP = 8, the multi-step rollout kernel): no work lists -- the search
 // items are left in dfr for step_pairs_search_inline() on the same wave.
-template <int NP, bool FEED, bool INLINE = false>
+// RES (with INLINE): the env state lives in *rs (EnvRegs) instead of HBM.
+template <int NP, bool FEED, bool INLINE = false, bool RES = false>
 __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out,
                                                uint32_t flags, int slot, int gt, const ObsLds &ob, int b0,
-                                               RegMap rm, PairsDeferred &dfr) {
+                                               RegMap rm, PairsDeferred &dfr, EnvRegs *rs = nullptr) {
     using namespace pairs;
     constexpr int L = NP * NP;
     constexpr uint32_t ROW = (1u << NP) - 1u;
@@ -119,22 +187,22 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const size_t ai = (size_t)b * N + i, aj = (size_t)b * N + j;
     const uint32_t env_id = e.env_offset + (uint32_t)b;
     // ---- every per-env / per-agent load is issued here, in two dependent rounds
-    const uint32_t clock = e.clock[b];
+    const uint32_t clock = RES ? rs->clock : e.clock[b];
     // calculateCostReward's table (cost_lut[d2], d2 <= R*R) in lanes: lane k holds
     // entry k, read with one permute instead of an fp64 sqrt + divide per lane
     const int RR = e.R * e.R;
     const bool lutreg = L == 64 && RR < 64;      // one env per wave: every lane is active
     const float creg = lutreg ? e.cost_lut[lane_id() <= RR ? lane_id() : 0] : 0.f;
-    const uint32_t hp = e.hpos[b], hn = e.hnext[b];
-    const int hs = e.hstep[b], hcur = e.hcur[b];
-    const int2 hlen2 = *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
-    const uint32_t hng = e.human_mode == 1 ? e.hnext_goal[b] : NO_CELL;
+    const uint32_t hp = RES ? rs->hp : e.hpos[b], hn = RES ? rs->hn : e.hnext[b];
+    const int hs = RES ? rs->hs : e.hstep[b], hcur = RES ? rs->hcur : e.hcur[b];
+    const int2 hlen2 = RES ? make_int2(rs->hlen0, rs->hlen1) : *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
+    const uint32_t hng = e.human_mode == 1 ? (RES ? rs->hng : e.hnext_goal[b]) : NO_CELL;
     const int hsi = e.human_mode == 2 ? e.hseq_idx[b] : 0, hsl = e.human_mode == 2 ? e.hseq_len[b] : 0;
 
-    const uint32_t pi = vi ? e.pos[ai] : 0u, pj = vj ? e.pos[aj] : 0u;
+    const uint32_t pi = RES ? rs->pi : (vi ? e.pos[ai] : 0u), pj = RES ? rs->pj : (vj ? e.pos[aj] : 0u);
     const int ri = prow(pi), ci = pcol(pi), rj = prow(pj), cj = pcol(pj);
-    const uint32_t gi = vi ? e.goal[ai] : 0u;
-    const int la = vi ? (int)e.last_act[ai] : -1;
+    const uint32_t gi = RES ? rs->gi : (vi ? e.goal[ai] : 0u);
+    const int la = RES ? rs->la : (vi ? (int)e.last_act[ai] : -1);
     int a_i, a_j;
     if (flags & 2u) {                       // random policy: one env-uniform Philox draw for all N <= 8 agents
 #if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 1)    // timing diagnostic only
@@ -167,8 +235,10 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     }
     const int L2 = cur2 ? hlen2.y : hlen2.x;
     const uint32_t *p2 = human_path(e, b, cur2);
-    const uint32_t hp_new = p2[hs2];
-    const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
+    if (RES && cur2 != hcur) env_regs_path_to_lds(e, b, cur2, L2, rs->lp);   // the path switches
+    const uint32_t *p2r = RES ? rs->lp : p2;                                  // ... read from LDS
+    const uint32_t hp_new = p2r[hs2];
+    const uint32_t hn_new = p2r[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
     unsigned st_mask = 0x1Fu;
     if (rm.on) {                            // getInvalidActions' static list from the register map
         unsigned m = 0;
@@ -369,7 +439,11 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
             if (i == k) ng = pack(r, c);
         }
     }
-    if (vi && head) {
+    if constexpr (RES) {
+        if (vi) { rs->pi = np; rs->gi = ng; rs->la = fixed; }
+        const uint32_t npj = shfl32(np, base + j * NP);          // agent j's new cell (row j)
+        if (vj) rs->pj = npj;
+    } else if (vi && head) {
         e.pos[ai] = np;
         e.goal[ai] = ng;
         e.last_act[ai] = (int8_t)fixed;
@@ -389,7 +463,11 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     // ---- human.nextStep (see step_kernel): side effects of the advance decided above
     if (at_end) {
         if (e.human_mode == 1) {
-            if (swapped && li == 0) { e.hgoal[b] = hng; e.hreplans[b] += 1u; }
+            if (RES) {
+                if (swapped) { rs->hgoal = hng; rs->replans += 1u; }
+            } else if (swapped && li == 0) {
+                e.hgoal[b] = hng; e.hreplans[b] += 1u;
+            }
         } else if (e.human_mode == 2) {
             if (li == 0) {
                 e.hgoal[b] = e.hseq[(size_t)b * e.HS + (seq_idx < hsl ? seq_idx : hsl - 1)];
@@ -400,7 +478,10 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     if (swapped) {
         uint32_t ns, ngl;
         plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0, rm);
-        if (li == 0) {
+        if (RES) {
+            rs->hstart = ns;
+            rs->hng = ngl;
+        } else if (li == 0) {
             e.hnext_start[b] = ns;
             e.hnext_goal[b] = ngl;
         }
@@ -415,7 +496,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
             dfr.rbuf = cur2 ^ 1;
         }
     }
-    if (li == 0) {
+    if (RES) {
+        rs->hcur = cur2;
+        rs->hs = hs2;
+        rs->hp = hp_new;
+        rs->hn = hn_new;
+        rs->clock = clock + 1u;
+    } else if (li == 0) {
         e.hcur[b] = cur2;
         e.hstep[b] = hs2;
         e.hpos[b] = hp_new;
@@ -442,7 +529,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
         if (li == 0) ob.shn[le] = hn_new;
         if (e.use_hp && e.C >= 6) {       // human.path[1..K] of the path it walks after the step
             const int kp = e.k_predict;
-            for (int q = 1 + li; q <= kp && q < L2; q += L) ob.shp[le * kp + q - 1] = p2[q];
+            for (int q = 1 + li; q <= kp && q < L2; q += L) ob.shp[le * kp + q - 1] = p2r[q];
             if (li == 0) ob.shpn[le] = min(kp, L2 - 1);
         } else if (li == 0) {
             ob.shpn[le] = 0;

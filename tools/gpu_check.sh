@@ -48,7 +48,8 @@ for s in $STEPS; do
     pmc)
       for ctr in WRITE_SIZE FETCH_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
-          -d "$OUT/pmc_$ctr" -o run -- python3 "$ROOT/bench.py" --steps 60 --warmup 10 --no-cpu --graph-steps 0) > "$OUT/pmc_$ctr.log" 2>&1
+          -d "$OUT/pmc_$ctr" -o run -- python3 "$ROOT/bench.py" --steps 64 --warmup 10 --no-cpu --graph-steps 0 \
+          --rollout-steps 32 --kernel-launches 4 ${PMC_ARGS:-}) > "$OUT/pmc_$ctr.log" 2>&1
         rc=$?; echo "pmc $ctr rc=$rc"; stop_if_fatal $rc pmc
       done
       find "$OUT" -path "*pmc_*" -name "*.csv" | head ;;
@@ -57,12 +58,13 @@ for s in $STEPS; do
       for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_INSTS_BRANCH" ${SQ_EXTRA:-}; do
         i=$((i+1))
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
-          -d "$OUT/sq_$i" -o run -- python3 "$ROOT/bench.py" --steps 30 --warmup 10 --no-cpu --graph-steps 0) > "$OUT/sq_$i.log" 2>&1
+          -d "$OUT/sq_$i" -o run -- python3 "$ROOT/bench.py" --steps 64 --warmup 10 --no-cpu --graph-steps 0 \
+          --rollout-steps 32 --kernel-launches 4) > "$OUT/sq_$i.log" 2>&1
         rc=$?; echo "sq $i ($grp) rc=$rc"; stop_if_fatal $rc sq
       done ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 20 --no-cpu) > "$OUT/prof.log" 2>&1
+        -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --no-cpu ${PROF_ARGS:-}) > "$OUT/prof.log" 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; stop_if_fatal $rc prof
       find "$OUT/prof" -name "*stats*" | head ;;
   esac

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--kernel", default="observe_kernel<false>")
     ap.add_argument("--algorithmic-bytes", type=float, default=None,
                     help="algorithmic bytes per launch, for the ratio")
+    ap.add_argument("--steps-per-launch", type=int, default=1,
+                    help="lockstep steps one launch of the kernel runs (mapf_rollout_random: T)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     w_kib, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
@@ -46,6 +48,7 @@ def main():
         "kernel": a.kernel, "launches": {"WRITE_SIZE": nw, "FETCH_SIZE": nf},
         "write_bytes": w, "fetch_bytes_raw": f, "fetch_bytes_x2": 2 * f,
         "traffic_bytes": w + f,
+        "steps_per_launch": a.steps_per_launch,
         "note": "per launch; counters in KiB x1024; WRITE_SIZE exact for 16 B/lane stores; "
                 "FETCH_SIZE raw (narrow reads, uncalibrated), x2 = wide-read correction upper bound",
     }

@@ -17,11 +17,11 @@ for lib in $LIBS; do
     i=$((i+1))
     d="$OUT/sq_${lib}_$i"
     (cd /tmp && export TMPDIR=/tmp && MAPF_LIB="$ROOT/primal-ppo_amd/lib/$lib.so" timeout -s KILL 120 rocprofv3 --pmc $grp \
-      --kernel-trace --output-format csv -d "$d" -o run -- python3 "$ROOT/bench.py" --steps 30 --warmup 10 --no-cpu \
-      --graph-steps 0) > "$OUT/sq_${lib}_$i.log" 2>&1
+      --kernel-trace --output-format csv -d "$d" -o run -- python3 "$ROOT/bench.py" --steps 64 --warmup 10 --no-cpu \
+      --graph-steps 0 --rollout-steps 32 --kernel-launches 4 ${BENCH_ARGS:-}) > "$OUT/sq_${lib}_$i.log" 2>&1
     rc=$?; echo "sq $lib $i rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$OUT/sq_${lib}_$i.log"; exit $rc; fi
     dirs="$dirs $d"
   done
-  python3 tools/pmc_table.py $dirs --kernel step_observe_kernel
+  python3 tools/pmc_table.py $dirs --kernel ${KERNEL:-rollout_random_kernel}
 done
