@@ -144,8 +144,8 @@ __host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
     return e.G == 8 && e.human_mode != 2 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) && e.W <= 30;
 }
 
-// LDS of a rollout workgroup: observation layout | 4 search scratch | 4 path copies
-__host__ __device__ inline size_t rollout_obs_lds(const DevEnv &e) { return (obs_lds_bytes(e, 4, true) + 15) & ~(size_t)15; }
+// LDS of a rollout workgroup: observation layout | nibble table | 4 search scratch | 4 path copies
+__host__ __device__ inline size_t rollout_obs_lds(const DevEnv &e) { return ((obs_lds_bytes(e, 4, true) + 15) & ~(size_t)15) + 256; }
 __host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
     return rollout_obs_lds(e) + 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W) + 4 * (size_t)e.Lmax * 4;
 }
@@ -156,7 +156,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     const int b0 = (int)blockIdx.x * E;
     const int nenv = min(E, e.B - b0);
     const int le = (int)(threadIdx.x >> 6);
-    const ObsLds L = obs_layout(e, E, smem, true);
+    ObsLds L = obs_layout(e, E, smem, true);
+    float4 *lut = reinterpret_cast<float4 *>(smem + rollout_obs_lds(e) - 256);
+    obs_lut_init(lut);
+    __syncthreads();
+    L.lut = lut;
     const size_t swl = srch::wave_lds<uint32_t, 1>(e.H, e.W);
     char *slds = smem + rollout_obs_lds(e) + (size_t)le * swl;
     uint32_t *lpath = reinterpret_cast<uint32_t *>(smem + rollout_obs_lds(e) + 4 * swl) + (size_t)le * e.Lmax;

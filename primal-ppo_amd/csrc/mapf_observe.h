@@ -38,6 +38,7 @@ struct ObsLds {
     uint8_t *idg;               // [E][H*W] agent index at each occupied cell (read only where occ is set)
     uint32_t *bfsw;             // BFS channel: [E*N][F][WD] dwords = 2*WD int16 cells of each FOV row's
     int32_t *bfsown;            //   bfsMap window, from column (tc & ~1); [E*N] bfsMap at the agent's cell
+    const float4 *lut;          // optional [16] float4: nibble -> its 4 bits as 0.f / 1.f (obs_lut_init)
     int stream_words, rowsz;
 };
 
@@ -77,7 +78,15 @@ __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem, bool per
     L.bfsw = reinterpret_cast<uint32_t *>(L.shpn + E);
     L.bfsown = reinterpret_cast<int32_t *>(L.bfsw + (obs_bfs_windows(e) ? (size_t)E * e.N * e.F * obs_bfs_wd(e) : 0));
     L.idg = reinterpret_cast<uint8_t *>(L.bfsown + (obs_bfs_windows(e) ? E * e.N : 0));
+    L.lut = nullptr;
     return L;
+}
+
+// the 16-entry nibble -> float4 table (256 B of LDS, 16-B aligned), filled by the
+// first 16 threads; the caller synchronises before use
+__device__ inline void obs_lut_init(float4 *lut) {
+    const int t = (int)threadIdx.x;
+    if (t < 16) lut[t] = make_float4((float)(t & 1), (float)((t >> 1) & 1), (float)((t >> 2) & 1), (float)(t >> 3));
 }
 
 namespace obsd {
@@ -378,7 +387,21 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
 #endif
     const size_t total = (size_t)K * CFF;
     float *dst = obs + (size_t)b0 * N * CFF;
-    if (((E * N * CFF) & 3) == 0) {
+    if (G.wave && L.lut && !skip_band && ((K * CFF) & 3) == 0) {
+        // one wave, one env, whole float4s: lane l stores float4 q = l + 64k, whose 4 bits
+        // are bits 4(l & 7).. of stream word (l >> 3) + 8k -- a lane-constant field (one
+        // v_bfe), an 8-lane LDS broadcast -- and the float4 of that nibble comes from the
+        // 16-entry LDS table L.lut: one 1 KiB store per wave instruction, constant step.
+        const int sh = (tid & 7) * 4;
+        const uint32_t *swp = stream + (tid >> 3);
+        float4 *dp = reinterpret_cast<float4 *>(dst) + tid;
+#pragma unroll 4
+        for (int rem = ((K * CFF) >> 2) - tid; rem > 0; rem -= 64) {
+            *dp = L.lut[__builtin_amdgcn_ubfe(*swp, sh, 4)];
+            swp += 8;
+            dp += 64;
+        }
+    } else if (((E * N * CFF) & 3) == 0) {
         const size_t n4 = total >> 2;
         float4 *d4 = reinterpret_cast<float4 *>(dst);
         int z0 = 0, z1 = 0;
