@@ -107,7 +107,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.obs_envs = 64 / d.N > 1 ? 64 / d.N : 1;
     d.step_block = 256;
     d.search_blocks = 64;
-    d.band_blocks = 256;
+    d.band_blocks = 0;       // zero-band workgroups (MAPF_BAND_BLOCKS): slower than the waves' table-driven stores
     if (const char *v = std::getenv("MAPF_BAND_BLOCKS")) { int x = std::atoi(v); if (x >= 0 && x <= 4096) d.band_blocks = x; }
     if (const char *v = std::getenv("MAPF_SEARCH_BLOCKS")) { int x = std::atoi(v); if (x >= 1 && x <= 1024) d.search_blocks = x; }
     if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }

@@ -72,7 +72,13 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     // and each wave then observes its own env with no workgroup barrier
     const bool regmap = NP == 8 && regmap_fits(e);
     const bool per_wave = regmap && fused_per_wave(e);
-    const ObsLds L = obs_layout(e, E, smem, per_wave);
+    ObsLds L = obs_layout(e, E, smem, per_wave);
+    if (per_wave && nband == 0) {     // the waves write every float: nibble table for their store loops
+        float4 *lut = reinterpret_cast<float4 *>(smem + ((obs_lds_bytes(e, E, true) + 15) & ~(size_t)15));
+        obs_lut_init(lut);
+        __syncthreads();
+        L.lut = lut;
+    }
     const uint32_t mreg = obs_map_word(e, b0, nenv, regmap ? (int)(threadIdx.x & 63) : (int)threadIdx.x);
     PairsDeferred dfr;
 #ifdef MAPF_DIAG_NOSTEP   // timing diagnostic only (make diag): observe the pre-step state, no step
@@ -241,6 +247,7 @@ static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uin
         nband = e.band_blocks;
     const int grid = (e.B + E - 1) / E + nsearch + nband;
     size_t lds = obs_lds_bytes(e, E, per_wave);
+    if (per_wave && nband == 0) lds = ((lds + 15) & ~(size_t)15) + 256;   // + the nibble table
     if (nsearch > 0) {
         const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
         if (sl > lds) lds = sl;
