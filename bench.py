@@ -102,7 +102,7 @@ def make_maps(kind, B, H, W, rank):
 # committed rocprofv3 --pmc passes (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py) of the c2 workload
 PMC_REPORTS = {"observe_kernel": "r01_pmc_observe_c2.json",
                "step_observe_kernel": "r01_pmc_step_observe_c2.json",
-               "rollout_random_kernel": "r01_pmc_rollout_c2.json"}
+               "rollout_random_kernel": "r01_pmc_rollout_c2.json"}   # (the [B]-buffer, plain-store launch)
 
 
 def pmc_traffic_per_step(B, N, H, W, F, C, kernel):
@@ -279,7 +279,8 @@ def main():
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
         if path == "rollout":
-            kname, bpa, kms, steps_pl = "rollout_random_kernel", fused_bytes_per_agent(C, F, H, W, N), roll_ms, T
+            kname = "rollout_random_kernel" + ("<true> (nontemporal stores)" if roll else "")
+            bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, T
         elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one
             kname, bpa, kms, steps_pl = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms, 1
         else:

@@ -156,6 +156,10 @@ __host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
     return rollout_obs_lds(e) + 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W) + 4 * (size_t)e.Lmax * 4;
 }
 
+// NT: nontemporal observation stores -- for slot buffers (fresh HBM lines every step,
+// measured faster); re-written [B]-leading buffers keep plain stores (their lines
+// stay cache-resident between steps, measured faster).
+template <bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(DevEnv e, int T, RolloutOut ro) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int E = 4;                     // envs per workgroup, one per wave
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
                                             L, b0, RegMap{mreg, true}, dfr, &rs);
         if (le < nenv) {
             const ObsGroup g = obs_wave_init(E, L, le, mreg);
-            obs_emit<false>(E, L, R.obs + s * BN * E.C * E.F * E.F, R.vec + s * BN * 4, g, b0, false);
+            obs_emit<false, NT>(E, L, R.obs + s * BN * E.C * E.F * E.F, R.vec + s * BN * 4, g, b0, false);
             step_pairs_search_inline(E, dfr, slds, L.mapc + (size_t)le * L.rowsz, rs);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -223,8 +227,12 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     size_t lds = rollout_lds_bytes(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
-    hipLaunchKernelGGL(rollout_random_kernel, dim3(grid), dim3(256), lds, s, e, T,
-                       RolloutOut{actions, out, obs, vec, slots});
+    if (slots)
+        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T,
+                           RolloutOut{actions, out, obs, vec, slots});
+    else
+        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, e, T,
+                           RolloutOut{actions, out, obs, vec, slots});
     return true;
 }
 

@@ -195,7 +195,8 @@ __device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ 
 // that follows obs_init and the agents' staging.  skip_band: the zero band's
 // whole float4s were written by obs_zero_band_store in this launch.
 // BFSCH = false compiles the BFS channel (C = 7) out (the fused launch never
-// has it: step_observe_fusable).
+// has it: step_observe_fusable).  NT: the table-driven store loop (L.lut) uses
+// nontemporal stores.
 // The threads that observe a run of the workgroup's envs together: the whole
 // workgroup (workgroup barriers) or one wave observing its own env (per_env
 // layout; wave-level ordering only).
@@ -234,7 +235,7 @@ __device__ inline ObsGroup obs_wave_init(const DevEnv &e, const ObsLds &L, int l
     return g;
 }
 
-template <bool BFSCH = true>
+template <bool BFSCH = true, bool NT = false>
 __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restrict__ obs, float *__restrict__ vec,
                                 const ObsGroup &G, int b0, bool skip_band = false) {
     using namespace obsd;
@@ -397,7 +398,13 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         float4 *dp = reinterpret_cast<float4 *>(dst) + tid;
 #pragma unroll 4
         for (int rem = ((K * CFF) >> 2) - tid; rem > 0; rem -= 64) {
-            *dp = L.lut[__builtin_amdgcn_ubfe(*swp, sh, 4)];
+            const float4 f = L.lut[__builtin_amdgcn_ubfe(*swp, sh, 4)];
+            if constexpr (NT) {   // streaming stores (rollout slot buffers: not re-read by this launch)
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4f{f.x, f.y, f.z, f.w}, reinterpret_cast<v4f *>(dp));
+            } else {
+                *dp = f;
+            }
             swp += 8;
             dp += 64;
         }
