@@ -147,7 +147,8 @@ struct RolloutOut {
 };
 
 __host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
-    return e.G == 8 && e.human_mode != 2 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) && e.W <= 30;
+    return e.G == 8 && e.human_mode != 2 && e.goal_mode == 1 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) &&
+           e.W <= 30;
 }
 
 // LDS of a rollout workgroup: observation layout | nibble table | 4 search scratch | 4 path copies
@@ -177,6 +178,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     const uint32_t mreg = obs_map_word(e, b0, nenv, (int)(threadIdx.x & 63));
     EnvRegs rs{};
     if (le < nenv) env_regs_load<8>(e, b0 + le, rs, lpath);
+    // every prologue load has landed before the loop: otherwise the compiler keeps a
+    // register's load "pending" at the loop header and waits vmcnt(0) -- i.e. behind
+    // all of the previous step's stores -- where the loop uses it
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt/lgkmcnt untouched
     for (int t = 0; t < T; ++t) {
         const DevEnv &E = e;
         const RolloutOut &R = ro;

@@ -75,18 +75,22 @@ __device__ bool group_free_cell(const DevEnv &e, uint32_t env_id, uint32_t purpo
 // planned (and searched) ahead of time.  Mode 1: a fresh getFreeCell goal on the
 // human's world (entrance marked) from the entrance; mode 2: the next scripted
 // pose from the current one; mode 0 (LoopingHuman) never switches.
+// hmode: the human mode if the caller has it as a constant (-1: e.human_mode);
+// entr: the entrance cell if the caller holds it (have_entr), else read e.hentr[b].
 __device__ inline void plan_next_path(const DevEnv &e, int b, uint32_t env_id, uint32_t epoch, int seq_idx,
-                                      uint32_t &nstart, uint32_t &ngoal, bool leader, RegMap rm = RegMap{0u, false}) {
+                                      uint32_t &nstart, uint32_t &ngoal, bool leader, RegMap rm = RegMap{0u, false},
+                                      int hmode = -1, uint32_t entr = 0u, bool have_entr = false) {
     nstart = NO_CELL;
     ngoal = NO_CELL;
-    if (e.human_mode == 1) {
-        const uint32_t ent = e.hentr[b];
+    if (hmode < 0) hmode = e.human_mode;
+    if (hmode == 1) {
+        const uint32_t ent = have_entr ? entr : e.hentr[b];
         const uint32_t *bits = env_map(e, b);
         auto ok = [&](int r, int c) -> bool { return !rm.obstacle(e, bits, r, c) && pack(r, c) != ent; };
         int r, c;
         if (group_free_cell(e, env_id, P_HGOAL, 0, epoch, ok, r, c)) { nstart = ent; ngoal = pack(r, c); }
         else if (leader) atomicAdd(&e.counters[C_FREECELL], 1u);
-    } else if (e.human_mode == 2) {
+    } else if (hmode == 2) {
         if (seq_idx + 1 < e.hseq_len[b]) {
             nstart = e.hseq[(size_t)b * e.HS + seq_idx];
             ngoal = e.hseq[(size_t)b * e.HS + seq_idx + 1];

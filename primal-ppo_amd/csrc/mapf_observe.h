@@ -249,6 +249,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     const int E = G.nenv;
 
     // ---- phase 1: worldWithAgents as a padded bitmap per env + agent index grid ----
+#ifndef MAPF_DIAG_NOOBS123   // timing diagnostic only: phases 1-3 compiled out (the stream stays zero)
     const int HW = e.H * e.W;
     for (int k = tid; k < K; k += nt) {
         const int le = G.le0 + k / N;
@@ -382,6 +383,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     obs_sync(G);
     TL_STAMP(4);
 
+#endif
     // ---- phase 4: bit-stream -> float stores ----
 #ifdef MAPF_DIAG_NOSTORE   // timing diagnostic only: no observation stores
     if (stream[0] != 0x12345678u) return;

@@ -71,7 +71,8 @@ struct PairsDeferred {
 struct EnvRegs {
     uint32_t pi, pj, gi;          // per lane (i, j): cells of agents i and j, agent i's goal
     int la;                       //                  agent i's last action (-1 = none)
-    uint32_t clock, hp, hn, hng, hgoal, hstart, replans;   // per env (wave-uniform)
+    float creg;                   //                  cost_lut[lane] (calculateCostReward's table in lanes)
+    uint32_t clock, hp, hn, hng, hgoal, hstart, hentr, replans;   // per env (wave-uniform)
     int hs, hcur, hlen0, hlen1;
     uint32_t *lp;                 // LDS copy of path buffer hcur (Lmax cells)
 };
@@ -93,7 +94,10 @@ __device__ inline void env_regs_load(const DevEnv &e, int b, EnvRegs &r, uint32_
     r.pj = vj ? e.pos[aj] : 0u;
     r.gi = vi ? e.goal[ai] : 0u;
     r.la = vi ? (int)e.last_act[ai] : -1;
+    const int RR = e.R * e.R;
+    r.creg = RR < 64 ? e.cost_lut[lane <= RR ? lane : 0] : 0.f;
     r.clock = e.clock[b];
+    r.hentr = e.hentr[b];
     r.hp = e.hpos[b];
     r.hn = e.hnext[b];
     r.hng = e.hnext_goal[b];
@@ -192,12 +196,16 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     // entry k, read with one permute instead of an fp64 sqrt + divide per lane
     const int RR = e.R * e.R;
     const bool lutreg = L == 64 && RR < 64;      // one env per wave: every lane is active
-    const float creg = lutreg ? e.cost_lut[lane_id() <= RR ? lane_id() : 0] : 0.f;
+    const float creg = !lutreg ? 0.f : RES ? rs->creg : e.cost_lut[lane_id() <= RR ? lane_id() : 0];
     const uint32_t hp = RES ? rs->hp : e.hpos[b], hn = RES ? rs->hn : e.hnext[b];
     const int hs = RES ? rs->hs : e.hstep[b], hcur = RES ? rs->hcur : e.hcur[b];
     const int2 hlen2 = RES ? make_int2(rs->hlen0, rs->hlen1) : *reinterpret_cast<const int2 *>(e.hlen + (size_t)b * 2);
-    const uint32_t hng = e.human_mode == 1 ? (RES ? rs->hng : e.hnext_goal[b]) : NO_CELL;
-    const int hsi = e.human_mode == 2 ? e.hseq_idx[b] : 0, hsl = e.human_mode == 2 ? e.hseq_len[b] : 0;
+    // RES: human modes 0 / 1 and random goals only (rollout_fusable), so the scripted
+    // human's and the goal sequences' loads are compiled out of the rollout loop
+    const int hmode = RES ? (e.human_mode == 1 ? 1 : 0) : e.human_mode;
+    const int gmode = RES ? 1 : e.goal_mode;
+    const uint32_t hng = hmode == 1 ? (RES ? rs->hng : e.hnext_goal[b]) : NO_CELL;
+    const int hsi = hmode == 2 ? e.hseq_idx[b] : 0, hsl = hmode == 2 ? e.hseq_len[b] : 0;
 
     const uint32_t pi = RES ? rs->pi : (vi ? e.pos[ai] : 0u), pj = RES ? rs->pj : (vj ? e.pos[aj] : 0u);
     const int ri = prow(pi), ci = pcol(pi), rj = prow(pj), cj = pcol(pj);
@@ -226,9 +234,9 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     bool swapped = false, at_end = hs >= Lc - 1;
     if (at_end) {
         hs2 = 0;
-        if (e.human_mode == 1) {
+        if (hmode == 1) {
             if (hng != NO_CELL) { cur2 = hcur ^ 1; swapped = true; }
-        } else if (e.human_mode == 2) {
+        } else if (hmode == 2) {
             seq_idx = hsi + 1;
             if (seq_idx < hsl) { cur2 = hcur ^ 1; swapped = true; }
         }
@@ -409,7 +417,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     if (true) {
     } else
 #endif
-    if (e.goal_mode == 0) {
+    if (gmode == 0) {
         if (reached && head) {
             int cur = e.seq_cur[ai];
             const int len = e.seq_len[ai];
@@ -462,13 +470,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
 
     // ---- human.nextStep (see step_kernel): side effects of the advance decided above
     if (at_end) {
-        if (e.human_mode == 1) {
+        if (hmode == 1) {
             if (RES) {
                 if (swapped) { rs->hgoal = hng; rs->replans += 1u; }
             } else if (swapped && li == 0) {
                 e.hgoal[b] = hng; e.hreplans[b] += 1u;
             }
-        } else if (e.human_mode == 2) {
+        } else if (hmode == 2) {
             if (li == 0) {
                 e.hgoal[b] = e.hseq[(size_t)b * e.HS + (seq_idx < hsl ? seq_idx : hsl - 1)];
                 e.hseq_idx[b] = seq_idx;
@@ -477,7 +485,8 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     }
     if (swapped) {
         uint32_t ns, ngl;
-        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0, rm);
+        plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, ngl, li == 0, rm, hmode,
+                       RES ? rs->hentr : 0u, RES);
         if (RES) {
             rs->hstart = ns;
             rs->hng = ngl;

@@ -28,9 +28,12 @@ def main():
                                      goal_mode="random", fix_choice=1, seed=1234))
     env.reset_seeded(generate_warehouse(20, 20))
     split = os.environ.get("SPLIT", "0") == "1"     # default: the fused step+observe launch
+    roll = os.environ.get("ROLLOUT", "0") == "1"    # the multi-step rollout launch (last step's phases)
 
     def one():
-        if split:
+        if roll:
+            env.rollout_random(32)
+        elif split:
             env.step_random()
             env.observe()
         else:
