@@ -73,8 +73,8 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     const bool regmap = NP == 8 && regmap_fits(e);
     const bool per_wave = regmap && fused_per_wave(e);
     ObsLds L = obs_layout(e, E, smem, per_wave);
-    if (per_wave && nband == 0) {     // the waves write every float: nibble table for their store loops
-        float4 *lut = reinterpret_cast<float4 *>(smem + ((obs_lds_bytes(e, E, true) + 15) & ~(size_t)15));
+    if (nband == 0) {     // the step workgroups write every float: nibble table for their store loops
+        float4 *lut = reinterpret_cast<float4 *>(smem + ((obs_lds_bytes(e, E, per_wave) + 15) & ~(size_t)15));
         obs_lut_init(lut);
         __syncthreads();
         L.lut = lut;
@@ -260,7 +260,7 @@ static void launch_np(const DevEnv &e, int32_t *actions, const StepOut &out, uin
         nband = e.band_blocks;
     const int grid = (e.B + E - 1) / E + nsearch + nband;
     size_t lds = obs_lds_bytes(e, E, per_wave);
-    if (per_wave && nband == 0) lds = ((lds + 15) & ~(size_t)15) + 256;   // + the nibble table
+    if (nband == 0) lds = ((lds + 15) & ~(size_t)15) + 256;   // + the nibble table
     if (nsearch > 0) {
         const size_t sl = 4 * srch::wave_lds<uint32_t, 1>(e.H, e.W);
         if (sl > lds) lds = sl;

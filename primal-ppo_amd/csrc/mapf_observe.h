@@ -410,6 +410,19 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             swp += 8;
             dp += 64;
         }
+    } else if (!G.wave && L.lut && !skip_band && ((E * N * CFF) & 3) == 0 && (nt & 7) == 0) {
+        // the same table-driven expansion for a workgroup's stream: thread t's float4s
+        // q = t + nt*k keep the bit field 4(t & 7) of words (t >> 3) + (nt / 8) k
+        const int sh = (tid & 7) * 4;
+        const uint32_t *swp = stream + (tid >> 3);
+        float4 *dp = reinterpret_cast<float4 *>(dst) + tid;
+        for (int rem = (int)(total >> 2) - tid; rem > 0; rem -= nt) {
+            *dp = L.lut[__builtin_amdgcn_ubfe(*swp, sh, 4)];
+            swp += nt >> 3;
+            dp += nt;
+        }
+        for (size_t q = ((total >> 2) << 2) + tid; q < total; q += nt)
+            dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
     } else if (((E * N * CFF) & 3) == 0) {
         const size_t n4 = total >> 2;
         float4 *d4 = reinterpret_cast<float4 *>(dst);

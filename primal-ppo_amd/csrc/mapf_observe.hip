@@ -33,7 +33,10 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     const int E = e.obs_envs;
     const int b0 = ((int)blockIdx.x - nsearch) * E;
     const int nenv = min(E, e.B - b0);
-    const ObsLds L = obs_layout(e, E, smem);
+    ObsLds L = obs_layout(e, E, smem);
+    float4 *lut = reinterpret_cast<float4 *>(smem + ((obs_lds_bytes(e, E) + 15) & ~(size_t)15));
+    obs_lut_init(lut);              // ordered before use by the barrier below
+    L.lut = lut;
     obs_init(e, L, E, b0, nenv, obs_map_word(e, b0, nenv, threadIdx.x));
     obs_load_agents(e, L, b0, nenv);
     TL_STAMP(1);
@@ -43,7 +46,7 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     TL_STAMP(3);
 }
 
-size_t observe_lds(const DevEnv &e) { return obs_lds_bytes(e, e.obs_envs); }
+size_t observe_lds(const DevEnv &e) { return ((obs_lds_bytes(e, e.obs_envs) + 15) & ~(size_t)15) + 256; }   // + nibble table
 
 bool observe_hosts_search(const DevEnv &e) { return e.W <= 32 && e.H <= 64; }
 
