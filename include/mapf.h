@@ -173,8 +173,10 @@ int mapf_step_observe_random(mapf_env *env, int32_t *actions_out, const mapf_ste
  * observe -> its own search work, so steps overlap other envs' store drains. */
 int mapf_rollout_random(mapf_env *env, int32_t T, int32_t slots, int32_t *actions_out, const mapf_step_out *out,
                         float *obs, float *vec, void *stream);
-/* 1 if mapf_rollout_random runs as one launch for this configuration (N in 5..8,
- * shared map of width <= 30, no BFS channel, no scripted human). */
+/* 1 if mapf_rollout_random runs as one launch for this configuration: N in 5..8
+ * with a whole number of float4s per env's observation, one shared map whose
+ * padded bitmap fits 64 words (W + 2*(F/2) <= 32, H + 2*(F/2) <= 64), no BFS
+ * channel, Human or LoopingHuman, random (MapfGym) goals. */
 int mapf_rollout_random_fused(const mapf_env *env);
 
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the

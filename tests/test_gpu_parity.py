@@ -240,16 +240,29 @@ def test_fused_step_observe_matches_oracle(name):
     run_random_case(name, FUSED_CASES[name], "fused")
 
 
-@pytest.mark.parametrize("name", list(FUSED_CASES) + ["c5_80x80_n64_f11_bfsch"])
+# configurations the one-launch rollout kernel covers (N in 5..8 with whole float4s
+# per env, a shared map whose padded bitmap fits 64 words -- W + 2*(F//2) <= 32 --,
+# Human / LoopingHuman, random goals): ragged B
+# (not a multiple of the 4 envs per workgroup), FOV 7/9/11, DA + HP channels, dense maps
+ROLLOUT_CASES = {
+    "r_n6_16x16_f9_dahp": dict(B=37, H=16, W=16, n=6, fov=9, nch=6, steps=120, map="wh", da=1, hp=1),
+    "r_n8_22x22_f11_looping": dict(B=18, H=22, W=22, n=8, fov=11, nch=6, steps=120, map="wh", human="looping"),
+    "r_n6_12x12_f7_dense": dict(B=41, H=12, W=12, n=6, fov=7, nch=6, steps=150, map="wh", allow=(2,)),
+    "r_n8_24x24_f9": dict(B=9, H=24, W=24, n=8, fov=9, nch=6, steps=100, map="wh"),   # padded row = 32 bits
+}
+
+
+@pytest.mark.parametrize("name", list(FUSED_CASES) + list(ROLLOUT_CASES) + ["c5_80x80_n64_f11_bfsch"])
 def test_rollout_random_matches_oracle(name):
     """mapf_rollout_random into [T]-slot rollout buffers, 23 steps per call: one launch
-    where covered (c2 shape, n7/n8 shapes: each wave loops step -> observe -> its own
-    search), T step_observe launches elsewhere -- every slot bit-exact vs the oracle."""
-    case = FUSED_CASES.get(name) or RANDOM_CASES[name]
-    run_random_case(name, case, "rollout")
+    where covered (each wave loops step -> observe -> its own search; the ROLLOUT_CASES
+    and the c2 shape), T step_observe launches elsewhere -- every slot bit-exact vs the
+    oracle."""
+    case = FUSED_CASES.get(name) or ROLLOUT_CASES.get(name) or RANDOM_CASES[name]
+    run_random_case(name, case, "rollout", expect_rollout_fused=name in ROLLOUT_CASES or name.startswith("c2"))
 
 
-def run_random_case(name, case, path):
+def run_random_case(name, case, path, expect_rollout_fused=None):
     B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
     rng = np.random.default_rng(5)
     maps, shared = build_maps(case, B, rng)
@@ -259,6 +272,8 @@ def run_random_case(name, case, path):
                  use_hp=case.get("hp", 0), human_mode=human, goal_mode="random", fix_choice=1, shared_map=shared,
                  seed=seed, env_offset=7)
     env.reset_seeded(maps)
+    if expect_rollout_fused is not None:
+        assert env.rollout_fused == expect_rollout_fused, name
     hm = {"random": 1, "looping": 0}[human]
     cfg = O.make_config(H, W, n, fov, nch, use_da=case.get("da", 0), use_hp=case.get("hp", 0), human_mode=hm,
                         goal_mode=1, fix_choice=1, seed=seed, env_offset=7)
