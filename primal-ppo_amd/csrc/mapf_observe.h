@@ -403,7 +403,13 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             const float4 f = L.lut[__builtin_amdgcn_ubfe(*swp, sh, 4)];
             if constexpr (NT) {   // streaming stores (rollout slot buffers: not re-read by this launch)
                 typedef float v4f __attribute__((ext_vector_type(4)));
+#if defined(MAPF_SLOT_STORE) && MAPF_SLOT_STORE == 2     // store-policy experiment: sc1 (line dropped from L2)
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dp), "v"(v4f{f.x, f.y, f.z, f.w}) : "memory");
+#elif defined(MAPF_SLOT_STORE) && MAPF_SLOT_STORE == 3   // store-policy experiment: plain
+                *dp = f;
+#else
                 __builtin_nontemporal_store(v4f{f.x, f.y, f.z, f.w}, reinterpret_cast<v4f *>(dp));
+#endif
             } else {
                 *dp = f;
             }
