@@ -225,6 +225,27 @@ int mapf_normalize_advantages(const float *ret, const float *v, const float *cre
 int mapf_sample_actions(const float *ps, int32_t ps_stride, int32_t *actions, int64_t *actions64, int32_t M,
                         uint64_t seed, uint32_t step, void *stream);
 
+/* ---- Policy acting forward: fused elementwise epilogues (csrc/mapf_policy.hip) ----
+ * SCRIMPNet.forward (net.py:101-155) under autocast with no grad (Model.step /
+ * Model.value, model.py:26-69); each call replaces two or three of torch's passes
+ * over one activation.  fp16 tensors are passed as uint16_t bit patterns; all
+ * pointers DEVICE, contiguous; dropout p in [0, 1) (0 = off), masks from Philox(seed).
+ *   nhwc_bias_relu       x[rows][C] = relu(x + bias)                 conv + F.relu (net.py:104-112)
+ *   nhwc_bias_relu_pool2 out = maxpool2(relu(x + bias)), x [B][H][W][C] conv + relu + pool1/pool2
+ *   layernorm_f16        y(fp16)[rows][512] = LayerNorm(x fp32, row stride)   transformer.py:7-24
+ *   dropout_residual     x(fp32) += dropout(y fp16), n % 4 == 0        Residual(... do1/do2)
+ *   gelu_dropout_f16     h = dropout(gelu(h)), n % 4 == 0               MLP_Block (transformer.py:27-45)
+ *   tokens               x[B][L+1][D] = dropout(cat(cls, A*VV) + pos)  net.py:124-131 */
+int mapf_nhwc_bias_relu(uint16_t *x, const uint16_t *bias, int64_t rows, int32_t C, void *stream);
+int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t *out, int32_t B, int32_t H, int32_t W,
+                              int32_t C, void *stream);
+int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
+                       int64_t rows, int32_t dim, float eps, void *stream);
+int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint64_t seed, void *stream);
+int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *stream);
+int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
+                int32_t D, float p, uint64_t seed, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

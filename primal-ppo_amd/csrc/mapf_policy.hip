@@ -1,0 +1,274 @@
+// primal-ppo_amd/csrc/mapf_policy.hip -- fused elementwise kernels of the
+// SCRIMPNet acting forward (net.py:101-155 run under torch.autocast with no
+// grad: Model.step / Model.value, model.py:26-69).
+//
+// Every kernel here is HBM-bound and replaces two or three of PyTorch's
+// elementwise passes over the same tensor (the rollout forward moves tensors of
+// 32,768 agents x 17 tokens x 512):
+//   nhwc_bias_relu          conv bias + ReLU on an NHWC fp16 conv output (in place)
+//   nhwc_bias_relu_pool2    conv bias + ReLU + 2x2 max-pool (nn.MaxPool2d(2), floor)
+//   layernorm_f16           LayerNorm of the fp32 residual stream, written as the fp16
+//                           the next autocast linear would cast it to
+//   dropout_residual        x(fp32) += dropout(y(fp16))      (PreNorm residual, do1/do2)
+//   gelu_dropout_f16        h = dropout(gelu(h))  in place   (MLP_Block af1 + do1)
+//   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
+// The training forward keeps PyTorch's ops (autograd needs them).
+//
+// Dropout: keep with probability 1 - p, kept values scaled by 1 / (1 - p) (torch's
+// inverted dropout); the mask bits come from Philox4x32-10 (mapf_common.h) keyed by
+// `seed` -- a different stream than torch's own generator; the reference's masks
+// are random anyway (the net is never eval()-ed, net.py:50-51).
+#include <hip/hip_fp16.h>
+
+#include "mapf.h"
+#include "mapf_common.h"
+
+namespace mapf {
+namespace pol {
+
+__device__ inline float h2f(uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xFFFFu))); }
+__device__ inline uint32_t f2h(float f) { return (uint32_t)__half_as_ushort(__float2half_rn(f)); }
+__device__ inline uint2 pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return make_uint2(a | (b << 16), c | (d << 16));
+}
+
+// 4 keep decisions from one Philox draw (bit k: element 4*i + k kept)
+__device__ inline unsigned keep4(uint64_t seed, uint64_t i, uint32_t thr) {
+    const u32x4 r = philox((uint32_t)i, (uint32_t)(i >> 32), 0xD0u, 0x5EEDu, seed);
+    return (r.x >= thr ? 1u : 0u) | (r.y >= thr ? 2u : 0u) | (r.z >= thr ? 4u : 0u) | (r.w >= thr ? 8u : 0u);
+}
+inline uint32_t drop_threshold(float p) {
+    const double t = (double)p * 4294967296.0;
+    return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// ---- conv epilogues (NHWC fp16, C % 4 == 0, C <= 1024) -------------------------
+// torch: the conv's fp16 output + fp16 bias (rounded to fp16), then ReLU
+__global__ __launch_bounds__(256) void nhwc_bias_relu(uint16_t *__restrict__ x, const uint16_t *__restrict__ bias,
+                                                      long rows, int C) {
+    const int c4n = C >> 2;
+    const int per = 256 / c4n;                      // rows per block pass
+    const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
+    if (tr >= per) return;
+    const uint2 bb = *reinterpret_cast<const uint2 *>(bias + 4 * c4);
+    const float b0 = h2f(bb.x), b1 = h2f(bb.x >> 16), b2 = h2f(bb.y), b3 = h2f(bb.y >> 16);
+    for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
+        uint2 *p = reinterpret_cast<uint2 *>(x + r * C) + c4;
+        const uint2 v = *p;
+        *p = pack4(f2h(fmaxf(h2f(f2h(h2f(v.x) + b0)), 0.f)), f2h(fmaxf(h2f(f2h(h2f(v.x >> 16) + b1)), 0.f)),
+                   f2h(fmaxf(h2f(f2h(h2f(v.y) + b2)), 0.f)), f2h(fmaxf(h2f(f2h(h2f(v.y >> 16) + b3)), 0.f)));
+    }
+}
+
+// in [B][H][W][C] -> out [B][H/2][W/2][C]: relu(round(max(window) + b)) equals the
+// max over the window of relu(round(x + b)) (both maps are monotone)
+__global__ __launch_bounds__(256) void nhwc_bias_relu_pool2(const uint16_t *__restrict__ x,
+                                                            const uint16_t *__restrict__ bias,
+                                                            uint16_t *__restrict__ out, int B, int H, int W, int C) {
+    const int Ho = H / 2, Wo = W / 2;
+    const long rows = (long)B * Ho * Wo;
+    const int c4n = C >> 2;
+    const int per = 256 / c4n;
+    const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
+    if (tr >= per) return;
+    const uint2 bb = *reinterpret_cast<const uint2 *>(bias + 4 * c4);
+    const float bv[4] = {h2f(bb.x), h2f(bb.x >> 16), h2f(bb.y), h2f(bb.y >> 16)};
+    for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
+        const long b = r / (Ho * Wo);
+        const int rem = (int)(r - b * Ho * Wo), i = rem / Wo, j = rem - i * Wo;
+        float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int di = 0; di < 2; ++di)
+#pragma unroll
+            for (int dj = 0; dj < 2; ++dj) {
+                const uint2 v =
+                    *(reinterpret_cast<const uint2 *>(x + ((b * H + 2 * i + di) * (long)W + 2 * j + dj) * C) + c4);
+                m[0] = fmaxf(m[0], h2f(v.x));
+                m[1] = fmaxf(m[1], h2f(v.x >> 16));
+                m[2] = fmaxf(m[2], h2f(v.y));
+                m[3] = fmaxf(m[3], h2f(v.y >> 16));
+            }
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f2h(fmaxf(h2f(f2h(m[k] + bv[k])), 0.f));
+        *(reinterpret_cast<uint2 *>(out + r * C) + c4) = pack4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// ---- LayerNorm: one wave per row of D = 512 fp32 (8 per lane) -> fp16 ---------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x, long xstride,
+                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                     uint16_t *__restrict__ y, long rows, float eps) {
+    constexpr int D = 512;
+    const int lane = (int)(threadIdx.x & 63);
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4 *xr = reinterpret_cast<const float4 *>(x + row * xstride);
+    const float4 a = xr[lane], c = xr[64 + lane];                 // elements 4l..4l+3 and 256+4l..
+    const float mean = wave_sum(a.x + a.y + a.z + a.w + c.x + c.y + c.z + c.w) * (1.f / D);
+    const float d[8] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean, c.x - mean, c.y - mean, c.z - mean, c.w - mean};
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss += d[k] * d[k];
+    const float rstd = 1.f / sqrtf(wave_sum(ss) * (1.f / D) + eps);
+    const float4 g0 = reinterpret_cast<const float4 *>(gamma)[lane], g1 = reinterpret_cast<const float4 *>(gamma)[64 + lane];
+    const float4 e0 = reinterpret_cast<const float4 *>(beta)[lane], e1 = reinterpret_cast<const float4 *>(beta)[64 + lane];
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = f2h(d[k] * rstd * g[k] + e[k]);
+    uint2 *yr = reinterpret_cast<uint2 *>(y + row * D);
+    yr[lane] = pack4(o[0], o[1], o[2], o[3]);
+    yr[64 + lane] = pack4(o[4], o[5], o[6], o[7]);
+}
+
+// ---- dropout epilogues -----------------------------------------------------------
+// x[i] += dropout(y[i]); torch: dropout on the fp16 tensor (y * scale rounded to fp16),
+// then fp16 + fp32 -> fp32
+__global__ __launch_bounds__(256) void dropout_residual(float *__restrict__ x, const uint16_t *__restrict__ y, long n4,
+                                                        uint32_t thr, float scale, uint64_t seed) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const unsigned k = thr ? keep4(seed, (uint64_t)i, thr) : 15u;
+        const uint2 v = reinterpret_cast<const uint2 *>(y)[i];
+        float4 a = reinterpret_cast<float4 *>(x)[i];
+        a.x += (k & 1u) ? h2f(f2h(h2f(v.x) * scale)) : 0.f;
+        a.y += (k & 2u) ? h2f(f2h(h2f(v.x >> 16) * scale)) : 0.f;
+        a.z += (k & 4u) ? h2f(f2h(h2f(v.y) * scale)) : 0.f;
+        a.w += (k & 8u) ? h2f(f2h(h2f(v.y >> 16) * scale)) : 0.f;
+        reinterpret_cast<float4 *>(x)[i] = a;
+    }
+}
+
+// h = dropout(gelu(h)) in place: exact (erf) GELU in fp32 rounded to fp16 like torch's
+// fp16 GELU, then dropout on the fp16 values
+__global__ __launch_bounds__(256) void gelu_dropout_f16(uint16_t *__restrict__ h, long n4, uint32_t thr, float scale,
+                                                        uint64_t seed) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const unsigned k = thr ? keep4(seed, (uint64_t)i, thr) : 15u;
+        uint2 *p = reinterpret_cast<uint2 *>(h) + i;
+        const uint2 v = *p;
+        const uint32_t in[4] = {v.x, v.x >> 16, v.y, v.y >> 16};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float a = h2f(in[q]);
+            const float g = h2f(f2h(0.5f * a * (1.f + erff(a * 0.70710678118654752f))));
+            o[q] = ((k >> q) & 1u) ? f2h(g * scale) : 0u;
+        }
+        *p = pack4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// x[b][0][:] = cls + pos[0];  x[b][1+t][:] = A[b][t] * VV[b][:] + pos[1+t];  then dropout
+// (all fp32: softmax output A is fp32 under autocast, the fp16 VV promotes).
+// A fp32 [B][L], VV fp16 [B][D], cls fp32 [D], pos fp32 [L+1][D]; D % 4 == 0.
+__global__ __launch_bounds__(256) void tokens(float *__restrict__ x, const float *__restrict__ A,
+                                              const uint16_t *__restrict__ VV, const float *__restrict__ cls,
+                                              const float *__restrict__ pos, long B, int L, int D, uint32_t thr,
+                                              float scale, uint64_t seed) {
+    const int d4n = D >> 2;
+    const long n4 = B * (L + 1) * d4n;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const long row = i / d4n;
+        const int d4 = (int)(i - row * d4n);
+        const long b = row / (L + 1);
+        const int t = (int)(row - b * (L + 1));
+        const float4 pp = reinterpret_cast<const float4 *>(pos + (long)t * D)[d4];
+        float4 v;
+        if (t == 0) {
+            const float4 c = reinterpret_cast<const float4 *>(cls)[d4];
+            v = make_float4(c.x + pp.x, c.y + pp.y, c.z + pp.z, c.w + pp.w);
+        } else {
+            const float a = A[b * L + t - 1];
+            const uint2 w = reinterpret_cast<const uint2 *>(VV + b * D)[d4];
+            v = make_float4(a * h2f(w.x) + pp.x, a * h2f(w.x >> 16) + pp.y, a * h2f(w.y) + pp.z,
+                            a * h2f(w.y >> 16) + pp.w);
+        }
+        if (thr) {
+            const unsigned k = keep4(seed, (uint64_t)i, thr);
+            v.x = (k & 1u) ? v.x * scale : 0.f;
+            v.y = (k & 2u) ? v.y * scale : 0.f;
+            v.z = (k & 4u) ? v.z * scale : 0.f;
+            v.w = (k & 8u) ? v.w * scale : 0.f;
+        }
+        reinterpret_cast<float4 *>(x)[i] = v;
+    }
+}
+
+inline int grid_for(long items, int per_block) {
+    long g = (items + per_block - 1) / per_block;
+    if (g > 16384) g = 16384;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace pol
+}  // namespace mapf
+
+using namespace mapf;
+
+extern "C" {
+
+int mapf_nhwc_bias_relu(uint16_t *x, const uint16_t *bias, int64_t rows, int32_t C, void *stream) {
+    if (!x || !bias || rows < 0 || C <= 0 || (C & 3) || C > 1024) return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    const int per = 256 / (C / 4);
+    hipLaunchKernelGGL(pol::nhwc_bias_relu, dim3(pol::grid_for(rows, per)), dim3(256), 0, (hipStream_t)stream, x, bias,
+                       (long)rows, (int)C);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t *out, int32_t B, int32_t H, int32_t W,
+                              int32_t C, void *stream) {
+    if (!x || !bias || !out || B < 0 || H < 2 || W < 2 || C <= 0 || (C & 3) || C > 1024) return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const int per = 256 / (C / 4);
+    const long rows = (long)B * (H / 2) * (W / 2);
+    hipLaunchKernelGGL(pol::nhwc_bias_relu_pool2, dim3(pol::grid_for(rows, per)), dim3(256), 0, (hipStream_t)stream, x,
+                       bias, out, (int)B, (int)H, (int)W, (int)C);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
+                       int64_t rows, int32_t dim, float eps, void *stream) {
+    if (!x || !gamma || !beta || !y || rows < 0 || dim != 512 || (x_row_stride & 3)) return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::layernorm_f16, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x,
+                       (long)x_row_stride, gamma, beta, y, (long)rows, eps);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint64_t seed, void *stream) {
+    if (!x || !y || n < 0 || (n & 3) || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
+    if (n == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::dropout_residual, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, x, y,
+                       (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *stream) {
+    if (!h || n < 0 || (n & 3) || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
+    if (n == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::gelu_dropout_f16, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, h,
+                       (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
+                int32_t D, float p, uint64_t seed, void *stream) {
+    if (!x || !A || !VV || !cls || !pos || B < 0 || L < 1 || D <= 0 || (D & 3) || !(p >= 0.f && p < 1.f))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const long n4 = (long)B * (L + 1) * (D / 4);
+    hipLaunchKernelGGL(pol::tokens, dim3(pol::grid_for(n4, 256)), dim3(256), 0, (hipStream_t)stream, x, A, VV, cls,
+                       pos, (long)B, (int)L, (int)D, pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+}  // extern "C"

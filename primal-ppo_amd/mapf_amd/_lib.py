@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("MAPF_LIB", os.path.join(PKG, "lib", "libmapf.so"))
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
 U32 = ctypes.c_uint32
+I64 = ctypes.c_int64
 
 
 class ResetSpec(ctypes.Structure):
@@ -60,6 +61,13 @@ SIGNATURES = {
     "mapf_gae": (ctypes.c_int, [P, P, P, P, P, I32, I32, ctypes.c_double, ctypes.c_double, P]),
     "mapf_normalize_advantages": (ctypes.c_int, [P, P, P, P, P, P, I32, ctypes.c_double, I32, P]),
     "mapf_sample_actions": (ctypes.c_int, [P, I32, P, P, I32, ctypes.c_uint64, U32, P]),
+    # policy acting forward epilogues (csrc/mapf_policy.hip)
+    "mapf_nhwc_bias_relu": (ctypes.c_int, [P, P, I64, I32, P]),
+    "mapf_nhwc_bias_relu_pool2": (ctypes.c_int, [P, P, P, I32, I32, I32, I32, P]),
+    "mapf_layernorm_f16": (ctypes.c_int, [P, I64, P, P, P, I64, I32, ctypes.c_float, P]),
+    "mapf_dropout_residual": (ctypes.c_int, [P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
+    "mapf_gelu_dropout_f16": (ctypes.c_int, [P, I64, ctypes.c_float, ctypes.c_uint64, P]),
+    "mapf_tokens": (ctypes.c_int, [P, P, P, P, P, I64, I32, I32, ctypes.c_float, ctypes.c_uint64, P]),
 }
 
 _lib = None

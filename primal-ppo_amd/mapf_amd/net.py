@@ -15,6 +15,7 @@ The tokeniser keeps the reference's exact arithmetic: its einsum
 length-1 axis, so every token equals the summed-V projection (kept literally).
 Runs under torch autocast like the reference (net.py:101).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -92,7 +93,8 @@ class _SelfAttention(nn.Module):
         b, n, d = x.shape
         h = self.heads
         w, bias = self.to_qkv.weight, self.to_qkv.bias
-        q = F.linear(x[:, :1], w[:d], bias[:d]).view(b, 1, h, d // h).transpose(1, 2)          # b, h, 1, dh
+        # x[:, 0] is a 2-D strided view: one GEMM with lda = n*d ([b, 1, d] would run as a slow bmm)
+        q = F.linear(x[:, 0], w[:d], bias[:d]).view(b, 1, h, d // h).transpose(1, 2)           # b, h, 1, dh
         kv = F.linear(x, w[d:], bias[d:]).view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)      # 2, b, h, n, dh
         out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=self.scale).transpose(1, 2).reshape(b, 1, d)
         return self.do1(self.nn1(out))
@@ -174,11 +176,14 @@ class SCRIMPNet(nn.Module):
         self.cost_value_layer = nn.Linear(W, 1)
         self.blocking_layer = nn.Linear(W, 1)
         self.apply(_xavier_like)
+        self.fused_acting = True      # no-grad GPU forward through _forward_fused (csrc/mapf_policy.hip)
 
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
         obs: [..., N, C, F, F] (any leading shape); the agent axis is num_agents (EnvParameters.N_AGENTS
-        when not given at construction)."""
+        when not given at construction).  Acting on the GPU (no grad): _forward_fused."""
+        if self.fused_acting and obs.is_cuda and not torch.is_grad_enabled() and self.cT == 512:
+            return self._forward_fused(obs, vector)
         with torch.autocast(device_type=obs.device.type, enabled=obs.device.type == "cuda"):
             n_agents = self.num_agents or EnvParameters.N_AGENTS
             F_ = self.fov or obs.shape[-1]
@@ -215,3 +220,101 @@ class SCRIMPNet(nn.Module):
             cost_value = self.cost_value_layer(x)
             blocking = torch.sigmoid(self.blocking_layer(x))
         return policy, value, blocking, policy_sig, x, logits, cost_value
+
+    # ------------------------------------------------------------ acting fast path
+    def _forward_fused(self, obs, vector):
+        """forward() for acting (no grad, GPU): the same operations at the same precision
+        as forward() under autocast, with the elementwise epilogues in the HIP kernels of
+        csrc/mapf_policy.hip -- conv bias + ReLU (+ max-pool) in one pass over each NHWC
+        activation, LayerNorm written straight as the fp16 the next linear reads, dropout
+        + residual add, GELU + dropout, tokeniser + positional embedding + dropout in one
+        pass.  Dropout masks come from the kernels' Philox stream (seeded from torch's
+        CPU generator), not from torch's."""
+        from . import _lib
+        lib, chk = _lib.lib(), _lib.check
+        dev = obs.device
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        seeds = iter(torch.randint(0, 2 ** 62, (16,), dtype=torch.int64).tolist())
+        drop = lambda m: float(m.p) if m.training else 0.0
+        with torch.autocast(device_type="cuda"):
+            n_agents = self.num_agents or EnvParameters.N_AGENTS
+            F_ = self.fov or obs.shape[-1]
+            x = obs.reshape(-1, self.num_channel, F_, F_).contiguous(memory_format=torch.channels_last)
+            v = vector.reshape(-1, NetParameters.VECTOR_LEN)
+
+            def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
+                y = F.conv2d(x, m.weight, None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
+                b = m.bias.to(torch.float16)
+                B_, C_, H_, W_ = y.shape
+                if pool:
+                    out = torch.empty((B_, C_, H_ // 2, W_ // 2), dtype=y.dtype, device=dev,
+                                      memory_format=torch.channels_last)
+                    chk(lib.mapf_nhwc_bias_relu_pool2(ptr(y), ptr(b), ptr(out), B_, H_, W_, C_, st))
+                    return out
+                chk(lib.mapf_nhwc_bias_relu(ptr(y), ptr(b), B_ * H_ * W_, C_, st))
+                return y
+
+            x = conv(conv(conv(x, self.conv1), self.conv1a), self.conv1b, pool=True)
+            x = conv(conv(conv(x, self.conv2), self.conv2a), self.conv2b, pool=True)
+            x = conv(x, self.conv3).flatten(1)
+            g = F.relu(self.fully_connected_1(v))
+            x3 = torch.cat((x, g), -1)
+            h = self.fully_connected_3(F.relu(self.fully_connected_2(x3)))
+            h = F.relu(h + x3).unsqueeze(1)                                   # [b, 1, 512]
+            b = h.shape[0]
+            hf = h.reshape(b, self.cT)                                        # 2-D GEMMs, not [b,1,512] bmm
+            A = torch.matmul(hf, self.token_wA.sum(0).transpose(0, 1)).unsqueeze(-1).softmax(dim=-1)
+            A = A.reshape(b, self.L).float().contiguous()                     # [b, 16] (all ones: length-1 softmax)
+            VV = torch.matmul(hf, self.token_wV.sum(0)).contiguous()           # [b, 512] fp16
+            xt = torch.empty(b, self.L + 1, self.cT, dtype=torch.float32, device=dev)
+            cls, pos = self.cls_token.detach().contiguous(), self.pos_embedding.detach().contiguous()
+            chk(lib.mapf_tokens(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
+                                drop(self.dropout), next(seeds), st))
+            x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop)[:, 0]
+            x = self.nn_same(self.nn_same(x))
+            x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
+            logits = self.policy_layer(x)
+            policy = logits.softmax(dim=-1)
+            policy_sig = torch.sigmoid(logits)
+            value = self.value_layer(x)
+            cost_value = self.cost_value_layer(x)
+            blocking = torch.sigmoid(self.blocking_layer(x))
+        return policy, value, blocking, policy_sig, x, logits, cost_value
+
+    def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop):
+        """self.transformer(x, first_only=True) on the fused epilogues; x fp32 [b, n, d] is
+        updated in place (the residual stream) and token 0 after the last block returned."""
+        layers = self.transformer.layers
+        b, n, d = x.shape
+
+        def ln(x, norm):                        # LayerNorm -> the fp16 the next linear reads
+            y = torch.empty(x.shape, dtype=torch.float16, device=x.device)
+            chk(lib.mapf_layernorm_f16(ptr(x), d, ptr(norm.weight), ptr(norm.bias), ptr(y), x.numel() // d, d,
+                                       float(norm.eps), st))
+            return y
+
+        def residual(x, y, m):                  # x += dropout(y)
+            y = y.contiguous()
+            chk(lib.mapf_dropout_residual(ptr(x), ptr(y), x.numel(), drop(m), next(seeds), st))
+
+        for li, (att, ff) in enumerate(layers):
+            a = att.fn.fn
+            hh = a.heads
+            y = ln(x, att.fn.norm)
+            if li < len(layers) - 1:
+                qkv = a.to_qkv(y).view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
+                out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
+                residual(x, a.nn1(out.transpose(1, 2).reshape(b, n, d)), a.do1)
+            else:                               # the last block: token 0's query only (see _Encoder)
+                w, bias = a.to_qkv.weight, a.to_qkv.bias
+                q = F.linear(y[:, 0], w[:d], bias[:d]).view(b, 1, hh, d // hh).transpose(1, 2)
+                kv = F.linear(y, w[d:], bias[d:]).view(b, n, 2, hh, d // hh).permute(2, 0, 3, 1, 4)
+                out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
+                x = x[:, :1].contiguous()
+                residual(x, a.nn1(out.transpose(1, 2).reshape(b, 1, d)), a.do1)
+            f = ff.fn.fn
+            hid = f.nn1(ln(x, ff.fn.norm)).contiguous()
+            chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(f.do1), next(seeds), st))
+            residual(x, f.nn2(hid), f.do2)
+        return x

@@ -1,0 +1,109 @@
+"""GPU tests of the acting forward's fused epilogues (csrc/mapf_policy.hip):
+SCRIMPNet._forward_fused against the same network's PyTorch path (autocast fp16,
+dropout off in both: the paths draw different dropout masks), and the dropout
+kernels' keep rate and scaling.  The reference outputs themselves pin the PyTorch
+path (tests/test_net.py, fp32 CPU)."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+
+
+def _net(n_agents=8):
+    from mapf_amd.model import Model
+    torch.manual_seed(3)
+    return Model(0, "cuda", numChannel=6, num_agents=n_agents, fov=9).network
+
+
+@pytest.mark.parametrize("B", [5, 256])
+def test_fused_acting_forward_matches_torch_path(B):
+    net = _net().eval()                        # dropout off: both paths deterministic
+    g = torch.Generator(device="cuda").manual_seed(B)
+    obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
+    vec = torch.randn(B, 8, 4, device="cuda", generator=g)
+    with torch.no_grad():
+        net.fused_acting = False
+        ref = net(obs, vec)
+        net.fused_acting = True
+        got = net(obs, vec)
+    names = ["policy", "value", "blocking", "policy_sig", "x", "logits", "cost_value"]
+    for name, r, o in zip(names, ref, got):
+        assert o.shape == r.shape, name
+        # fp16 autocast on both sides; the fused LayerNorm / epilogues round like torch's
+        # ops but reduce in a different order
+        torch.testing.assert_close(o.float(), r.float(), rtol=3e-2, atol=3e-2, msg=name)
+
+
+def test_training_forward_keeps_torch_ops():
+    net = _net()
+    obs = (torch.rand(4, 8, 6, 9, 9, device="cuda") < 0.25).float()
+    vec = torch.randn(4, 8, 4, device="cuda")
+    out = net(obs, vec)                        # grad enabled: the autograd path
+    out[1].sum().backward()
+    assert net.conv1.weight.grad is not None and torch.isfinite(net.conv1.weight.grad).all()
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def test_dropout_kernels_keep_rate_and_scale():
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n = 1 << 22
+    x = torch.zeros(n, device="cuda")
+    y = torch.ones(n, dtype=torch.float16, device="cuda")
+    _lib.check(lib.mapf_dropout_residual(_p(x), _p(y), n, 0.2, 1234, st))
+    kept = (x == 1.25).float().mean().item()
+    assert abs(kept - 0.8) < 3e-3 and bool(((x == 0) | (x == 1.25)).all())
+    # a different seed draws a different mask
+    x2 = torch.zeros(n, device="cuda")
+    _lib.check(lib.mapf_dropout_residual(_p(x2), _p(y), n, 0.2, 1235, st))
+    assert (x != x2).float().mean().item() > 0.2
+    # GELU + dropout: kept entries equal fp16(gelu(v) * 1.25)
+    v = torch.linspace(-4, 4, n, device="cuda").half()
+    h = v.clone()
+    _lib.check(lib.mapf_gelu_dropout_f16(_p(h), n, 0.2, 99, st))
+    ref = (torch.nn.functional.gelu(v.float()).half().float() * 1.25).half()
+    keep = h != 0
+    assert abs(keep.float().mean().item() - 0.8) < 5e-3
+    torch.testing.assert_close(h[keep], ref[keep], rtol=0, atol=2e-3)
+    # p = 0 is the identity
+    h0 = v.clone()
+    _lib.check(lib.mapf_gelu_dropout_f16(_p(h0), n, 0.0, 99, st))
+    torch.testing.assert_close(h0, torch.nn.functional.gelu(v.float()).half(), rtol=0, atol=2e-3)
+
+
+def test_layernorm_and_conv_epilogues_vs_torch():
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rows = 1000
+    x = torch.randn(rows, 512, device="cuda") * 3 + 1
+    ln = torch.nn.LayerNorm(512).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    y = torch.empty(rows, 512, dtype=torch.float16, device="cuda")
+    _lib.check(lib.mapf_layernorm_f16(_p(x), 512, _p(ln.weight), _p(ln.bias), _p(y), rows, 512, 1e-5, st))
+    torch.testing.assert_close(y.float(), ln(x).detach().half().float(), rtol=0, atol=4e-3)
+    # conv epilogue: NHWC [B, C, H, W] channels_last fp16
+    B, C, H, W = 7, 128, 9, 9
+    c = torch.randn(B, C, H, W, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    bias = torch.randn(C, device="cuda").half()
+    ref = torch.relu(c + bias.view(1, C, 1, 1))
+    pooled = torch.empty(B, C, H // 2, W // 2, dtype=torch.float16, device="cuda",
+                         memory_format=torch.channels_last)
+    _lib.check(lib.mapf_nhwc_bias_relu_pool2(_p(c), _p(bias), _p(pooled), B, H, W, C, st))
+    assert torch.equal(pooled, torch.nn.functional.max_pool2d(ref, 2))
+    _lib.check(lib.mapf_nhwc_bias_relu(_p(c), _p(bias), B * H * W, C, st))
+    assert torch.equal(c, ref)

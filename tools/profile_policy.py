@@ -19,7 +19,8 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--nchw", action="store_true", help="keep the network NCHW")
-    ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--no-find", action="store_true", help="torch.backends.cudnn.benchmark off (no MIOpen find)")
+    ap.add_argument("--torch-path", action="store_true", help="the PyTorch forward, not the fused acting path")
     args = ap.parse_args()
     from mapf_amd.model import Model
     dev = torch.device("cuda", 0)
@@ -29,7 +30,9 @@ def main():
     vec = torch.randn(B, N, 4, device=dev)
     if args.nchw:
         model.network = model.network.to(memory_format=torch.contiguous_format)
-    torch.backends.cudnn.benchmark = args.benchmark
+    if args.no_find:
+        torch.backends.cudnn.benchmark = False
+    model.network.fused_acting = not args.torch_path
     for _ in range(3):
         model.step(obs, vec, None)
     torch.cuda.synchronize()
