@@ -12,6 +12,7 @@
 //   dropout_residual        x(fp32) += dropout(y(fp16))      (PreNorm residual, do1/do2)
 //   gelu_dropout_f16        h = dropout(gelu(h))  in place   (MLP_Block af1 + do1)
 //   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
+//   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32
 // The training forward keeps PyTorch's ops (autograd needs them).
 //
 // Dropout: keep with probability 1 - p, kept values scaled by 1 / (1 - p) (torch's
@@ -202,6 +203,79 @@ __global__ __launch_bounds__(256) void tokens(float *__restrict__ x, const float
     }
 }
 
+// ---- attention over a short token axis (transformer.py:48-85; n <= 17 tokens) -----
+// softmax(q k^T * scale) v per head, fp16 in, fp32 accumulation and softmax, fp16
+// out -- the same arithmetic as the fused SDPA call it replaces, whose flash kernel
+// is built for long sequences (here n = 17, dh = 32).  One wave per (sequence,
+// half of the 512-wide model dim; n <= NMAX = 17): lane l owns dims 4l..4l+3 of its half, so one
+// head = 8 lanes; the wave's K and V rows live in registers (fp16 pairs), q rows
+// stream in, dot products as v_dot2_f32_f16 + a 3-step DPP reduction over the 8
+// lanes of the head.  Strides in fp16 elements: token (row) and sequence.
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+__device__ inline h2_t as_h2(uint32_t u) { return __builtin_bit_cast(h2_t, u); }
+template <int CTRL>
+__device__ inline float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void attention_f16(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
+                                                     const uint16_t *__restrict__ v, uint16_t *__restrict__ out,
+                                                     long B, int n, int q_rows, long q_ts, long q_bs, long kv_ts,
+                                                     long kv_bs, float scale) {
+    const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wave >= 2 * B) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const long b = wave >> 1;
+    const int d0 = (int)(wave & 1) * 256 + 4 * lane;          // first of this lane's 4 dims
+    uint2 kr[NMAX], vr[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j)
+        if (j < n) {
+            kr[j] = *reinterpret_cast<const uint2 *>(k + b * kv_bs + j * kv_ts + d0);
+            vr[j] = *reinterpret_cast<const uint2 *>(v + b * kv_bs + j * kv_ts + d0);
+        }
+    uint2 qr[NMAX];                                           // every query row in flight at once
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i)
+        if (i < q_rows) qr[i] = *reinterpret_cast<const uint2 *>(q + b * q_bs + i * q_ts + d0);
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i) {
+        if (i >= q_rows) break;
+        const uint2 qi = qr[i];
+        float s[NMAX];
+        float m = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (j < n) {
+                float d = __builtin_amdgcn_fdot2(as_h2(qi.x), as_h2(kr[j].x), 0.f, false);
+                d = __builtin_amdgcn_fdot2(as_h2(qi.y), as_h2(kr[j].y), d, false);
+                d += dpp_f<0xB1>(d);                         // quad_perm [1,0,3,2]: lane ^ 1
+                d += dpp_f<0x4E>(d);                         // quad_perm [2,3,0,1]: lane ^ 2
+                d += dpp_f<0x141>(d);                        // row_half_mirror: the other quad of 8
+                s[j] = d * scale;
+                m = fmaxf(m, s[j]);
+            }
+        }
+        float sum = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (j < n) {
+                const float p = __expf(s[j] - m);
+                sum += p;
+                const h2_t va = as_h2(vr[j].x), vb = as_h2(vr[j].y);
+                o0 += p * (float)va.x;
+                o1 += p * (float)va.y;
+                o2 += p * (float)vb.x;
+                o3 += p * (float)vb.y;
+            }
+        }
+        const float r = 1.f / sum;
+        *reinterpret_cast<uint2 *>(out + (b * q_rows + i) * 512 + d0) = pack4(f2h(o0 * r), f2h(o1 * r), f2h(o2 * r),
+                                                                              f2h(o3 * r));
+    }
+}
+
 inline int grid_for(long items, int per_block) {
     long g = (items + per_block - 1) / per_block;
     if (g > 16384) g = 16384;
@@ -268,6 +342,20 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
     const long n4 = (long)B * (L + 1) * (D / 4);
     hipLaunchKernelGGL(pol::tokens, dim3(pol::grid_for(n4, 256)), dim3(256), 0, (hipStream_t)stream, x, A, VV, cls,
                        pos, (long)B, (int)L, (int)D, pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *out, int64_t B, int32_t n,
+                       int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
+                       int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream) {
+    if (!q || !k || !v || !out || B < 0 || n < 1 || n > 17 || q_rows < 1 || q_rows > n || heads * head_dim != 512 ||
+        head_dim != 32 || ((q_token_stride | q_seq_stride | kv_token_stride | kv_seq_stride) & 3))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const unsigned grid = (unsigned)((2 * B + 3) / 4);
+    hipLaunchKernelGGL(pol::attention_f16<17>, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, k, v, out, (long)B,
+                       (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride, (long)kv_token_stride,
+                       (long)kv_seq_stride, scale);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

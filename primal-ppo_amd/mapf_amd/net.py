@@ -177,6 +177,7 @@ class SCRIMPNet(nn.Module):
         self.blocking_layer = nn.Linear(W, 1)
         self.apply(_xavier_like)
         self.fused_acting = True      # no-grad GPU forward through _forward_fused (csrc/mapf_policy.hip)
+        self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
 
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
@@ -298,21 +299,41 @@ class SCRIMPNet(nn.Module):
             y = y.contiguous()
             chk(lib.mapf_dropout_residual(ptr(x), ptr(y), x.numel(), drop(m), next(seeds), st))
 
+        def attend(q, k, v, rows, q_ts, kv_ts, a):     # fp16 [b, rows, d], heads concatenated
+            o = torch.empty(b, rows, d, dtype=torch.float16, device=x.device)
+            chk(lib.mapf_attention_f16(ptr(q), ptr(k), ptr(v), ptr(o), b, n, rows, q_ts, q_ts * (n if rows > 1 else 1),
+                                       kv_ts, kv_ts * n, a.heads, d // a.heads, float(a.scale), st))
+            return o
+
         for li, (att, ff) in enumerate(layers):
             a = att.fn.fn
             hh = a.heads
             y = ln(x, att.fn.norm)
+            own_attn = self.fused_attention and hh * 32 == d == 512 and n <= 17
             if li < len(layers) - 1:
-                qkv = a.to_qkv(y).view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
-                out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
-                residual(x, a.nn1(out.transpose(1, 2).reshape(b, n, d)), a.do1)
+                qkv = a.to_qkv(y)
+                if own_attn:
+                    assert qkv.dtype == torch.float16 and qkv.is_contiguous()
+                    out = attend(qkv, qkv[..., d:], qkv[..., 2 * d:], n, 3 * d, 3 * d, a)
+                else:
+                    qkv = qkv.view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
+                    out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
+                    out = out.transpose(1, 2).reshape(b, n, d)
+                residual(x, a.nn1(out), a.do1)
             else:                               # the last block: token 0's query only (see _Encoder)
                 w, bias = a.to_qkv.weight, a.to_qkv.bias
-                q = F.linear(y[:, 0], w[:d], bias[:d]).view(b, 1, hh, d // hh).transpose(1, 2)
-                kv = F.linear(y, w[d:], bias[d:]).view(b, n, 2, hh, d // hh).permute(2, 0, 3, 1, 4)
-                out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
+                q = F.linear(y[:, 0], w[:d], bias[:d])
+                kv = F.linear(y, w[d:], bias[d:])
+                if own_attn:
+                    assert q.dtype == kv.dtype == torch.float16 and q.is_contiguous() and kv.is_contiguous()
+                    out = attend(q, kv, kv[..., d:], 1, d, 2 * d, a)
+                else:
+                    q = q.view(b, 1, hh, d // hh).transpose(1, 2)
+                    kv = kv.view(b, n, 2, hh, d // hh).permute(2, 0, 3, 1, 4)
+                    out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
+                    out = out.transpose(1, 2).reshape(b, 1, d)
                 x = x[:, :1].contiguous()
-                residual(x, a.nn1(out.transpose(1, 2).reshape(b, 1, d)), a.do1)
+                residual(x, a.nn1(out), a.do1)
             f = ff.fn.fn
             hid = f.nn1(ln(x, ff.fn.norm)).contiguous()
             chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(f.do1), next(seeds), st))

@@ -23,9 +23,10 @@ def _net(n_agents=8):
     return Model(0, "cuda", numChannel=6, num_agents=n_agents, fov=9).network
 
 
-@pytest.mark.parametrize("B", [5, 256])
-def test_fused_acting_forward_matches_torch_path(B):
+@pytest.mark.parametrize("B,own_attn", [(5, True), (256, True), (256, False)])
+def test_fused_acting_forward_matches_torch_path(B, own_attn):
     net = _net().eval()                        # dropout off: both paths deterministic
+    net.fused_attention = own_attn
     g = torch.Generator(device="cuda").manual_seed(B)
     obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
     vec = torch.randn(B, 8, 4, device="cuda", generator=g)
@@ -107,3 +108,27 @@ def test_layernorm_and_conv_epilogues_vs_torch():
     assert torch.equal(pooled, torch.nn.functional.max_pool2d(ref, 2))
     _lib.check(lib.mapf_nhwc_bias_relu(_p(c), _p(bias), B * H * W, C, st))
     assert torch.equal(c, ref)
+
+
+@pytest.mark.parametrize("n,rows", [(17, 17), (17, 1), (5, 5), (1, 1)])
+def test_attention_kernel_vs_sdpa(n, rows):
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    B, d, hh = 300, 512, 16
+    g = torch.Generator(device="cuda").manual_seed(n * 100 + rows)
+    qkv = (torch.randn(B, n, 3 * d, device="cuda", generator=g) * 2).half()
+    scale = d ** -0.5
+    out = torch.empty(B, rows, d, dtype=torch.float16, device="cuda")
+    q = qkv[:, :rows, :d]
+    _lib.check(lib.mapf_attention_f16(_p(qkv), _p(qkv[..., d:]), _p(qkv[..., 2 * d:]), _p(out), B, n, rows,
+                                      3 * d, n * 3 * d, 3 * d, n * 3 * d, hh, d // hh, scale, st))
+    heads = lambda t: t.reshape(B, t.shape[1], hh, d // hh).transpose(1, 2).float()
+    ref = torch.nn.functional.scaled_dot_product_attention(heads(q), heads(qkv[..., d:2 * d]),
+                                                           heads(qkv[..., 2 * d:]), scale=scale)
+    ref = ref.transpose(1, 2).reshape(B, rows, d)
+    # fp32 math on fp16 inputs; the only rounding is the fp16 output
+    torch.testing.assert_close(out.float(), ref, rtol=2e-3, atol=2e-3)
+    # argument checks fail without launching
+    assert lib.mapf_attention_f16(_p(qkv), _p(qkv), _p(qkv), _p(out), B, 18, 1, 3 * d, 0, 3 * d, 0, hh, 32, scale,
+                                  st) != 0
