@@ -245,9 +245,10 @@ int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint6
 int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *stream);
 int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
                 int32_t D, float p, uint64_t seed, void *stream);
-/* out[B][q_rows][512] = softmax(q k^T * scale) v per head (16 heads x 32, n <= 17 tokens; fp16 in/out,
- * fp32 math) -- transformer.py:48-85's attention for the first q_rows queries.  Strides in fp16
- * elements between consecutive tokens / sequences of q and of k, v. */
+/* out[B][q_rows][512] = softmax(q k^T * scale) v per head (heads = 16, head_dim = 32, n <= 32 tokens;
+ * fp16 in/out, fp32 scores and softmax, P rounded to fp16 for P.V like flash SDPA) --
+ * transformer.py:48-85's attention for the first q_rows queries.  Strides in fp16 elements between
+ * consecutive tokens / sequences of q and of k, v (multiples of 8; q, k, v 16-B aligned). */
 int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *out, int64_t B, int32_t n,
                        int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                        int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream);

@@ -12,7 +12,7 @@
 //   dropout_residual        x(fp32) += dropout(y(fp16))      (PreNorm residual, do1/do2)
 //   gelu_dropout_f16        h = dropout(gelu(h))  in place   (MLP_Block af1 + do1)
 //   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
-//   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32
+//   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32 (MFMA)
 // The training forward keeps PyTorch's ops (autograd needs them).
 //
 // Dropout: keep with probability 1 - p, kept values scaled by 1 / (1 - p) (torch's
@@ -203,76 +203,114 @@ __global__ __launch_bounds__(256) void tokens(float *__restrict__ x, const float
     }
 }
 
-// ---- attention over a short token axis (transformer.py:48-85; n <= 17 tokens) -----
-// softmax(q k^T * scale) v per head, fp16 in, fp32 accumulation and softmax, fp16
-// out -- the same arithmetic as the fused SDPA call it replaces, whose flash kernel
-// is built for long sequences (here n = 17, dh = 32).  One wave per (sequence,
-// half of the 512-wide model dim; n <= NMAX = 17): lane l owns dims 4l..4l+3 of its half, so one
-// head = 8 lanes; the wave's K and V rows live in registers (fp16 pairs), q rows
-// stream in, dot products as v_dot2_f32_f16 + a 3-step DPP reduction over the 8
-// lanes of the head.  Strides in fp16 elements: token (row) and sequence.
-typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-__device__ inline h2_t as_h2(uint32_t u) { return __builtin_bit_cast(h2_t, u); }
-template <int CTRL>
-__device__ inline float dpp_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
+// ---- attention over a short token axis (transformer.py:48-85; n <= 32 tokens) -----
+// softmax(q k^T * scale) v per head (head_dim 32), fp16 in, fp32 scores / softmax,
+// P rounded to fp16 for the P.V product (as the flash SDPA kernel it replaces does),
+// fp16 out.  MFMA v_mfma_f32_16x16x32_f16, one contraction step = one head's 32 dims:
+//   S^T[key][query] = K Q^T   A = K rows (16-B loads), B = Q rows (16-B loads); keys and
+//                             queries padded to 2 tiles of 16 (n = 17: CLS + 16 cells)
+//   softmax over keys         the accumulator holds a query column on each lane, its keys
+//                             in registers + the 4 lanes l, l^16, l^32, l^48
+//   O^T[dh][query] = V^T P^T  the accumulator is the B operand as is (its k order is
+//                             (r>>2)*16 + 4*(l>>4) + (r&3)); V^T comes from an LDS image of
+//                             V read with ds_read_b64_tr_b16 in that same key order
+// One workgroup per sequence, 4 waves x 4 heads; all of a wave's loads issue up front.
+// Strides in fp16 elements: token (row) and sequence.
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-template <int NMAX>
+// V image of one head: 32 key rows x 64 B; 16-B chunk c of row r sits at chunk
+// c ^ 2*((r >> 2) & 1), so the transposed reads' rows r and r + 4 use different banks
+__device__ inline int vimg_off(int r, int c) { return r * 64 + ((c ^ (((r >> 2) & 1) << 1)) << 4); }
+
+__device__ inline uint4 ld16(const uint16_t *p, bool ok) {
+    return ok ? *reinterpret_cast<const uint4 *>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+__device__ inline h8_t as_h8(uint4 u) { return __builtin_bit_cast(h8_t, u); }
+
+template <int QT>
 __global__ __launch_bounds__(256) void attention_f16(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
                                                      const uint16_t *__restrict__ v, uint16_t *__restrict__ out,
-                                                     long B, int n, int q_rows, long q_ts, long q_bs, long kv_ts,
-                                                     long kv_bs, float scale) {
-    const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wave >= 2 * B) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const long b = wave >> 1;
-    const int d0 = (int)(wave & 1) * 256 + 4 * lane;          // first of this lane's 4 dims
-    uint2 kr[NMAX], vr[NMAX];
+                                                     int n, int q_rows, long q_ts, long q_bs, long kv_ts, long kv_bs,
+                                                     float scale_log2e) {
+    constexpr int HW = 4;                                     // heads per wave
+    __shared__ __attribute__((aligned(16))) uint8_t vimg[4][HW][2048];
+    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+    const int g = lane >> 4, i = lane & 15;
+    const long b = blockIdx.x;
+    const uint16_t *qb = q + b * q_bs, *kb = k + b * kv_bs, *vb = v + b * kv_bs;
+    uint4 kf[HW][2], vf[HW][2], qf[HW][QT];
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j)
-        if (j < n) {
-            kr[j] = *reinterpret_cast<const uint2 *>(k + b * kv_bs + j * kv_ts + d0);
-            vr[j] = *reinterpret_cast<const uint2 *>(v + b * kv_bs + j * kv_ts + d0);
+    for (int hh = 0; hh < HW; ++hh) {
+        const int col = (w * HW + hh) * 32 + 8 * g;           // this lane's 8 dims of the head
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int key = 16 * t + i;
+            kf[hh][t] = ld16(kb + key * kv_ts + col, key < n);
+            vf[hh][t] = ld16(vb + key * kv_ts + col, key < n);
         }
-    uint2 qr[NMAX];                                           // every query row in flight at once
 #pragma unroll
-    for (int i = 0; i < NMAX; ++i)
-        if (i < q_rows) qr[i] = *reinterpret_cast<const uint2 *>(q + b * q_bs + i * q_ts + d0);
+        for (int t = 0; t < QT; ++t) qf[hh][t] = ld16(qb + (16 * t + i) * q_ts + col, 16 * t + i < q_rows);
+    }
 #pragma unroll
-    for (int i = 0; i < NMAX; ++i) {
-        if (i >= q_rows) break;
-        const uint2 qi = qr[i];
-        float s[NMAX];
-        float m = -INFINITY;
+    for (int hh = 0; hh < HW; ++hh)
 #pragma unroll
-        for (int j = 0; j < NMAX; ++j) {
-            if (j < n) {
-                float d = __builtin_amdgcn_fdot2(as_h2(qi.x), as_h2(kr[j].x), 0.f, false);
-                d = __builtin_amdgcn_fdot2(as_h2(qi.y), as_h2(kr[j].y), d, false);
-                d += dpp_f<0xB1>(d);                         // quad_perm [1,0,3,2]: lane ^ 1
-                d += dpp_f<0x4E>(d);                         // quad_perm [2,3,0,1]: lane ^ 2
-                d += dpp_f<0x141>(d);                        // row_half_mirror: the other quad of 8
-                s[j] = d * scale;
-                m = fmaxf(m, s[j]);
+        for (int t = 0; t < 2; ++t) *reinterpret_cast<uint4 *>(&vimg[w][hh][vimg_off(16 * t + i, g)]) = vf[hh][t];
+    __syncthreads();
+#pragma unroll
+    for (int hh = 0; hh < HW; ++hh) {
+        const int h = w * HW + hh;
+        f4_t s[2][QT];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(kf[hh][kt]), as_h8(qf[hh][qt]),
+                                                                   f4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        h8_t pf[QT];
+        float inv[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            float x[8], m = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int key = (e >> 2) * 16 + 4 * g + (e & 3);
+                x[e] = key < n ? s[e >> 2][qt][e & 3] * scale_log2e : -INFINITY;
+                m = fmaxf(m, x[e]);
+            }
+            m = fmaxf(m, __shfl_xor(m, 16, 64));
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            float sum = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float pe = exp2f(x[e] - m);
+                sum += pe;
+                pf[qt][e] = (_Float16)pe;
+            }
+            sum += __shfl_xor(sum, 16, 64);
+            sum += __shfl_xor(sum, 32, 64);
+            inv[qt] = 1.f / sum;
+        }
+        const int rq = i >> 2, cp = i & 3;                    // this lane's address in its tr-read block
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const uint8_t *img = vimg[w][hh];
+            const int c = 2 * dt + (cp >> 1), hb = 8 * (cp & 1);
+            const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t *)(img + vimg_off(4 * g + rq, c) + hb));
+            const s4_t hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t *)(img + vimg_off(16 + 4 * g + rq, c) + hb));
+            const h8_t vt = __builtin_bit_cast(h8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const f4_t o = __builtin_amdgcn_mfma_f32_16x16x32_f16(vt, pf[qt], f4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const int qr = 16 * qt + i;
+                if (qr < q_rows)
+                    *reinterpret_cast<uint2 *>(out + (b * q_rows + qr) * 512 + h * 32 + 16 * dt + 4 * g) =
+                        pack4(f2h(o[0] * inv[qt]), f2h(o[1] * inv[qt]), f2h(o[2] * inv[qt]), f2h(o[3] * inv[qt]));
             }
         }
-        float sum = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-#pragma unroll
-        for (int j = 0; j < NMAX; ++j) {
-            if (j < n) {
-                const float p = __expf(s[j] - m);
-                sum += p;
-                const h2_t va = as_h2(vr[j].x), vb = as_h2(vr[j].y);
-                o0 += p * (float)va.x;
-                o1 += p * (float)va.y;
-                o2 += p * (float)vb.x;
-                o3 += p * (float)vb.y;
-            }
-        }
-        const float r = 1.f / sum;
-        *reinterpret_cast<uint2 *>(out + (b * q_rows + i) * 512 + d0) = pack4(f2h(o0 * r), f2h(o1 * r), f2h(o2 * r),
-                                                                              f2h(o3 * r));
     }
 }
 
@@ -348,14 +386,21 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
 int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *out, int64_t B, int32_t n,
                        int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                        int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream) {
-    if (!q || !k || !v || !out || B < 0 || n < 1 || n > 17 || q_rows < 1 || q_rows > n || heads * head_dim != 512 ||
-        head_dim != 32 || ((q_token_stride | q_seq_stride | kv_token_stride | kv_seq_stride) & 3))
+    // 16-B operand loads: 8-element aligned strides and 16-B aligned bases
+    if (!q || !k || !v || !out || B < 0 || n < 1 || n > 32 || q_rows < 1 || q_rows > n || heads != 16 ||
+        head_dim != 32 || ((q_token_stride | q_seq_stride | kv_token_stride | kv_seq_stride) & 7) ||
+        (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) || ((uintptr_t)out & 7))
         return MAPF_EINVAL;
     if (B == 0) return MAPF_OK;
-    const unsigned grid = (unsigned)((2 * B + 3) / 4);
-    hipLaunchKernelGGL(pol::attention_f16<17>, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, k, v, out, (long)B,
-                       (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride, (long)kv_token_stride,
-                       (long)kv_seq_stride, scale);
+    const float sl2e = scale * 1.4426950408889634f;
+    if (q_rows <= 16)
+        hipLaunchKernelGGL(pol::attention_f16<1>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, q, k, v, out,
+                           (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride, (long)kv_token_stride,
+                           (long)kv_seq_stride, sl2e);
+    else
+        hipLaunchKernelGGL(pol::attention_f16<2>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, q, k, v, out,
+                           (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride, (long)kv_token_stride,
+                           (long)kv_seq_stride, sl2e);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
