@@ -242,6 +242,10 @@ int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t 
 int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
                        int64_t rows, int32_t dim, float eps, void *stream);
 int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint64_t seed, void *stream);
+/* mapf_dropout_residual on rows x 512 contiguous x, y, then z = LayerNorm(x) as fp16 (like
+ * mapf_layernorm_f16) in one pass; bit-identical to the two calls with the same seed. */
+int mapf_dropout_residual_layernorm(float *x, const uint16_t *y, const float *gamma, const float *beta, uint16_t *z,
+                                    int64_t rows, int32_t dim, float eps, float p, uint64_t seed, void *stream);
 int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *stream);
 int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
                 int32_t D, float p, uint64_t seed, void *stream);

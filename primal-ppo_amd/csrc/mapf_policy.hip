@@ -10,6 +10,7 @@
 //   layernorm_f16           LayerNorm of the fp32 residual stream, written as the fp16
 //                           the next autocast linear would cast it to
 //   dropout_residual        x(fp32) += dropout(y(fp16))      (PreNorm residual, do1/do2)
+//   dropout_residual_layernorm   the residual above + the next PreNorm's LayerNorm, one pass
 //   gelu_dropout_f16        h = dropout(gelu(h))  in place   (MLP_Block af1 + do1)
 //   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
 //   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32 (MFMA)
@@ -103,15 +104,10 @@ __device__ inline float wave_sum(float v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x, long xstride,
-                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
-                                                     uint16_t *__restrict__ y, long rows, float eps) {
+// LayerNorm of one 512-wide row held by a wave as a = elements 4l..4l+3, c = 256+4l..
+__device__ inline void ln_row(float4 a, float4 c, int lane, const float *__restrict__ gamma,
+                              const float *__restrict__ beta, float eps, uint16_t *__restrict__ y) {
     constexpr int D = 512;
-    const int lane = (int)(threadIdx.x & 63);
-    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    const float4 *xr = reinterpret_cast<const float4 *>(x + row * xstride);
-    const float4 a = xr[lane], c = xr[64 + lane];                 // elements 4l..4l+3 and 256+4l..
     const float mean = wave_sum(a.x + a.y + a.z + a.w + c.x + c.y + c.z + c.w) * (1.f / D);
     const float d[8] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean, c.x - mean, c.y - mean, c.z - mean, c.w - mean};
     float ss = 0.f;
@@ -125,26 +121,60 @@ __global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x
     uint32_t o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = f2h(d[k] * rstd * g[k] + e[k]);
-    uint2 *yr = reinterpret_cast<uint2 *>(y + row * D);
+    uint2 *yr = reinterpret_cast<uint2 *>(y);
     yr[lane] = pack4(o[0], o[1], o[2], o[3]);
     yr[64 + lane] = pack4(o[4], o[5], o[6], o[7]);
 }
 
+__global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x, long xstride,
+                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                     uint16_t *__restrict__ y, long rows, float eps) {
+    const int lane = (int)(threadIdx.x & 63);
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4 *xr = reinterpret_cast<const float4 *>(x + row * xstride);
+    ln_row(xr[lane], xr[64 + lane], lane, gamma, beta, eps, y + row * 512);
+}
+
 // ---- dropout epilogues -----------------------------------------------------------
+__device__ inline float4 add_dropped(float4 a, uint2 v, unsigned k, float scale) {
+    a.x += (k & 1u) ? h2f(f2h(h2f(v.x) * scale)) : 0.f;
+    a.y += (k & 2u) ? h2f(f2h(h2f(v.x >> 16) * scale)) : 0.f;
+    a.z += (k & 4u) ? h2f(f2h(h2f(v.y) * scale)) : 0.f;
+    a.w += (k & 8u) ? h2f(f2h(h2f(v.y >> 16) * scale)) : 0.f;
+    return a;
+}
+
 // x[i] += dropout(y[i]); torch: dropout on the fp16 tensor (y * scale rounded to fp16),
 // then fp16 + fp32 -> fp32
 __global__ __launch_bounds__(256) void dropout_residual(float *__restrict__ x, const uint16_t *__restrict__ y, long n4,
                                                         uint32_t thr, float scale, uint64_t seed) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
         const unsigned k = thr ? keep4(seed, (uint64_t)i, thr) : 15u;
-        const uint2 v = reinterpret_cast<const uint2 *>(y)[i];
-        float4 a = reinterpret_cast<float4 *>(x)[i];
-        a.x += (k & 1u) ? h2f(f2h(h2f(v.x) * scale)) : 0.f;
-        a.y += (k & 2u) ? h2f(f2h(h2f(v.x >> 16) * scale)) : 0.f;
-        a.z += (k & 4u) ? h2f(f2h(h2f(v.y) * scale)) : 0.f;
-        a.w += (k & 8u) ? h2f(f2h(h2f(v.y >> 16) * scale)) : 0.f;
-        reinterpret_cast<float4 *>(x)[i] = a;
+        reinterpret_cast<float4 *>(x)[i] =
+            add_dropped(reinterpret_cast<float4 *>(x)[i], reinterpret_cast<const uint2 *>(y)[i], k, scale);
     }
+}
+
+// x += dropout(y); z = LayerNorm(x) -> fp16: dropout_residual then layernorm_f16 in one
+// pass over the residual stream (same mask bits, same arithmetic -- bit-identical to the
+// two launches), one wave per 512-wide row of contiguous x, y
+__global__ __launch_bounds__(256) void dropout_residual_layernorm(float *__restrict__ x, const uint16_t *__restrict__ y,
+                                                                  const float *__restrict__ gamma,
+                                                                  const float *__restrict__ beta,
+                                                                  uint16_t *__restrict__ z, long rows, uint32_t thr,
+                                                                  float scale, float eps, uint64_t seed) {
+    const int lane = (int)(threadIdx.x & 63);
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const long i0 = row * 128 + lane, i1 = i0 + 64;          // float4 indices, as dropout_residual's
+    float4 *xr = reinterpret_cast<float4 *>(x);
+    const uint2 *yr = reinterpret_cast<const uint2 *>(y);
+    const float4 a = add_dropped(xr[i0], yr[i0], thr ? keep4(seed, (uint64_t)i0, thr) : 15u, scale);
+    const float4 c = add_dropped(xr[i1], yr[i1], thr ? keep4(seed, (uint64_t)i1, thr) : 15u, scale);
+    xr[i0] = a;
+    xr[i1] = c;
+    ln_row(a, c, lane, gamma, beta, eps, z + row * 512);
 }
 
 // h = dropout(gelu(h)) in place: exact (erf) GELU in fp32 rounded to fp16 like torch's
@@ -361,6 +391,16 @@ int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint6
     if (n == 0) return MAPF_OK;
     hipLaunchKernelGGL(pol::dropout_residual, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, x, y,
                        (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_dropout_residual_layernorm(float *x, const uint16_t *y, const float *gamma, const float *beta, uint16_t *z,
+                                    int64_t rows, int32_t dim, float eps, float p, uint64_t seed, void *stream) {
+    if (!x || !y || !gamma || !beta || !z || rows < 0 || dim != 512 || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::dropout_residual_layernorm, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, x, y, gamma, beta, z, (long)rows, pol::drop_threshold(p), 1.f / (1.f - p),
+                       eps, seed);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

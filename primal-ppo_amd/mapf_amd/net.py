@@ -178,6 +178,7 @@ class SCRIMPNet(nn.Module):
         self.apply(_xavier_like)
         self.fused_acting = True      # no-grad GPU forward through _forward_fused (csrc/mapf_policy.hip)
         self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
+        self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
 
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
@@ -295,9 +296,15 @@ class SCRIMPNet(nn.Module):
                                        float(norm.eps), st))
             return y
 
-        def residual(x, y, m):                  # x += dropout(y)
+        def residual(x, y, m, norm=None):       # x += dropout(y); then LayerNorm(x) -> fp16 if norm
             y = y.contiguous()
-            chk(lib.mapf_dropout_residual(ptr(x), ptr(y), x.numel(), drop(m), next(seeds), st))
+            if norm is None or not self.fused_residual_ln:
+                chk(lib.mapf_dropout_residual(ptr(x), ptr(y), x.numel(), drop(m), next(seeds), st))
+                return None if norm is None else ln(x, norm)
+            z = torch.empty(x.shape, dtype=torch.float16, device=x.device)
+            chk(lib.mapf_dropout_residual_layernorm(ptr(x), ptr(y), ptr(norm.weight), ptr(norm.bias), ptr(z),
+                                                    x.numel() // d, d, float(norm.eps), drop(m), next(seeds), st))
+            return z
 
         def attend(q, k, v, rows, q_ts, kv_ts, a):     # fp16 [b, rows, d], heads concatenated
             o = torch.empty(b, rows, d, dtype=torch.float16, device=x.device)
@@ -305,10 +312,11 @@ class SCRIMPNet(nn.Module):
                                        kv_ts, kv_ts * n, a.heads, d // a.heads, float(a.scale), st))
             return o
 
+        y = ln(x, layers[0][0].fn.norm)
         for li, (att, ff) in enumerate(layers):
             a = att.fn.fn
             hh = a.heads
-            y = ln(x, att.fn.norm)
+            f = ff.fn.fn
             own_attn = self.fused_attention and hh * 32 == d == 512 and n <= 17
             if li < len(layers) - 1:
                 qkv = a.to_qkv(y)
@@ -319,7 +327,7 @@ class SCRIMPNet(nn.Module):
                     qkv = qkv.view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
                     out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, n, d)
-                residual(x, a.nn1(out), a.do1)
+                yf = residual(x, a.nn1(out), a.do1, ff.fn.norm)
             else:                               # the last block: token 0's query only (see _Encoder)
                 w, bias = a.to_qkv.weight, a.to_qkv.bias
                 q = F.linear(y[:, 0], w[:d], bias[:d])
@@ -333,9 +341,8 @@ class SCRIMPNet(nn.Module):
                     out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, 1, d)
                 x = x[:, :1].contiguous()
-                residual(x, a.nn1(out), a.do1)
-            f = ff.fn.fn
-            hid = f.nn1(ln(x, ff.fn.norm)).contiguous()
+                yf = residual(x, a.nn1(out), a.do1, ff.fn.norm)
+            hid = f.nn1(yf).contiguous()
             chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(f.do1), next(seeds), st))
-            residual(x, f.nn2(hid), f.do2)
+            y = residual(x, f.nn2(hid), f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
         return x

@@ -23,10 +23,11 @@ def _net(n_agents=8):
     return Model(0, "cuda", numChannel=6, num_agents=n_agents, fov=9).network
 
 
-@pytest.mark.parametrize("B,own_attn", [(5, True), (256, True), (256, False)])
-def test_fused_acting_forward_matches_torch_path(B, own_attn):
+@pytest.mark.parametrize("B,own_attn,res_ln", [(5, True, True), (256, True, True), (256, False, False)])
+def test_fused_acting_forward_matches_torch_path(B, own_attn, res_ln):
     net = _net().eval()                        # dropout off: both paths deterministic
     net.fused_attention = own_attn
+    net.fused_residual_ln = res_ln
     g = torch.Generator(device="cuda").manual_seed(B)
     obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
     vec = torch.randn(B, 8, 4, device="cuda", generator=g)
@@ -135,3 +136,23 @@ def test_attention_kernel_vs_sdpa(n, rows):
                                   st) != 0
     assert lib.mapf_attention_f16(_p(qkv), _p(qkv), _p(qkv), _p(out), B, n, 1, 3 * d + 4, 0, 3 * d, 0, hh, 32,
                                   scale, st) != 0
+
+
+def test_residual_layernorm_equals_two_launches():
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rows = 777
+    x = torch.randn(rows, 512, device="cuda") * 2
+    y = torch.randn(rows, 512, device="cuda").half()
+    g = torch.rand(512, device="cuda") + 0.5
+    e = torch.randn(512, device="cuda")
+    x1, x2 = x.clone(), x.clone()
+    z1 = torch.empty(rows, 512, dtype=torch.float16, device="cuda")
+    z2 = torch.empty_like(z1)
+    for p in (0.0, 0.2):
+        _lib.check(lib.mapf_dropout_residual(_p(x1), _p(y), x1.numel(), p, 77, st))
+        _lib.check(lib.mapf_layernorm_f16(_p(x1), 512, _p(g), _p(e), _p(z1), rows, 512, 1e-5, st))
+        _lib.check(lib.mapf_dropout_residual_layernorm(_p(x2), _p(y), _p(g), _p(e), _p(z2), rows, 512, 1e-5, p, 77,
+                                                       st))
+        assert torch.equal(x1, x2) and torch.equal(z1, z2)
