@@ -249,6 +249,11 @@ int mapf_dropout_residual_layernorm(float *x, const uint16_t *y, const float *ga
 int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *stream);
 int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
                 int32_t D, float p, uint64_t seed, void *stream);
+/* mapf_tokens (D = 512) and z = LayerNorm(x) as fp16 (gamma, beta, eps) in one pass; bit-identical
+ * to mapf_tokens then mapf_layernorm_f16. */
+int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
+                          int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
+                          float eps, uint16_t *z, void *stream);
 /* out[B][q_rows][512] = softmax(q k^T * scale) v per head (heads = 16, head_dim = 32, n <= 32 tokens;
  * fp16 in/out, fp32 scores and softmax, P rounded to fp16 for P.V like flash SDPA) --
  * transformer.py:48-85's attention for the first q_rows queries.  Strides in fp16 elements between

@@ -13,6 +13,7 @@
 //   dropout_residual_layernorm   the residual above + the next PreNorm's LayerNorm, one pass
 //   gelu_dropout_f16        h = dropout(gelu(h))  in place   (MLP_Block af1 + do1)
 //   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
+//   tokens_layernorm        tokens + the first block's LayerNorm, one pass
 //   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32 (MFMA)
 // The training forward keeps PyTorch's ops (autograd needs them).
 //
@@ -200,6 +201,29 @@ __global__ __launch_bounds__(256) void gelu_dropout_f16(uint16_t *__restrict__ h
 // x[b][0][:] = cls + pos[0];  x[b][1+t][:] = A[b][t] * VV[b][:] + pos[1+t];  then dropout
 // (all fp32: softmax output A is fp32 under autocast, the fp16 VV promotes).
 // A fp32 [B][L], VV fp16 [B][D], cls fp32 [D], pos fp32 [L+1][D]; D % 4 == 0.
+__device__ inline float4 token4(const float *__restrict__ A, const uint16_t *__restrict__ VV,
+                                const float *__restrict__ cls, const float *__restrict__ pos, long b, int t, int d4,
+                                int L, int D, long i, uint32_t thr, float scale, uint64_t seed) {
+    const float4 pp = reinterpret_cast<const float4 *>(pos + (long)t * D)[d4];
+    float4 v;
+    if (t == 0) {
+        const float4 c = reinterpret_cast<const float4 *>(cls)[d4];
+        v = make_float4(c.x + pp.x, c.y + pp.y, c.z + pp.z, c.w + pp.w);
+    } else {
+        const float a = A[b * L + t - 1];
+        const uint2 w = reinterpret_cast<const uint2 *>(VV + b * D)[d4];
+        v = make_float4(a * h2f(w.x) + pp.x, a * h2f(w.x >> 16) + pp.y, a * h2f(w.y) + pp.z, a * h2f(w.y >> 16) + pp.w);
+    }
+    if (thr) {
+        const unsigned k = keep4(seed, (uint64_t)i, thr);
+        v.x = (k & 1u) ? v.x * scale : 0.f;
+        v.y = (k & 2u) ? v.y * scale : 0.f;
+        v.z = (k & 4u) ? v.z * scale : 0.f;
+        v.w = (k & 8u) ? v.w * scale : 0.f;
+    }
+    return v;
+}
+
 __global__ __launch_bounds__(256) void tokens(float *__restrict__ x, const float *__restrict__ A,
                                               const uint16_t *__restrict__ VV, const float *__restrict__ cls,
                                               const float *__restrict__ pos, long B, int L, int D, uint32_t thr,
@@ -210,27 +234,30 @@ __global__ __launch_bounds__(256) void tokens(float *__restrict__ x, const float
         const long row = i / d4n;
         const int d4 = (int)(i - row * d4n);
         const long b = row / (L + 1);
-        const int t = (int)(row - b * (L + 1));
-        const float4 pp = reinterpret_cast<const float4 *>(pos + (long)t * D)[d4];
-        float4 v;
-        if (t == 0) {
-            const float4 c = reinterpret_cast<const float4 *>(cls)[d4];
-            v = make_float4(c.x + pp.x, c.y + pp.y, c.z + pp.z, c.w + pp.w);
-        } else {
-            const float a = A[b * L + t - 1];
-            const uint2 w = reinterpret_cast<const uint2 *>(VV + b * D)[d4];
-            v = make_float4(a * h2f(w.x) + pp.x, a * h2f(w.x >> 16) + pp.y, a * h2f(w.y) + pp.z,
-                            a * h2f(w.y >> 16) + pp.w);
-        }
-        if (thr) {
-            const unsigned k = keep4(seed, (uint64_t)i, thr);
-            v.x = (k & 1u) ? v.x * scale : 0.f;
-            v.y = (k & 2u) ? v.y * scale : 0.f;
-            v.z = (k & 4u) ? v.z * scale : 0.f;
-            v.w = (k & 8u) ? v.w * scale : 0.f;
-        }
-        reinterpret_cast<float4 *>(x)[i] = v;
+        reinterpret_cast<float4 *>(x)[i] =
+            token4(A, VV, cls, pos, b, (int)(row - b * (L + 1)), d4, L, D, i, thr, scale, seed);
     }
+}
+
+// tokens + the first PreNorm's LayerNorm (z fp16) in one pass, one wave per 512-wide
+// row; bit-identical to tokens followed by layernorm_f16
+__global__ __launch_bounds__(256) void tokens_layernorm(float *__restrict__ x, const float *__restrict__ A,
+                                                        const uint16_t *__restrict__ VV, const float *__restrict__ cls,
+                                                        const float *__restrict__ pos, long B, int L, uint32_t thr,
+                                                        float scale, uint64_t seed, const float *__restrict__ gamma,
+                                                        const float *__restrict__ beta, float eps,
+                                                        uint16_t *__restrict__ z) {
+    const int lane = (int)(threadIdx.x & 63);
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= B * (L + 1)) return;
+    const long b = row / (L + 1);
+    const int t = (int)(row - b * (L + 1));
+    const float4 a = token4(A, VV, cls, pos, b, t, lane, L, 512, row * 128 + lane, thr, scale, seed);
+    const float4 c = token4(A, VV, cls, pos, b, t, 64 + lane, L, 512, row * 128 + 64 + lane, thr, scale, seed);
+    float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
+    xr[lane] = a;
+    xr[64 + lane] = c;
+    ln_row(a, c, lane, gamma, beta, eps, z + row * 512);
 }
 
 // ---- attention over a short token axis (transformer.py:48-85; n <= 32 tokens) -----
@@ -420,6 +447,20 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
     const long n4 = (long)B * (L + 1) * (D / 4);
     hipLaunchKernelGGL(pol::tokens, dim3(pol::grid_for(n4, 256)), dim3(256), 0, (hipStream_t)stream, x, A, VV, cls,
                        pos, (long)B, (int)L, (int)D, pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
+                          int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
+                          float eps, uint16_t *z, void *stream) {
+    if (!x || !A || !VV || !cls || !pos || !gamma || !beta || !z || B < 0 || L < 1 || D != 512 ||
+        !(p >= 0.f && p < 1.f))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const long rows = (long)B * (L + 1);
+    hipLaunchKernelGGL(pol::tokens_layernorm, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, A,
+                       VV, cls, pos, (long)B, (int)L, pol::drop_threshold(p), 1.f / (1.f - p), seed, gamma, beta, eps,
+                       z);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

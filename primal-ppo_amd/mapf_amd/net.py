@@ -271,9 +271,17 @@ class SCRIMPNet(nn.Module):
             VV = torch.matmul(hf, self.token_wV.sum(0)).contiguous()           # [b, 512] fp16
             xt = torch.empty(b, self.L + 1, self.cT, dtype=torch.float32, device=dev)
             cls, pos = self.cls_token.detach().contiguous(), self.pos_embedding.detach().contiguous()
-            chk(lib.mapf_tokens(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
-                                drop(self.dropout), next(seeds), st))
-            x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop)[:, 0]
+            y0 = None
+            if self.fused_residual_ln:                     # tokens + the first LayerNorm in one pass
+                norm = self.transformer.layers[0][0].fn.norm
+                y0 = torch.empty(xt.shape, dtype=torch.float16, device=dev)
+                chk(lib.mapf_tokens_layernorm(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
+                                              drop(self.dropout), next(seeds), ptr(norm.weight), ptr(norm.bias),
+                                              float(norm.eps), ptr(y0), st))
+            else:
+                chk(lib.mapf_tokens(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
+                                    drop(self.dropout), next(seeds), st))
+            x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop, y0)[:, 0]
             x = self.nn_same(self.nn_same(x))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)
@@ -284,9 +292,10 @@ class SCRIMPNet(nn.Module):
             blocking = torch.sigmoid(self.blocking_layer(x))
         return policy, value, blocking, policy_sig, x, logits, cost_value
 
-    def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop):
+    def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop, y0=None):
         """self.transformer(x, first_only=True) on the fused epilogues; x fp32 [b, n, d] is
-        updated in place (the residual stream) and token 0 after the last block returned."""
+        updated in place (the residual stream) and token 0 after the last block returned; y0 is
+        the first block's LayerNorm of x when the caller already computed it."""
         layers = self.transformer.layers
         b, n, d = x.shape
 
@@ -312,7 +321,7 @@ class SCRIMPNet(nn.Module):
                                        kv_ts, kv_ts * n, a.heads, d // a.heads, float(a.scale), st))
             return o
 
-        y = ln(x, layers[0][0].fn.norm)
+        y = ln(x, layers[0][0].fn.norm) if y0 is None else y0
         for li, (att, ff) in enumerate(layers):
             a = att.fn.fn
             hh = a.heads

@@ -156,3 +156,27 @@ def test_residual_layernorm_equals_two_launches():
         _lib.check(lib.mapf_dropout_residual_layernorm(_p(x2), _p(y), _p(g), _p(e), _p(z2), rows, 512, 1e-5, p, 77,
                                                        st))
         assert torch.equal(x1, x2) and torch.equal(z1, z2)
+
+
+def test_tokens_layernorm_equals_two_launches():
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    B, L, D = 333, 16, 512
+    A = torch.rand(B, L, device="cuda")
+    VV = torch.randn(B, D, device="cuda").half()
+    cls, pos = torch.randn(D, device="cuda"), torch.randn(L + 1, D, device="cuda")
+    g, e = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda")
+    for p in (0.0, 0.1):
+        x1 = torch.empty(B, L + 1, D, device="cuda")
+        x2 = torch.empty_like(x1)
+        z1 = torch.empty(B, L + 1, D, dtype=torch.float16, device="cuda")
+        z2 = torch.empty_like(z1)
+        _lib.check(lib.mapf_tokens(_p(x1), _p(A), _p(VV), _p(cls), _p(pos), B, L, D, p, 5, st))
+        _lib.check(lib.mapf_layernorm_f16(_p(x1), D, _p(g), _p(e), _p(z1), B * (L + 1), D, 1e-5, st))
+        _lib.check(lib.mapf_tokens_layernorm(_p(x2), _p(A), _p(VV), _p(cls), _p(pos), B, L, D, p, 5, _p(g), _p(e),
+                                             1e-5, _p(z2), st))
+        assert torch.equal(x1, x2) and torch.equal(z1, z2)
+        if p == 0:                             # the token formula itself (net.py:124-131)
+            ref = torch.cat([cls.expand(B, 1, D), A[..., None] * VV.float()[:, None]], 1) + pos
+            torch.testing.assert_close(x1, ref, rtol=1e-6, atol=1e-6)
