@@ -179,6 +179,7 @@ class SCRIMPNet(nn.Module):
         self.fused_acting = True      # no-grad GPU forward through _forward_fused (csrc/mapf_policy.hip)
         self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
         self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
+        self._h16 = {}                 # fp16 weights of the acting forward (_half)
 
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
@@ -239,6 +240,7 @@ class SCRIMPNet(nn.Module):
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())
         seeds = iter(torch.randint(0, 2 ** 62, (16,), dtype=torch.int64).tolist())
         drop = lambda m: float(m.p) if m.training else 0.0
+        h16, lin = self._half, self._lin16
         with torch.autocast(device_type="cuda"):
             n_agents = self.num_agents or EnvParameters.N_AGENTS
             F_ = self.fov or obs.shape[-1]
@@ -246,8 +248,8 @@ class SCRIMPNet(nn.Module):
             v = vector.reshape(-1, NetParameters.VECTOR_LEN)
 
             def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
-                y = F.conv2d(x, m.weight, None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
-                b = m.bias.to(torch.float16)
+                y = F.conv2d(x, h16(m.weight), None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
+                b = h16(m.bias)
                 B_, C_, H_, W_ = y.shape
                 if pool:
                     out = torch.empty((B_, C_, H_ // 2, W_ // 2), dtype=y.dtype, device=dev,
@@ -260,15 +262,15 @@ class SCRIMPNet(nn.Module):
             x = conv(conv(conv(x, self.conv1), self.conv1a), self.conv1b, pool=True)
             x = conv(conv(conv(x, self.conv2), self.conv2a), self.conv2b, pool=True)
             x = conv(x, self.conv3).flatten(1)
-            g = F.relu(self.fully_connected_1(v))
+            g = F.relu(lin(self.fully_connected_1, v))
             x3 = torch.cat((x, g), -1)
-            h = self.fully_connected_3(F.relu(self.fully_connected_2(x3)))
+            h = lin(self.fully_connected_3, F.relu(lin(self.fully_connected_2, x3)))
             h = F.relu(h + x3).unsqueeze(1)                                   # [b, 1, 512]
             b = h.shape[0]
             hf = h.reshape(b, self.cT)                                        # 2-D GEMMs, not [b,1,512] bmm
-            A = torch.matmul(hf, self.token_wA.sum(0).transpose(0, 1)).unsqueeze(-1).softmax(dim=-1)
+            A = torch.matmul(hf, h16(self.token_wA, "sumT")).unsqueeze(-1).softmax(dim=-1)
             A = A.reshape(b, self.L).float().contiguous()                     # [b, 16] (all ones: length-1 softmax)
-            VV = torch.matmul(hf, self.token_wV.sum(0)).contiguous()           # [b, 512] fp16
+            VV = torch.matmul(hf, h16(self.token_wV, "sum")).contiguous()      # [b, 512] fp16
             xt = torch.empty(b, self.L + 1, self.cT, dtype=torch.float32, device=dev)
             cls, pos = self.cls_token.detach().contiguous(), self.pos_embedding.detach().contiguous()
             y0 = None
@@ -282,7 +284,7 @@ class SCRIMPNet(nn.Module):
                 chk(lib.mapf_tokens(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
                                     drop(self.dropout), next(seeds), st))
             x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop, y0)[:, 0]
-            x = self.nn_same(self.nn_same(x))
+            x = lin(self.nn_same, lin(self.nn_same, x))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)
             policy = logits.softmax(dim=-1)
@@ -292,12 +294,32 @@ class SCRIMPNet(nn.Module):
             blocking = torch.sigmoid(self.blocking_layer(x))
         return policy, value, blocking, policy_sig, x, logits, cost_value
 
+    _HALF_VIEWS = {"sumT": lambda t: t.sum(0).transpose(0, 1), "sum": lambda t: t.sum(0),
+                   "q": lambda t: t[:t.shape[0] // 3], "kv": lambda t: t[t.shape[0] // 3:]}
+
+    def _half(self, t, view=None):
+        """fp16 copy of parameter t (or of a fixed view of it) for the acting forward, kept
+        until t changes in place (optimizer step, load_state_dict bump its version) --
+        autocast would re-cast every weight on every forward."""
+        key = (id(t), view)
+        ver = (t._version, t.data_ptr())
+        hit = self._h16.get(key)
+        if hit is None or hit[0] != ver:
+            src = self._HALF_VIEWS[view](t) if view else t
+            hit = (ver, src.detach().to(torch.float16).contiguous())
+            self._h16[key] = hit
+        return hit[1]
+
+    def _lin16(self, m, x):
+        return F.linear(x, self._half(m.weight), None if m.bias is None else self._half(m.bias))
+
     def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop, y0=None):
         """self.transformer(x, first_only=True) on the fused epilogues; x fp32 [b, n, d] is
         updated in place (the residual stream) and token 0 after the last block returned; y0 is
         the first block's LayerNorm of x when the caller already computed it."""
         layers = self.transformer.layers
         b, n, d = x.shape
+        h16, lin = self._half, self._lin16
 
         def ln(x, norm):                        # LayerNorm -> the fp16 the next linear reads
             y = torch.empty(x.shape, dtype=torch.float16, device=x.device)
@@ -328,7 +350,7 @@ class SCRIMPNet(nn.Module):
             f = ff.fn.fn
             own_attn = self.fused_attention and hh * 32 == d == 512 and n <= 17
             if li < len(layers) - 1:
-                qkv = a.to_qkv(y)
+                qkv = lin(a.to_qkv, y)
                 if own_attn:
                     assert qkv.dtype == torch.float16 and qkv.is_contiguous()
                     out = attend(qkv, qkv[..., d:], qkv[..., 2 * d:], n, 3 * d, 3 * d, a)
@@ -336,11 +358,11 @@ class SCRIMPNet(nn.Module):
                     qkv = qkv.view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
                     out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, n, d)
-                yf = residual(x, a.nn1(out), a.do1, ff.fn.norm)
+                yf = residual(x, lin(a.nn1, out), a.do1, ff.fn.norm)
             else:                               # the last block: token 0's query only (see _Encoder)
                 w, bias = a.to_qkv.weight, a.to_qkv.bias
-                q = F.linear(y[:, 0], w[:d], bias[:d])
-                kv = F.linear(y, w[d:], bias[d:])
+                q = F.linear(y[:, 0], h16(w, "q"), h16(bias, "q"))
+                kv = F.linear(y, h16(w, "kv"), h16(bias, "kv"))
                 if own_attn:
                     assert q.dtype == kv.dtype == torch.float16 and q.is_contiguous() and kv.is_contiguous()
                     out = attend(q, kv, kv[..., d:], 1, d, 2 * d, a)
@@ -350,8 +372,8 @@ class SCRIMPNet(nn.Module):
                     out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, 1, d)
                 x = x[:, :1].contiguous()
-                yf = residual(x, a.nn1(out), a.do1, ff.fn.norm)
-            hid = f.nn1(yf).contiguous()
+                yf = residual(x, lin(a.nn1, out), a.do1, ff.fn.norm)
+            hid = lin(f.nn1, yf).contiguous()
             chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(f.do1), next(seeds), st))
-            y = residual(x, f.nn2(hid), f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
+            y = residual(x, lin(f.nn2, hid), f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
         return x

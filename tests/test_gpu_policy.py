@@ -180,3 +180,19 @@ def test_tokens_layernorm_equals_two_launches():
         if p == 0:                             # the token formula itself (net.py:124-131)
             ref = torch.cat([cls.expand(B, 1, D), A[..., None] * VV.float()[:, None]], 1) + pos
             torch.testing.assert_close(x1, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_fp16_weight_cache_follows_in_place_updates():
+    net = _net().eval()
+    obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.25).float()
+    vec = torch.randn(16, 8, 4, device="cuda")
+    with torch.no_grad():
+        net(obs, vec)                          # fills the cache
+        for prm in (net.conv1a.weight, net.transformer.layers[0][0].fn.fn.to_qkv.weight,
+                    net.transformer.layers[1][0].fn.fn.to_qkv.bias, net.token_wV):
+            prm.mul_(0.5)                      # an optimizer-style in-place update
+        got = net(obs, vec)
+        net.fused_acting = False
+        ref = net(obs, vec)
+    torch.testing.assert_close(got[1].float(), ref[1].float(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(got[5].float(), ref[5].float(), rtol=3e-2, atol=3e-2)
