@@ -78,7 +78,8 @@ def main():
         def upd():
             return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
                                sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
-        upd()
+        for _ in range(3):             # MIOpen find for the backward convolutions, GradScaler warm-up
+            upd()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.updates):

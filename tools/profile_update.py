@@ -1,0 +1,60 @@
+"""Profile one PPO minibatch update (Model.train, c4: 256 x 8 rows) with the torch
+profiler: wall time per update and the GPU kernels by total time.
+
+  python tools/profile_update.py [--rows 256] [--updates 5]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd")]
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=256)
+    ap.add_argument("--updates", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    from mapf_amd.config import EnvParameters, make_config
+    from mapf_amd.env import BatchedMapfGym
+    from mapf_amd.maps import generate_warehouse
+    from mapf_amd.model import Model
+    from mapf_amd.runner import DeviceRunner
+    N = 8
+    EnvParameters.N_AGENTS = N
+    EnvParameters.FOV_SIZE = 9
+    env = BatchedMapfGym(make_config(args.rows, 20, 20, num_agents=N, fov=9, num_channel=6, human_mode="random",
+                                     goal_mode="random", fix_choice=1, seed=1234), device=dev)
+    env.reset_seeded(generate_warehouse(20, 20))
+    model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=9)
+    runner = DeviceRunner(env, model, n_steps=1, seed=0)
+    mb, _ = runner.run()
+    idx = torch.arange(args.rows, device=dev)
+    sl = lambda k: mb[k][idx]
+
+    def upd():
+        return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
+                           sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
+    for _ in range(3):
+        upd()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.updates):
+        upd()
+    torch.cuda.synchronize()
+    print(f"update: {(time.perf_counter() - t0) / args.updates * 1e3:.2f} ms for {args.rows} x {N} rows", flush=True)
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for _ in range(args.updates):
+            upd()
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), flush=True)
+
+
+if __name__ == "__main__":
+    main()
