@@ -262,6 +262,22 @@ int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, 
                        int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                        int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream);
 
+/* ---- PPO loss (model.py:115-175) ------------------------------------------
+ * All loss terms of one minibatch update over R = rows x agents elements with A actions each,
+ * plus d(all_loss)/d(new_ps, new_v, new_cv, policy_sig), in one launch.  Device pointers: fp32
+ * new_ps / old_ps / policy_sig / train_valid [R][A], int64 action [R], fp32 new_v, old_v, returns,
+ * new_cv, old_cv, cost_returns, advantage, cost_advantage [R]; sig_fp16 != 0 when policy_sig was
+ * fp16 (autocast): its clamp bounds and 1 - sig round to fp16 like torch's.  HOST pointer coef[6]
+ * = {CLIP_RANGE, ENTROPY_COEF, VALUE_COEF, VALID_COEF, COST_VALUE_COEF, COST_COEF * lambda}.
+ * loss[1] (device) = all_loss; terms[7] (device) = {policy, entropy, critic, valid, cost critic,
+ * cost, clip_frac}; the grads have the shapes of their inputs.  Deterministic (fixed-order reduction). */
+int mapf_ppo_loss(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,
+                  const float *old_v, const float *returns, const float *new_cv, const float *old_cv,
+                  const float *cost_returns, const float *advantage, const float *cost_advantage,
+                  const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
+                  const float *coef, float *loss, float *terms, float *grad_ps, float *grad_v, float *grad_cv,
+                  float *grad_sig, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

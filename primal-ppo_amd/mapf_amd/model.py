@@ -10,6 +10,8 @@ Mirrors the reference's Model (model.py:13-231) and Lagrangian multipliers
     unscale the RCCL all-reduce of the flattened gradient bucket (SURVEY.md §3.4:
     the only exchange step of the path).
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -17,6 +19,42 @@ import torch.nn.functional as F
 
 from .config import EnvParameters, LagrangianParameters, NetParameters, TrainingParameters
 from .net import SCRIMPNet
+
+
+class _FusedPPOLoss(torch.autograd.Function):
+    """model.py:115-175's loss terms and their gradient in one HIP launch
+    (csrc/mapf_ppo.hip, mapf_ppo_loss).  Returns (all_loss, terms[7] = policy, entropy,
+    critic, valid, cost critic, cost, clip_frac); only all_loss carries a gradient."""
+
+    @staticmethod
+    def forward(ctx, new_ps, new_v, new_cv, policy_sig, old_ps, action, old_v, returns, old_cv, cost_returns,
+                advantage, cost_advantage, train_valid, coef):
+        from . import _lib
+        A = new_ps.shape[-1]
+        R = new_ps.numel() // A
+        f = lambda t, *shape: t.detach().float().reshape(*shape).contiguous()
+        ins = [f(new_ps, R, A), f(old_ps, R, A), action.detach().long().reshape(R).contiguous()]
+        vecs = [f(t, R) for t in (new_v, old_v, returns, new_cv, old_cv, cost_returns, advantage, cost_advantage)]
+        sig, tv = f(policy_sig, R, A), f(train_valid, R, A)
+        loss = torch.empty((), device=new_ps.device)
+        terms = torch.empty(7, device=new_ps.device)
+        grads = [torch.empty(R, A, device=new_ps.device), torch.empty(R, device=new_ps.device),
+                 torch.empty(R, device=new_ps.device), torch.empty(R, A, device=new_ps.device)]
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        c = (ctypes.c_float * 6)(*coef)
+        st = ctypes.c_void_p(torch.cuda.current_stream(new_ps.device).cuda_stream)
+        _lib.check(_lib.lib().mapf_ppo_loss(*[p(t) for t in ins], *[p(t) for t in vecs[:6]], p(vecs[6]),
+                                            p(vecs[7]), p(sig), int(policy_sig.dtype == torch.float16), p(tv), R, A,
+                                            c, p(loss), p(terms), *[p(g) for g in grads], st))
+        ctx.save_for_backward(*grads)
+        ctx.meta = [(t.shape, t.dtype) for t in (new_ps, new_v, new_cv, policy_sig)]
+        ctx.mark_non_differentiable(terms)
+        return loss, terms
+
+    @staticmethod
+    def backward(ctx, g_loss, g_terms):
+        out = [(g * g_loss).reshape(shape).to(dtype) for g, (shape, dtype) in zip(ctx.saved_tensors, ctx.meta)]
+        return (*out,) + (None,) * 10
 
 
 class Lagrangian:
@@ -91,6 +129,7 @@ class Model:
             torch.backends.cudnn.benchmark = True
         self.num_agents = num_agents or EnvParameters.N_AGENTS
         self._flat = None
+        self.fused_loss = True        # GPU: the loss terms + their gradient in one launch (_FusedPPOLoss)
         if global_model:
             self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr)
             self.lagrange = get_lagrangian(LagrangianParameters.LAGRANGIAN_TYPE, TrainingParameters.COST_LIMIT_PER_AGENT)
@@ -161,6 +200,17 @@ class Model:
             if TrainingParameters.MINUS_ADV_WITH_CADV:
                 advantage = (advantage - lam * cost_advantage) / (lam + 1)
 
+        if dev.type == "cuda" and self.fused_loss:
+            with torch.autocast(device_type="cuda"):
+                new_ps, new_v, block, policy_sig, _, _, new_cv = self.network(observation, vector, input_state)
+            T = TrainingParameters
+            all_loss, terms = _FusedPPOLoss.apply(
+                new_ps, new_v, new_cv, policy_sig, old_ps, action, old_v, returns, old_cv, cost_returns, advantage,
+                cost_advantage, train_valid,
+                (T.CLIP_RANGE, T.ENTROPY_COEF, T.VALUE_COEF, T.VALID_COEF, T.COST_VALUE_COEF, T.COST_COEF * lam))
+            policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss, clip_frac = terms.unbind()
+            return self._finish_update(all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss,
+                                       cost_loss, clip_frac, advantage, cost_advantage, episode_cost, distributed)
         with torch.autocast(device_type=dev.type, enabled=dev.type == "cuda"):
             new_ps, new_v, block, policy_sig, _, _, new_cv = self.network(observation, vector, input_state)
             new_p = new_ps.gather(-1, action)
@@ -185,7 +235,13 @@ class Model:
                         + TrainingParameters.COST_VALUE_COEF * cost_critic_loss
                         + TrainingParameters.COST_COEF * lam * cost_loss)
         clip_frac = torch.mean(torch.greater(torch.abs(ratio - 1.0), clip).float())
+        return self._finish_update(all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss,
+                                   cost_loss, clip_frac, advantage, cost_advantage, episode_cost, distributed)
 
+    def _finish_update(self, all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss,
+                       clip_frac, advantage, cost_advantage, episode_cost, distributed):
+        """model.py:177-199: backward, gradient exchange, Lagrangian step, clip, Adam, stats."""
+        dev = self.device
         self.net_scaler.scale(all_loss).backward()
         self._allreduce_grads()
         self.net_scaler.unscale_(self.net_optimizer)
@@ -197,9 +253,7 @@ class Model:
         grad_norm = torch.nn.utils.clip_grad_norm_(self.network.parameters(), TrainingParameters.MAX_GRAD_NORM)
         self.net_scaler.step(self.net_optimizer)
         self.net_scaler.update()
-        return [all_loss.detach().cpu().numpy(), policy_loss.detach().cpu().numpy(), entropy.detach().cpu().numpy(),
-                critic_loss.detach().cpu().numpy(), valid_loss.detach().cpu().numpy(),
-                cost_critic_loss.detach().cpu().numpy(), cost_loss.detach().cpu().numpy(),
-                clip_frac.detach().cpu().numpy(), grad_norm.detach().cpu().numpy(),
-                torch.mean(advantage).detach().cpu().numpy(), torch.mean(cost_advantage).detach().cpu().numpy(),
-                self.lagrange.get_lagrangian_param()]
+        stats = torch.stack([t.detach().float().reshape(()) for t in (
+            all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss, clip_frac, grad_norm,
+            torch.mean(advantage), torch.mean(cost_advantage))]).cpu().numpy()       # one device -> host copy
+        return [np.asarray(v) for v in stats] + [self.lagrange.get_lagrangian_param()]
