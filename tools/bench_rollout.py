@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--steps", type=int, default=16, help="rollout length T")
     ap.add_argument("--train", action="store_true", help="also time PPO minibatch updates")
     ap.add_argument("--minibatch", type=int, default=256, help="rows per PPO minibatch (x N agents)")
-    ap.add_argument("--updates", type=int, default=10)
+    ap.add_argument("--updates", type=int, default=20)
+    ap.add_argument("--update-warmup", type=int, default=12)
     ap.add_argument("--reference-maps", action="store_true",
                     help="runner.py:30 semantics: a fresh MapfGym() (random-size warehouse, padded to 40x60) "
                          "per env per rollout, instead of --size")
@@ -78,18 +79,23 @@ def main():
         def upd():
             return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
                                sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
-        for _ in range(3):             # MIOpen find for the backward convolutions, GradScaler warm-up
+        # warm-up: MIOpen find for the backward convolutions, and GradScaler's first finite
+        # step (the updates before it skip Adam; the first real one allocates Adam's state)
+        for _ in range(args.update_warmup):
             upd()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        each = []
         for _ in range(args.updates):
-            upd()
+            t1 = time.perf_counter()
+            upd()                      # returns host numpy stats: synchronises every update
+            each.append(round((time.perf_counter() - t1) * 1e3, 2))
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if rank == 0:
             print(json.dumps({"phase": "PPO minibatch update (fwd+bwd+RCCL all-reduce+Adam)", "n_gpus": world,
                               "ms_per_update": round(dt / args.updates * 1e3, 3),
-                              "rows_per_update_per_gpu": rows, "agents": N,
+                              "ms_median": sorted(each)[len(each) // 2], "ms_each": each, "rows_per_update_per_gpu": rows, "agents": N,
                               "grad_bytes_allreduced": 4 * sum(p.numel() for p in model.network.parameters())}),
                   flush=True)
     if world > 1:
