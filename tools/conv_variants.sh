@@ -3,10 +3,13 @@
 #   nomfma  MFMAs replaced by one VALU op (LDS reads, barriers, loads kept)
 #   now     no weight streaming (every tap uses tap 0's LDS copy)
 #   noin    no input loads (zero images)
+#   nolds   MFMA operands made in registers instead of read from LDS
+#   noepi   no epilogue (accumulators summed, nothing stored)
 set -e
 cd "$(dirname "$0")/../primal-ppo_amd/csrc"
 HIPCC=/opt/rocm/bin/hipcc
-for v in "nomfma:-DMAPF_CONV_DIAG_NOMFMA" "now:-DMAPF_CONV_DIAG_NOW" "noin:-DMAPF_CONV_DIAG_NOIN" "base:"; do
+for v in "nomfma:-DMAPF_CONV_DIAG_NOMFMA" "now:-DMAPF_CONV_DIAG_NOW" "noin:-DMAPF_CONV_DIAG_NOIN" \
+         "nolds:-DMAPF_CONV_DIAG_NOLDS" "noepi:-DMAPF_CONV_DIAG_NOEPI" "base:"; do
     n=${v%%:*}
     d=${v#*:}
     mkdir -p ../lib/obj_c$n
