@@ -57,24 +57,75 @@ def fused_bytes_per_agent(C, F, H, W, N):
     return C * F * F * 4 + 16 + 9 + 9 + 4 + 45 + (-(-H * W // 8) + 64) / N
 
 
+def _oracle_rate(O, cfg, world, B, seconds, threads):
+    """Agent-steps/s of `threads` OS threads, each stepping its own OracleBatch of B envs for
+    ~`seconds` (ctypes drops the GIL inside oc_batch_run; the C oracle has no global state)."""
+    import threading
+    batches = [O.OracleBatch(cfg, world, B) for _ in range(threads)]
+    steps = [0] * threads
+    for b in batches:
+        b.run(5)
+    start = threading.Barrier(threads + 1)
+
+    def work(i):
+        start.wait()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            batches[i].run(10)
+            steps[i] += 10
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    start.wait()
+    t0 = time.perf_counter()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    return B * cfg.num_agents * sum(steps) / dt, sum(steps), dt
+
+
+def host_threads():
+    """Threads for the all-cores CPU baseline: the CPUs this process may run on, capped at 16
+    (the GPU box's CPU share per GPU; nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def host_cpu():
+    """CPU model and nproc of this host (the GPU box's nproc counts the whole machine)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model}, nproc {os.cpu_count()}"
+
+
 def cpu_baseline(world, H, W, N, F, C, seconds):
-    """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host, one thread,
-    on a bounded sample: 32 envs sharing the workload's first map, stepped for ~`seconds`."""
+    """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host on a bounded sample:
+    32 envs per thread sharing the workload's first map, stepped for ~`seconds/2` on one thread,
+    then ~`seconds/2` on every host thread (all host cores, count stated)."""
     from oracle import oracle as O
     world = world if world.ndim == 2 else world[0]
     B = 32
     cfg = O.make_config(H, W, N, F, C, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
-    batch = O.OracleBatch(cfg, world, B)
-    batch.run(5)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        batch.run(10)
-        steps += 10
-    dt = time.perf_counter() - t0
-    return {"value": round(B * N * steps / dt, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{B} envs x {N} agents, {H}x{W}, FOV {F}, {C} channels, random policy, {steps} lockstep "
-                      f"steps (step+observe) in {dt:.1f}s, single thread; reference Python measured 3,442 "
-                      f"agent-steps/s/core on the c2 shape (BASELINE.md)"}
+    one, steps1, dt1 = _oracle_rate(O, cfg, world, B, seconds / 2, 1)
+    P = host_threads()
+    allc, stepsP, dtP = _oracle_rate(O, cfg, world, B, seconds / 2, P) if P > 1 else (one, steps1, dt1)
+    return {"value": round(allc, 1), "unit": "agent-steps/s", "cores": P, "kind": "port",
+            "single_thread_value": round(one, 1), "host": host_cpu(),
+            "sample": f"{P} threads x {B} envs x {N} agents, {H}x{W}, FOV {F}, {C} channels, random policy, "
+                      f"{stepsP} lockstep env-batch steps (step+observe) in {dtP:.1f}s; one thread: {steps1} "
+                      f"steps in {dt1:.1f}s; reference Python measured 3,442 agent-steps/s/core on the c2 "
+                      f"shape (BASELINE.md)"}
 
 
 # BASELINE.json configs as env-only workloads (SURVEY.md §8d); envs are PER GPU.

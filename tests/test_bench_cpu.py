@@ -1,0 +1,45 @@
+"""bench.py's cpu_baseline leg (CPU): the oracle timed on one thread and on every host
+thread, threads stepping independent batches through ctypes."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def test_cpu_baseline_reports_thread_count():
+    import bench
+    from mapf_amd.maps import generate_warehouse
+    line = bench.cpu_baseline(generate_warehouse(10, 10), 10, 10, 4, 11, 6, 1.0)
+    assert line["kind"] == "port" and line["unit"] == "agent-steps/s"
+    assert line["cores"] == bench.host_threads() and 1 <= line["cores"] <= 16
+    assert line["value"] > 0 and line["single_thread_value"] > 0
+    assert f"{line['cores']} threads" in line["sample"] and "nproc" in line["host"]
+
+
+def test_threaded_batches_match_single_thread():
+    """Threads share nothing: a batch stepped alongside others ends where it ends alone
+    (oc_batch_run leaves the last env's observation in the batch's buffers)."""
+    import threading
+
+    from mapf_amd.maps import generate_warehouse
+    from oracle import oracle as O
+    world = generate_warehouse(20, 20)
+    cfg = O.make_config(20, 20, 8, 11, 6, human_mode=1, goal_mode=1, fix_choice=1, seed=99)
+    alone = O.OracleBatch(cfg, world, 4)
+    want = [alone.run(7) for _ in range(3)], alone.obs.copy(), alone.vec.copy()
+    batches = [O.OracleBatch(cfg, world, 4) for _ in range(4)]
+    got = [None] * 4
+
+    def work(i):
+        got[i] = [batches[i].run(7) for _ in range(3)]
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for i, b in enumerate(batches):
+        assert got[i] == want[0]
+        assert (b.obs == want[1]).all() and (b.vec == want[2]).all()
