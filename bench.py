@@ -201,12 +201,20 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # MAPF_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin;
+    # RCCL refuses two ranks on one GPU).  The env path has no collective either way: the
+    # backend only carries the barriers and the max-over-ranks time.
+    backend = os.environ.get("MAPF_BENCH_BACKEND", "nccl")
+    dev_idx = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     dist = None
     if world_size > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from mapf_amd.config import make_config
     from mapf_amd.env import BatchedMapfGym
@@ -287,7 +295,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
