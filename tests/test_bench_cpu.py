@@ -18,6 +18,14 @@ def test_cpu_baseline_reports_thread_count():
     assert f"{line['cores']} threads" in line["sample"] and "nproc" in line["host"]
 
 
+def test_roofline_bytes_match_design():
+    """DESIGN.md §4/§6: 3,001.25 B per agent-step for the rollout / step_observe kernels at c2;
+    SURVEY.md §8d's observe formula at c5 (3,424.6 B)."""
+    import bench
+    assert bench.fused_bytes_per_agent(6, 11, 20, 20, 8) == 3001.25
+    assert abs(bench.observe_bytes_per_agent(7, 11, 80, 80, 64) - 3424.6) < 0.1
+
+
 def test_threaded_batches_match_single_thread():
     """Threads share nothing: a batch stepped alongside others ends where it ends alone
     (oc_batch_run leaves the last env's observation in the batch's buffers)."""
