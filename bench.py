@@ -364,7 +364,8 @@ def main():
                              "step_observe_launch": round(fused_ms, 4),
                              "split": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
                                        "observe_kernel": round(obs_ms, 4)},
-                             "timing": f"HIP events around direct launches ({KT} rollout launches, {KS} of each "
+                             "timing": f"HIP events around direct launches ("
+                                       + (f"{KT} rollout launches, " if path == "rollout" else "") + f"{KS} of each "
                                        f"per-step path; split: search flushed alone); value timed over the {path} "
                                        f"path" + (f" with hipGraph replays of {G} steps" if graph else "")},
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
