@@ -27,6 +27,9 @@
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -shared -fPIC).
  */
 #include <stdint.h>
+#ifdef OC_DIAG
+#include <stdio.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
@@ -76,6 +79,7 @@ typedef struct oc_env {
     oc_cell *hseq; int hseq_len, hseq_idx;
     int16_t *bfs;          /* agent.bfsMap per agent, H*W */
     uint32_t env_id, clock, hreplans, errors;
+    uint32_t fix_empty, fix_deadlock;   /* states the reference raises on / never leaves (fix_actions) */
     /* scratch */
     int *world; int *tmp;
 } oc_env;
@@ -386,27 +390,136 @@ static void action_status(const oc_env *e, const int *act, int *st) {
     }
 }
 
+/* ------------------------------------------------------------------ */
+/* CPython 3.10 set iteration order (Objects/setobject.c set_add_entry,
+ * set_table_resize, set_insert_clean, set_intersection; Objects/tupleobject.c
+ * tuplehash).  fixActions' eviction branch (mapf_gym.py:590-596) appends the
+ * evicted agents in the iteration order of
+ *     set(tuple(x) for x in agentActionPairs) & set(tuple(x) for x in np.array(restrictedAction[r]))
+ * Elements are (int, int) tuples of small ints (numpy int64 hashes like int:
+ * hash(-1) == -2), so the order is deterministic: no hash randomisation.
+ * Sets here hold at most OC_PYSET_MAX elements (tables of 8 or 32 slots). */
+#define OC_PYSET_MAX 8
+typedef struct { int n; uint64_t mask, occ; int64_t key[OC_PYSET_MAX]; uint64_t hash[OC_PYSET_MAX]; int slot[OC_PYSET_MAX]; } oc_pyset;
+
+static uint64_t py_hash_small(int64_t v) { return (uint64_t)(v == -1 ? -2 : v); }
+uint64_t oc_py_hash_pair(int64_t a, int64_t b) {           /* tuplehash, 64-bit xxHash lanes */
+    const uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P5 = 2870177450012600261ULL;
+    uint64_t acc = P5, lane[2] = {py_hash_small(a), py_hash_small(b)};
+    for (int k = 0; k < 2; ++k) { acc += lane[k] * P2; acc = (acc << 31) | (acc >> 33); acc *= P1; }
+    acc += 2ULL ^ (P5 ^ 3527539ULL);
+    return acc == ~0ULL ? 1546275796ULL : acc;
+}
+static int pyset_probe(uint64_t occ, uint64_t mask, uint64_t hash) {   /* first empty slot on the probe path */
+    uint64_t perturb = hash, i = hash & mask;
+    for (;;) {
+        if (!(occ >> i & 1)) return (int)i;
+        if (i + 9 <= mask)                                    /* LINEAR_PROBES */
+            for (uint64_t j = 1; j <= 9; ++j) if (!(occ >> (i + j) & 1)) return (int)(i + j);
+        perturb >>= 5;                                        /* PERTURB_SHIFT */
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+static void pyset_init(oc_pyset *s) { s->n = 0; s->mask = 7; s->occ = 0; }
+static void pyset_add(oc_pyset *s, int64_t key, uint64_t hash) {
+    for (int k = 0; k < s->n; ++k) if (s->key[k] == key) return;   /* already present: no change */
+    int sl = pyset_probe(s->occ, s->mask, hash);
+    s->key[s->n] = key; s->hash[s->n] = hash; s->slot[s->n] = sl; s->n++;
+    s->occ |= 1ULL << sl;
+    if ((uint64_t)s->n * 5 < s->mask * 3) return;            /* fill*5 < mask*3 (no dummies: fill == used) */
+    uint64_t ns = 8;
+    while (ns <= (uint64_t)s->n * 4) ns <<= 1;                /* set_table_resize(used*4) */
+    int ord[OC_PYSET_MAX], m = s->n;
+    for (int k = 0; k < m; ++k) ord[k] = k;
+    for (int a = 1; a < m; ++a)                               /* re-insert in old slot order */
+        for (int b = a; b > 0 && s->slot[ord[b]] < s->slot[ord[b - 1]]; --b) { int t = ord[b]; ord[b] = ord[b - 1]; ord[b - 1] = t; }
+    s->mask = ns - 1; s->occ = 0;
+    for (int k = 0; k < m; ++k) { int e2 = ord[k]; s->slot[e2] = pyset_probe(s->occ, s->mask, s->hash[e2]); s->occ |= 1ULL << s->slot[e2]; }
+}
+static int pyset_iter(const oc_pyset *s, int *ord) {        /* element indices in slot order */
+    int m = 0;
+    for (int sl = 0; sl <= (int)s->mask; ++sl)
+        for (int k = 0; k < s->n; ++k) if (s->slot[k] == sl) ord[m++] = k;
+    return m;
+}
+static int64_t pair_key(int j, int b) { return (int64_t)(j + 1) * 8 + (b + 1); }
+
+/* The evicted agents, in the reference's order.  pairs[j] = agent j's
+ * assigned action or -1 (agentActionPairs[j] == [-1, -1]); (rj, rb)[0..nr) =
+ * restrictedAction[r] in list order.  Returns the count, agents in out_j. */
+int oc_evict_order(const int *pairs, int N, const int *rj, const int *rb, int nr, int *out_j) {
+    oc_pyset P, R, X;
+    pyset_init(&P); pyset_init(&R); pyset_init(&X);
+    int nP = 0, unassigned = 0;
+    for (int j = 0; j < N; ++j) { if (pairs[j] >= 0) ++nP; else unassigned = 1; }
+    nP += unassigned;                                         /* len(set(pairs)) */
+    int rk[OC_PYSET_MAX * 4][2], nR = 0;
+    for (int k = 0; k < nr; ++k) {                            /* len(set(restricted)) */
+        int dup = 0;
+        for (int m = 0; m < nR; ++m) if (rk[m][0] == rj[k] && rk[m][1] == rb[k]) dup = 1;
+        if (!dup && nR < OC_PYSET_MAX * 4) { rk[nR][0] = rj[k]; rk[nR][1] = rb[k]; ++nR; }
+    }
+    int srcj[OC_PYSET_MAX], srcb[OC_PYSET_MAX], ns = 0, ord[OC_PYSET_MAX];
+    if (nR > nP) {      /* set_intersection iterates the smaller operand: set(pairs) */
+        for (int j = 0; j < N; ++j) {
+            int a = pairs[j] >= 0 ? j : -1, b = pairs[j] >= 0 ? pairs[j] : -1;
+            pyset_add(&P, pair_key(a, b), oc_py_hash_pair(a, b));
+        }
+        int m = pyset_iter(&P, ord);
+        for (int k = 0; k < m; ++k) {
+            int64_t key = P.key[ord[k]];
+            int a = (int)(key / 8) - 1, b = (int)(key % 8) - 1;
+            for (int q = 0; q < nR; ++q) if (rk[q][0] == a && rk[q][1] == b) { srcj[ns] = a; srcb[ns] = b; ++ns; break; }
+        }
+    } else {            /* ... set(restricted) */
+        for (int q = 0; q < nR; ++q) pyset_add(&R, pair_key(rk[q][0], rk[q][1]), oc_py_hash_pair(rk[q][0], rk[q][1]));
+        int m = pyset_iter(&R, ord);
+        for (int k = 0; k < m; ++k) {
+            int64_t key = R.key[ord[k]];
+            int a = (int)(key / 8) - 1, b = (int)(key % 8) - 1;
+            if (a >= 0 && pairs[a] == b) { srcj[ns] = a; srcb[ns] = b; ++ns; }
+        }
+    }
+    for (int k = 0; k < ns; ++k) pyset_add(&X, pair_key(srcj[k], srcb[k]), oc_py_hash_pair(srcj[k], srcb[k]));
+    int m = pyset_iter(&X, ord);
+    for (int k = 0; k < m; ++k) out_j[k] = (int)(X.key[ord[k]] / 8) - 1;
+    return m;
+}
+
 /* fixActions (mapf_gym.py:552-612).  random.choice(viable): fix_choice==0
  * takes viable[k % len] for the k-th draw of this call (the rule the golden
  * vectors were generated with, tests/golden/make_golden.py rotating_choice);
  * fix_choice==1 takes viable[mulhi(w0, len)] from Philox (P_FIX, agent,
- * clock, round).  Evictions are appended in ascending agent order (the
- * reference iterates a Python set of tuples there). */
-static int fix_actions(oc_env *e, const int *act, const int *st, int *pairs) {
+ * clock, draw).  Evicted agents are appended in the reference's set order
+ * (oc_evict_order).
+ *
+ * States the reference does not survive:
+ *  - empty viable set: random.choice([]) raises IndexError (:588).  Here the
+ *    agent stays (action 0) and evicts what conflicts with staying, as if 0
+ *    had been drawn; counted (fix_empty).
+ *  - deadlock: agents whose every viable action conflicts with each other's
+ *    (e.g. one pushed by the human into a dead end held by another) evict each
+ *    other forever -- the reference's while loop never ends.  After
+ *    OC_FIX_DRAWS(N) draws in one call the remaining work-list agents stay and
+ *    every mover whose target cell holds a staying agent is reverted to stay,
+ *    until no mover is left blocked (a unique fixpoint: no two agents share a
+ *    cell or swap); counted (fix_deadlock). */
+#ifndef OC_FIX_DRAWS
+#define OC_FIX_DRAWS(N) (16 * (N) + 64)
+#endif
+static void fix_actions(oc_env *e, const int *act, const int *st, int *pairs) {
     int N = e->N;
-    int *queue = (int *)malloc(sizeof(int) * (64 * N * (N + 1) + 8));
+    int *queue = (int *)malloc(sizeof(int) * (N + 2 * (OC_FIX_DRAWS(N) + 1) + 8));
     int qh = 0, qt = 0;
     for (int i = 0; i < N; ++i) pairs[i] = -1;
     for (int i = 0; i < N; ++i) if (st[i] < 0) queue[qt++] = i;
     for (int i = 0; i < N; ++i) if (st[i] == 1) pairs[i] = act[i];
-    int iters = 0, rounds = 0;
+    int draws = 0;
     while (qh < qt) {
-        if (++iters > 64 * N) { e->errors++; break; }
         int idx = queue[qh];
         oc_agent *a = &e->ag[idx];
         if (a->good) {
-            int t = __builtin_ctz(a->good);
-            pairs[idx] = t; qh++;       /* problemAgents.remove(idx): idx is at the head */
+            pairs[idx] = __builtin_ctz(a->good); qh++;   /* problemAgents.remove(idx): idx is at the head */
             continue;
         }
         unsigned viable = (~(a->inv_static | a->inv_human)) & 0x1Fu;
@@ -421,28 +534,51 @@ static int fix_actions(oc_env *e, const int *act, const int *st, int *pairs) {
             if (!hit) { pairs[idx] = t; qh++; done = 1; }
         }
         if (done) continue;
-        int nv = __builtin_popcount(viable), pick = rounds % (nv > 0 ? nv : 1);
-        if (nv == 0) { e->errors++; pairs[idx] = 0; qh++; continue; }   /* reference: IndexError */
-        if (e->cfg.fix_choice == 1) {
-            uint32_t o[4];
-            philox(e->env_id, P_FIX | ((uint32_t)idx << 8), e->clock, (uint32_t)rounds, e->cfg.seed, o);
-            pick = (int)mulhi32(o[0], (uint32_t)nv);
+        if (draws >= OC_FIX_DRAWS(N)) {
+#ifdef OC_DIAG
+            fprintf(stderr, "DEADLOCK env %u clock %u human %d,%d next %d,%d\n", e->env_id, e->clock, e->hpos.r, e->hpos.c, human_next(e).r, human_next(e).c);
+#endif
+            e->fix_deadlock++; e->errors++;
+            break;
         }
-        rounds++;
-        int r = -1;
-        for (int t = 0; t < OC_NA; ++t) if (viable >> t & 1) { if (pick == 0) { r = t; break; } --pick; }
-        /* conflicts = set(pairs) & set(restrictedAction[r]) -> evict */
-        for (int j = 0; j < N; ++j) {
-            if (pairs[j] < 0) continue;
-            int hit = 0;
-            for (int k = 0; k < a->n_restr[r]; ++k)
-                if (a->restr_j[r][k] == j && a->restr_b[r][k] == pairs[j]) { hit = 1; break; }
-            if (hit) { pairs[j] = -1; queue[qt++] = j; }
+        int nv = __builtin_popcount(viable), r = 0;
+        if (nv == 0) {
+#ifdef OC_DIAG
+            fprintf(stderr, "EMPTYVIABLE env %u clock %u agent %d\n", e->env_id, e->clock, idx);
+#endif
+            e->fix_empty++; e->errors++;
+        } else {
+            int pick = draws % nv;
+            if (e->cfg.fix_choice == 1) {
+                uint32_t o[4];
+                philox(e->env_id, P_FIX | ((uint32_t)idx << 8), e->clock, (uint32_t)draws, e->cfg.seed, o);
+                pick = (int)mulhi32(o[0], (uint32_t)nv);
+            }
+            for (int t = 0; t < OC_NA; ++t) if (viable >> t & 1) { if (pick == 0) { r = t; break; } --pick; }
         }
+        draws++;
+        /* conflicts = set(pairs) & set(restrictedAction[r]) -> evict, in set order */
+        int ev[OC_PYSET_MAX];
+        int nev = oc_evict_order(pairs, N, a->restr_j[r], a->restr_b[r], a->n_restr[r], ev);
+        for (int k = 0; k < nev; ++k) { pairs[ev[k]] = -1; queue[qt++] = ev[k]; }
         pairs[idx] = r; qh++;
     }
+#ifdef OC_DIAG
+    if (draws > 8) fprintf(stderr, "DRAWS %d N %d\n", draws, N);
+#endif
+    if (qh < qt) {      /* deadlock: stay, then revert blocked movers to a fixpoint */
+        for (int q = qh; q < qt; ++q) pairs[queue[q]] = 0;
+        for (int changed = 1; changed;) {
+            changed = 0;
+            for (int i = 0; i < N; ++i) {
+                if (pairs[i] <= 0) continue;
+                int tr = e->ag[i].pos.r + DR[pairs[i]], tc = e->ag[i].pos.c + DC[pairs[i]];
+                for (int k = 0; k < N; ++k)
+                    if (k != i && pairs[k] == 0 && e->ag[k].pos.r == tr && e->ag[k].pos.c == tc) { pairs[i] = 0; changed = 1; break; }
+            }
+        }
+    }
     free(queue);
-    return 0;
 }
 
 /* fp64 radial cost (mapf_gym.py:513-526): max(R - ||h - p||, 0) / R */
@@ -505,7 +641,7 @@ int oc_reset_fixed(oc_env *e, const int8_t *map, const int *seq_rc, const int *s
                    int hsr, int hsc, int hgr, int hgc, const int *hseq_rc, int hseq_len) {
     int cells = e->H * e->W;
     memcpy(e->map, map, cells);
-    e->clock = 0; e->errors = 0; e->hreplans = 0;
+    e->clock = 0; e->errors = 0; e->hreplans = 0; e->fix_empty = e->fix_deadlock = 0;
     int S = e->cfg.max_seq;
     for (int i = 0; i < e->N; ++i) {
         e->seq_len[i] = seq_len[i];
@@ -540,7 +676,7 @@ int oc_reset_fixed(oc_env *e, const int8_t *map, const int *seq_rc, const int *s
 int oc_reset_random(oc_env *e, const int8_t *map) {
     int cells = e->H * e->W;
     memcpy(e->map, map, cells);
-    e->clock = 0; e->errors = 0; e->hreplans = 0;
+    e->clock = 0; e->errors = 0; e->hreplans = 0; e->fix_empty = e->fix_deadlock = 0;
     for (int i = 0; i < cells; ++i) e->tmp[i] = map[i];
     /* Human.__init__ (mapf_gym.py:10-16) */
     if (free_cell(e, e->tmp, 1, P_ENTRANCE, 0, 0, &e->hentr) != 0) e->errors++;
@@ -741,6 +877,7 @@ int oc_get_human_path(const oc_env *e, int *rc, int cap) {
 }
 void oc_get_bfs(const oc_env *e, int16_t *out) { memcpy(out, e->bfs, sizeof(int16_t) * e->N * e->H * e->W); }
 uint32_t oc_get_errors(const oc_env *e) { return e->errors; }
+void oc_get_fix_counts(const oc_env *e, uint32_t *out2) { out2[0] = e->fix_empty; out2[1] = e->fix_deadlock; }
 uint32_t oc_get_clock(const oc_env *e) { return e->clock; }
 
 /* Test hook (g2 fuzz scenarios): put the human at path index hstep and set

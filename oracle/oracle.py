@@ -70,6 +70,11 @@ def lib():
         L.oc_get_bfs.argtypes = [P, P]
         L.oc_get_errors.argtypes = [P]; L.oc_get_errors.restype = ctypes.c_uint32
         L.oc_get_clock.argtypes = [P]; L.oc_get_clock.restype = ctypes.c_uint32
+        L.oc_get_fix_counts.argtypes = [P, P]
+        L.oc_evict_order.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P]
+        L.oc_evict_order.restype = ctypes.c_int
+        L.oc_py_hash_pair.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.oc_py_hash_pair.restype = ctypes.c_uint64
         L.oc_random_actions.argtypes = [P, P]
         L.oc_debug_set.argtypes = [P, ctypes.c_int, P]
         L.oc_astar.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
@@ -177,6 +182,13 @@ class OracleEnv:
     def errors(self):
         return int(lib().oc_get_errors(self.h))
 
+    def fix_counts(self):
+        """(empty viable sets, fixActions deadlocks) since reset: the states the
+        reference raises on (mapf_gym.py:588) or never leaves (:563)."""
+        o = np.zeros(2, np.uint32)
+        lib().oc_get_fix_counts(self.h, _p(o))
+        return int(o[0]), int(o[1])
+
     def random_actions(self):
         a = np.zeros(self.N, np.int32)
         lib().oc_random_actions(self.h, _p(a))
@@ -211,6 +223,22 @@ def gae(rewards, values, last_values, gamma=0.95, lam=0.95):
     adv = np.zeros_like(r); ret = np.zeros_like(r)
     lib().oc_gae(_p(r), _p(v), _p(lv), _p(adv), _p(ret), T, M, gamma, lam)
     return adv, ret
+
+
+def evict_order(pairs, restricted):
+    """Agents evicted by fixActions' random branch (mapf_gym.py:590-596), in the
+    iteration order of CPython's set(pairs) & set(restricted).  pairs[j] = agent
+    j's assigned action or -1; restricted = [(j, b), ...] in list order."""
+    pr = np.ascontiguousarray(pairs, np.int32)
+    rs = np.asarray(restricted, np.int32).reshape(-1, 2)
+    rj = np.ascontiguousarray(rs[:, 0]); rb = np.ascontiguousarray(rs[:, 1])
+    out = np.zeros(8, np.int32)
+    n = lib().oc_evict_order(_p(pr), len(pr), _p(rj), _p(rb), len(rs), _p(out))
+    return out[:n].tolist()
+
+
+def py_hash_pair(a, b):
+    return int(lib().oc_py_hash_pair(a, b))
 
 
 def philox_word(c0, c1, c2, c3, seed, w):

@@ -22,6 +22,7 @@
 // replan work lists) -- latency bound, not bandwidth bound.
 #include "mapf_group.h"
 #include "mapf_kernels.h"
+#include "mapf_pyset.h"
 
 namespace mapf {
 
@@ -154,24 +155,26 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
 
     STAMP(2);
     // ---- jointStep: fixActions (:552-612) ----------------------------------
+    // Worklist semantics of the reference; evictions appended in its set order
+    // (mapf_pyset.h).  States the reference does not survive: an
+    // empty viable set (random.choice([]) raises, :588) stays and evicts as if 0
+    // had been drawn; a deadlock (the while loop never ends, :563) is declared
+    // after fix_draws(N) draws: the unplaced agents stay and blocked movers are
+    // reverted to stay until none is left (fix_revert_blocked).
     int fixed = a;
     const uint64_t need = g.ballot(act && (st == -1 || st == -2 || st == -3));
     if (need) {
         int assigned = (act && st == 1) ? a : -1;
         const uint64_t qm = g.ballot(act && st < 0);
         int q = (act && st < 0) ? popc64(qm & below(i)) : -1;
-        int next_q = popc64(qm), head = 0, rounds = 0, iters = 0;
+        int next_q = popc64(qm), head = 0, draws = 0;
         const unsigned viable_me = ~(st_mask | hu_mask) & 0x1Fu;
         while (head < next_q) {
-            if (++iters > 64 * N) {
-                if (i == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
-                break;
-            }
             const uint64_t hm = g.ballot(act && q == head);
             const int idx = ctz64(hm);
-            ++head;
             const unsigned good_idx = g.shfl(good, idx);
             if (good_idx) {
+                ++head;
                 if (i == idx) { assigned = __builtin_ctz(good_idx); q = -1; }
                 continue;
             }
@@ -193,8 +196,13 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
                 if (g.ballot((cj >> t) & 1u)) U |= 1u << t;
             const unsigned fr = viable & ~U;
             if (fr) {
+                ++head;
                 if (i == idx) { assigned = __builtin_ctz(fr); q = -1; }
                 continue;
+            }
+            if (draws >= fix_draws(N)) {        // deadlock: idx stays queued
+                if (i == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
+                break;
             }
             const int nv = __popc(viable);
             int rsel = 0;
@@ -202,16 +210,37 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
                 if (i == idx) atomicAdd(&e.counters[C_EMPTY_VIABLE], 1u);
             } else {
                 int pick;
-                if (e.fix_choice == 0) pick = rounds % nv;
-                else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)rounds, e.seed).x,
+                if (e.fix_choice == 0) pick = draws % nv;
+                else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)draws, e.seed).x,
                                           (uint32_t)nv);
-                ++rounds;
                 rsel = nth_bit(viable, pick);
-                const uint64_t ev = g.ballot((cj >> rsel) & 1u);   // evicted (ascending agent order)
-                if ((ev >> i) & 1ull) { assigned = -1; q = next_q + popc64(ev & below(i)); }
-                next_q += popc64(ev);
             }
+            ++draws;
+            ++head;
+            const uint64_t ev = g.ballot((cj >> rsel) & 1u);   // evicted agents (at most two)
+            int rank = popc64(ev & below(i));
+            if (__builtin_expect(popc64(ev) == 2, 0)) {
+                const int ja = ctz64(ev), jb = 63 - __builtin_clzll(ev);
+                // restrictedAction[idx][rsel] as (j, b) masks on lane j
+                const int Xr = ir + dr(rsel), Xc = ic + dc(rsel);
+                unsigned rb = 0;
+                if (act && i != idx) {
+#pragma unroll
+                    for (int t = 0; t < NA; ++t) {
+                        const int yr = pr + dr(t), yc = pc + dc(t);
+                        if ((yr == Xr && yc == Xc) || (Xr == pr && Xc == pc && yr == ir && yc == ic)) rb |= 1u << t;
+                    }
+                }
+                if (evict_pair_swapped(g, N, rb, assigned, ja, g.shfl_i(assigned, ja), jb, g.shfl_i(assigned, jb)))
+                    rank = 1 - rank;
+            }
+            if ((ev >> i) & 1ull) { assigned = -1; q = next_q + rank; }
+            next_q += popc64(ev);
             if (i == idx) { assigned = rsel; q = -1; }
+        }
+        if (head < next_q) {
+            if (act && assigned < 0) assigned = 0;
+            fix_revert_blocked(g, act, pp, assigned);
         }
         fixed = assigned >= 0 ? assigned : 0;
     }

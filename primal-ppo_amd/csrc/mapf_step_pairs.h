@@ -17,6 +17,7 @@
 #include "mapf_group.h"
 #include "mapf_kernels.h"
 #include "mapf_observe.h"
+#include "mapf_pyset.h"
 
 namespace mapf {
 
@@ -337,7 +338,10 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     STAMP(2);
     if (!(flags & 1u)) return;
 
-    // ---- fixActions (worklist; agent values row-replicated, j's copies in column)
+    // ---- fixActions (worklist; agent values row-replicated, j's copies in column).
+    // Same semantics as step_kernel (mapf_step.hip): reference set order for a
+    // two-agent eviction (mapf_pyset.h), empty viable set -> stay, deadlock after
+    // fix_draws(N) draws -> unplaced agents stay, blocked movers revert.
     int fixed = a_i;
 #if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 2)    // timing diagnostic only
     const uint32_t need = 0;
@@ -350,18 +354,14 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
         int asg_j = (vj && st_j == 1) ? a_j : -1;
         const uint32_t qm = agents_of(eballot(head && vi && st < 0));
         int q = (vi && st < 0) ? __popc(qm & ((1u << i) - 1u)) : -1;
-        int next_q = __popc(qm), hd = 0, rounds = 0, iters = 0;
+        int next_q = __popc(qm), hd = 0, draws = 0;
         const unsigned viable_i = ~(st_mask | hu_mask) & 0x1Fu;
         while (hd < next_q) {
-            if (++iters > 64 * N) {
-                if (li == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
-                break;
-            }
             const int idx = __builtin_ctz(agents_of(eballot(head && vi && q == hd)));
-            ++hd;
             const unsigned good_idx = shfl32(good, base + idx * NP);
             int newa = -1;
             uint32_t ev = 0;
+            bool swap_ev = false;
             if (good_idx) {
                 newa = __builtin_ctz(good_idx);
             } else {
@@ -383,26 +383,73 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
                 if (fr) {
                     newa = __builtin_ctz(fr);
                 } else {
+                    if (draws >= fix_draws(N)) {      // deadlock: idx stays queued
+                        if (li == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
+                        break;
+                    }
                     const int nv = __popc(viable);
                     newa = 0;
                     if (nv == 0) {
                         if (li == 0) atomicAdd(&e.counters[C_EMPTY_VIABLE], 1u);
                     } else {
                         int pick;
-                        if (e.fix_choice == 0) pick = rounds % nv;
-                        else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)rounds,
+                        if (e.fix_choice == 0) pick = draws % nv;
+                        else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)draws,
                                                          e.seed).x, (uint32_t)nv);
-                        ++rounds;
                         newa = nth_bit(viable, pick);
-                        ev = (uint32_t)(eballot((cjm >> newa) & 1u) >> (idx * NP)) & ROW;   // evicted agents
+                    }
+                    ++draws;
+                    ev = (uint32_t)(eballot((cjm >> newa) & 1u) >> (idx * NP)) & ROW;   // evicted agents
+                    if (__builtin_expect(__popc(ev) == 2, 0)) {
+                        // restrictedAction[idx][newa] of agent j, computed in row idx, moved to group lane j
+                        unsigned rb = 0;
+                        if (i == idx && vj && j != idx) {
+                            const int Xr = ri + dr(newa), Xc = ci + dc(newa);
+#pragma unroll
+                            for (int t = 0; t < NA; ++t) {
+                                const int yr = rj + dr(t), yc = cj + dc(t);
+                                if ((yr == Xr && yc == Xc) || (Xr == rj && Xc == cj && yr == ri && yc == ci)) rb |= 1u << t;
+                            }
+                        }
+                        const unsigned rbk = shfl32(rb, base + idx * NP + (li < NP ? li : 0));
+                        const int ja = __builtin_ctz(ev), jb = 31 - __builtin_clz(ev);
+                        const int asg_k = li < NP ? asg_j : -1;          // row 0: lane k holds agent k's
+                        if constexpr (L == 64) {   // one env per wave: scalar operands
+                            const int ba = __builtin_amdgcn_readlane(asg_j, ja), bb = __builtin_amdgcn_readlane(asg_j, jb);
+                            swap_ev = evict_pair_swapped(WaveGroup(), N, li < NP ? rbk : 0u, asg_k, ja, ba, jb, bb);
+                        } else {
+                            const int ba = (int)shfl32((uint32_t)asg_j, base + ja), bb = (int)shfl32((uint32_t)asg_j, base + jb);
+                            swap_ev = evict_pair_swapped(Group(L), N, li < NP ? rbk : 0u, asg_k, ja, ba, jb, bb);
+                        }
                     }
                 }
             }
-            if ((ev >> i) & 1u) { asg_i = -1; q = next_q + __popc(ev & ((1u << i) - 1u)); }
+            ++hd;
+            if ((ev >> i) & 1u) {
+                const int rank = __popc(ev & ((1u << i) - 1u));
+                asg_i = -1;
+                q = next_q + (swap_ev ? 1 - rank : rank);
+            }
             if ((ev >> j) & 1u) asg_j = -1;
             next_q += __popc(ev);
             if (i == idx) { asg_i = newa; q = -1; }
             if (j == idx) asg_j = newa;
+        }
+        if (hd < next_q) {     // deadlock fallback (fix_revert_blocked in the pair layout)
+            if (vi && asg_i < 0) asg_i = 0;
+            if (vj && asg_j < 0) asg_j = 0;
+            uint32_t frontier = agents_of(eballot(head && vi && asg_i == 0));
+            while (frontier) {
+                const bool blk = vi && vj && asg_i > 0 && ((frontier >> j) & 1u) &&
+                                 pack(ri + dr(asg_i), ci + dc(asg_i)) == pj;
+                const uint64_t bm = eballot(blk);
+                uint32_t nb = 0;
+#pragma unroll
+                for (int k = 0; k < NP; ++k) nb |= (uint32_t)(((bm >> (k * NP)) & ROW) != 0ull) << k;
+                if ((nb >> i) & 1u) asg_i = 0;
+                if ((nb >> j) & 1u) asg_j = 0;
+                frontier = nb;
+            }
         }
         fixed = asg_i >= 0 ? asg_i : 0;
     }

@@ -47,6 +47,7 @@ def import_reference():
 alg, astar_mod, mapgen, mg, util = import_reference()
 CHOICE_HITS = [0]
 ROUND = [0]
+EVICT_LOG = []   # per random.choice in fixActions: the agents its pick evicts, in the reference's order
 
 
 def rotating_choice(seq):
@@ -58,7 +59,15 @@ def rotating_choice(seq):
     ROUND[0] += 1
     if k > 1000:
         raise RuntimeError("fixActions did not terminate")
-    return seq[k % len(seq)]
+    choice = seq[k % len(seq)]
+    # record what the pick will evict: the same set expression fixActions
+    # evaluates next (mapf_gym.py:590-591), read from its frame
+    f = sys._getframe(1).f_locals
+    agent, pairs = f.get("agent"), f.get("agentActionPairs")
+    if agent is not None and pairs is not None and choice in agent.restrictedAction:
+        conf = [x for x in set(tuple(x) for x in pairs) & set(tuple(x) for x in np.array(agent.restrictedAction[choice]))]
+        EVICT_LOG.append([int(x[0]) for x in conf])
+    return choice
 
 
 mg.random.choice = rotating_choice
@@ -211,16 +220,17 @@ def constraints_f32(c):
     return np.asarray(c, dtype=np.float32)
 
 
-def g2_fuzz(count, seed):
-    """One-step scenarios on small dense maps."""
+def g2_fuzz(count, seed, name="g2_fuzz", size=(4, 9), density=(0.0, 0.3), agents=(2, 9), keep=None):
+    """One-step scenarios on small dense maps.  keep(evictions) selects scenarios by
+    the eviction lists their fixActions call produced (None: keep all)."""
     rng = np.random.default_rng(seed)
     recs = []
     skipped = 0
     for sc in range(count):
-        H = int(rng.integers(4, 9)); W = int(rng.integers(4, 9))
-        world = -(rng.random((H, W)) < rng.uniform(0.0, 0.3)).astype(np.int64)
+        H = int(rng.integers(*size)); W = int(rng.integers(*size))
+        world = -(rng.random((H, W)) < rng.uniform(*density)).astype(np.int64)
         free = free_cells(world)
-        n = int(rng.integers(2, 9))
+        n = int(rng.integers(*agents))
         if len(free) < n + 2:
             skipped += 1
             continue
@@ -264,6 +274,7 @@ def g2_fuzz(count, seed):
                 return out
             env.fixActions = fix_wrap
             c0 = CHOICE_HITS[0]
+            e0 = len(EVICT_LOG)
             st = env.getActionStatus(actions)
             rw, sh = env.calculateActionReward(actions, st)
             cost = env.calculateCostReward(actions)
@@ -273,6 +284,8 @@ def g2_fuzz(count, seed):
             obs1, vec1 = env.getAllObservations()
         except Exception:
             skipped += 1
+            continue
+        if keep is not None and not keep(EVICT_LOG[e0:]):
             continue
         recs.append(dict(H=H, W=W, n=n, fov=fov, map=world.astype(np.int8).ravel(), pos0=pos0, goal0=goal0,
                          seq=np.array([s.items for s in seqs]), hpath=np.array(env.human.path), hstep0=hstep0,
@@ -294,9 +307,9 @@ def g2_fuzz(count, seed):
         flat[k + "__shape"] = json.dumps([list(a.shape) for a in arrs])
         flat[k] = np.concatenate([a.ravel() for a in arrs]) if arrs else np.zeros(0)
     flat["count"] = len(recs)
-    np.savez_compressed(os.path.join(OUT, "g2_fuzz.npz"), **flat)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **flat)
     allst = np.concatenate([r["status"] for r in recs])
-    print(f"g2_fuzz: {len(recs)} scenarios ({skipped} skipped), statuses {np.unique(allst, return_counts=True)}, "
+    print(f"{name}: {len(recs)} scenarios ({skipped} skipped), statuses {np.unique(allst, return_counts=True)}, "
           f"choice hits {sum(r['choice'] for r in recs)}")
 
 
@@ -503,7 +516,18 @@ def g6_episodes():
     np.savez_compressed(os.path.join(folder, "expected.npz"), **out)
 
 
+def g2_evict():
+    """One-step scenarios whose fixActions evicts two agents with one pick
+    (mapf_gym.py:588-596): the eviction order is the iteration order of a
+    Python set of (agent, action) tuples.  Dense maps, 3..16 agents."""
+    g2_fuzz(60000, 22, name="g2_evict", size=(4, 8), density=(0.1, 0.4), agents=(3, 17),
+            keep=lambda ev: any(len(x) >= 2 for x in ev))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["g2_evict"]:
+        g2_evict()
+        sys.exit(0)
     if sys.argv[1:] == ["g6"]:
         g6_episodes()
         sys.exit(0)
@@ -522,6 +546,7 @@ if __name__ == "__main__":
     run_episode("g1_dense", warehouse(10, 10), 16, 9, 6, 200, 16, p_greedy=0.3)
     run_episode("g1_fixedpath", warehouse(12, 12), 6, 9, 6, 150, 17, human_seq=12, use_da=True, use_hp=True)
     g2_fuzz(3000, 21)
+    g2_evict()
     g3_search(31)
     g4_gae()
     g6_episodes()

@@ -22,10 +22,10 @@ def unpack_obs(packed, shape):
 
 
 class Fuzz:
-    """g2_fuzz.npz: ragged one-step scenarios stored flat."""
+    """g2_fuzz.npz / g2_evict.npz: ragged one-step scenarios stored flat."""
 
-    def __init__(self):
-        z = load("g2_fuzz")
+    def __init__(self, name="g2_fuzz"):
+        z = load(name)
         self.count = int(z["count"])
         self.data = {}
         for k in z.files:

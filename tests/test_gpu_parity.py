@@ -118,8 +118,11 @@ def run_g1(name, pad):
 
 
 # --------------------------------------------------------------------------- g2
-def test_g2_fuzz_on_device():
-    fz = Fuzz()
+@pytest.mark.parametrize("fixture", ["g2_fuzz", "g2_evict"])
+def test_g2_fuzz_on_device(fixture):
+    """g2_fuzz: one-step scenarios; g2_evict: scenarios whose fixActions evicts two
+    agents with one pick, appended in the reference's set order (mapf_pyset.h)."""
+    fz = Fuzz(fixture)
     groups = collections.defaultdict(list)
     for k in range(fz.count):
         c = fz.case(k)
@@ -205,6 +208,11 @@ RANDOM_CASES = {
     "dense_12x12_n16_f9_dahp": dict(B=16, H=12, W=12, n=16, fov=9, nch=6, steps=200, map="wh", da=1, hp=1),
     "c4_40x40_n16_f9_looping": dict(B=16, H=40, W=40, n=16, fov=9, nch=6, steps=100, map="wh", human="looping"),
     "c5_80x80_n64_f11_bfsch": dict(B=3, H=80, W=80, n=64, fov=11, nch=7, steps=40, map="rand"),
+    # one shared random 12x12 map (seed 6) on which fixActions deadlocks (the reference loops
+    # forever, mapf_gym.py:563) and empty viable sets (it raises, :588) occur: counters 1 and 2
+    # equal the oracle's, every step bit-exact through them
+    "r_n8_12x12_f11_deadlock": dict(B=64, H=12, W=12, n=8, fov=11, nch=6, steps=200, map="rand_shared",
+                                    map_seed=6, allow=(1, 2), min_deadlocks=1),
 }
 
 
@@ -212,6 +220,9 @@ def build_maps(case, B, rng):
     from mapf_amd.maps import generate_warehouse, keep_largest_component, random_map
     if case["map"] == "wh":
         return generate_warehouse(case["H"], case["W"]), True
+    if case["map"] == "rand_shared":
+        m = random_map(np.random.default_rng(case["map_seed"]), case["H"], case["W"], 0.3)
+        return keep_largest_component(m), True
     return np.stack([keep_largest_component(random_map(rng, case["H"], case["W"], 0.3)) for _ in range(B)]), False
 
 
@@ -234,10 +245,10 @@ def test_random_mode_matches_oracle(name):
     run_random_case(name, RANDOM_CASES[name], "random" if list(RANDOM_CASES).index(name) % 2 == 1 else "plain")
 
 
-@pytest.mark.parametrize("name", list(FUSED_CASES))
+@pytest.mark.parametrize("name", list(FUSED_CASES) + ["r_n8_12x12_f11_deadlock"])
 def test_fused_step_observe_matches_oracle(name):
     """mapf_step_observe_random: step + observations in one launch, search one launch behind."""
-    run_random_case(name, FUSED_CASES[name], "fused")
+    run_random_case(name, FUSED_CASES.get(name) or RANDOM_CASES[name], "fused")
 
 
 # configurations the one-launch rollout kernel covers (N in 5..8 with whole float4s
@@ -249,6 +260,7 @@ ROLLOUT_CASES = {
     "r_n8_22x22_f11_looping": dict(B=18, H=22, W=22, n=8, fov=11, nch=6, steps=120, map="wh", human="looping"),
     "r_n6_12x12_f7_dense": dict(B=41, H=12, W=12, n=6, fov=7, nch=6, steps=150, map="wh", allow=(2,)),
     "r_n8_24x24_f9": dict(B=9, H=24, W=24, n=8, fov=9, nch=6, steps=100, map="wh"),   # padded row = 32 bits
+    "r_n8_12x12_f11_deadlock": RANDOM_CASES["r_n8_12x12_f11_deadlock"],
 }
 
 
@@ -356,9 +368,103 @@ def run_random_case(name, case, path, expect_rollout_fused=None):
     assert_no_errors(env, allow=allow)
     if allow:   # the oracle counts the same events
         assert int(env.counters()[:8].sum()) == sum(oe.errors() for oe in oracles)
+        fix = np.sum([oe.fix_counts() for oe in oracles], axis=0)
+        assert (int(env.counters()[2]), int(env.counters()[1])) == tuple(int(x) for x in fix)
+        assert fix[1] >= case.get("min_deadlocks", 0)
     else:
         for oe in oracles:
             assert oe.errors() == 0
+
+
+# ---------------------------------------------------------------- full-size c5
+def c5_maps(count, seed=1234):
+    """c5's maps: 80x80, p = 0.3 (random_generator's rule), largest 4-connected component."""
+    from mapf_amd.maps import keep_largest_component, random_map
+    rng = np.random.default_rng(seed)
+    return np.stack([keep_largest_component(random_map(rng, 80, 80, 0.3)) for _ in range(count)])
+
+
+def test_c5_full_size_invariants_and_sampled_oracle():
+    """BASELINE config c5 per GPU (2048 envs x 64 agents, 80x80 random maps, FOV 11,
+    BFS channel): agents on free cells and pairwise distinct in every env after
+    every step, legal statuses, sampled envs bit-exact vs the oracle (step outputs,
+    observations incl. the BFS channel), and the fixActions counters equal to the
+    oracle's on those envs."""
+    B, n, H, W, fov, C = 2048, 64, 80, 80, 11, 7
+    maps = c5_maps(B)
+    env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=C, human_mode="random", goal_mode="random",
+                 fix_choice=1, shared_map=False, seed=1234)
+    env.reset_seeded(maps)
+    cfg = O.make_config(H, W, n, fov, C, human_mode=1, goal_mode=1, fix_choice=1, seed=1234)
+    sample = [0, 1, 777, 2047]
+    oracles = {b: O.OracleEnv(cfg, env_id=b) for b in sample}
+    for b, oe in oracles.items():
+        oe.reset_random(maps[b])
+    free = maps == 0
+    bidx = np.arange(B)[:, None]
+    for t in range(30):
+        acts = env.random_actions()
+        a_host = acts.cpu().numpy()
+        out = host(env.step(acts))
+        obs, vec = env.observe()
+        pos = env.get_state()["pos"]
+        assert free[bidx, pos[..., 0], pos[..., 1]].all(), f"t={t}: agent off the free cells"
+        srt = np.sort(pos[..., 0] * W + pos[..., 1], axis=1)
+        assert (np.diff(srt, axis=1) > 0).all(), f"t={t}: two agents share a cell"
+        assert np.isin(out["status"], [1, -1, -2, -3, -4]).all()
+        for b, oe in oracles.items():
+            r = oe.step(a_host[b])
+            np.testing.assert_array_equal(out["status"][b], r["status"], err_msg=f"t={t} b={b}")
+            np.testing.assert_array_equal(out["actions_fixed"][b], r["fixed"], err_msg=f"t={t} b={b}")
+            np.testing.assert_array_equal(out["train_valid"][b], r["valid"], err_msg=f"t={t} b={b}")
+            if b == sample[t % len(sample)]:
+                oo, ov = oe.observe()
+                np.testing.assert_array_equal(obs[b].cpu().numpy(), oo, err_msg=f"t={t} b={b} obs")
+                np.testing.assert_array_equal(vec[b].cpu().numpy(), ov, err_msg=f"t={t} b={b} vec")
+    assert_no_errors(env, allow=(1, 2))
+    for oe in oracles.values():
+        assert oe.errors() == sum(oe.fix_counts())
+
+
+# fixActions deadlocks found by the oracle on c5's maps (c5_maps, seed 1234): env id ->
+# steps to run past it.  An agent pushed by the human into a dead end held by another
+# agent: each one's only viable actions evict the other, and the reference's while
+# loop (mapf_gym.py:563) never ends.
+DEADLOCK_ENVS = {512: 470, 763: 920, 1081: 800, 1862: 380}
+
+
+def test_fix_deadlocks_match_oracle():
+    """Through the deadlocks: the device declares them where the oracle does (after
+    fix_draws(N) draws), resolves them to the same conflict-free moves (unplaced agents
+    stay, blocked movers revert), and agents stay on distinct free cells."""
+    maps = c5_maps(max(DEADLOCK_ENVS) + 1)
+    H = W = 80
+    n = 64
+    for b, T in DEADLOCK_ENVS.items():
+        env = mk_env(B=1, H=H, W=W, num_agents=n, fov=11, num_channel=6, human_mode="random", goal_mode="random",
+                     fix_choice=1, shared_map=False, keep_bfs=False, seed=1234, env_offset=b)
+        env.reset_seeded(maps[b:b + 1])
+        oe = O.OracleEnv(O.make_config(H, W, n, 11, 6, human_mode=1, goal_mode=1, fix_choice=1, keep_bfs=0,
+                                       seed=1234), env_id=b)
+        oe.reset_random(maps[b])
+        free = maps[b] == 0
+        for t in range(T):
+            acts = env.random_actions()
+            a_host = acts.cpu().numpy()[0]
+            out = host(env.step(acts))
+            r = oe.step(a_host)
+            np.testing.assert_array_equal(out["status"][0], r["status"], err_msg=f"env {b} t={t}")
+            np.testing.assert_array_equal(out["actions_fixed"][0], r["fixed"], err_msg=f"env {b} t={t}")
+            pos = env.get_state()["pos"][0]
+            assert free[pos[:, 0], pos[:, 1]].all()
+            assert len(np.unique(pos[:, 0] * W + pos[:, 1])) == n, f"env {b} t={t}: shared cell"
+        p, _ = oe.agents()
+        np.testing.assert_array_equal(env.get_state()["pos"][0], p)
+        empty, deadlocks = oe.fix_counts()
+        assert deadlocks >= 1, f"env {b}: the oracle saw no deadlock"
+        c = env.counters()
+        assert (int(c[1]), int(c[2])) == (deadlocks, empty), f"env {b}: counters {c[:3]}"
+        env.close()
 
 
 # ---------------------------------------------------------------- full-size c2

@@ -71,9 +71,10 @@ def run_fuzz_case(c):
     return env
 
 
-def test_g2_fuzz_one_step_bit_exact():
-    fz = Fuzz()
-    assert fz.count > 2000
+@pytest.mark.parametrize("name,min_count", [("g2_fuzz", 2000), ("g2_evict", 1000)])
+def test_g2_fuzz_one_step_bit_exact(name, min_count):
+    fz = Fuzz(name)
+    assert fz.count > min_count
     bad = []
     for i in range(fz.count):
         c = fz.case(i)
