@@ -86,13 +86,17 @@ def _oracle_rate(O, cfg, world, B, seconds, threads):
 
 
 def host_threads():
-    """Threads for the all-cores CPU baseline: the CPUs this process may run on, capped at 16
-    (the GPU box's CPU share per GPU; nproc there shows the whole machine)."""
+    """Threads for the all-cores CPU baseline: this GPU's CPU share of the host.  The GPU box
+    runs one job per GPU and gives each its share of the machine (OMP_NUM_THREADS, 16 there;
+    nproc shows the whole machine's 256); elsewhere, every CPU this process may run on."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
 
 def host_cpu():
@@ -112,7 +116,9 @@ def host_cpu():
 def cpu_baseline(world, H, W, N, F, C, seconds):
     """The oracle (CPU restatement, oracle/mapf_oracle.c) timed on this host on a bounded sample:
     32 envs per thread sharing the workload's first map, stepped for ~`seconds/2` on one thread,
-    then ~`seconds/2` on every host thread (all host cores, count stated)."""
+    then ~`seconds/2` on every thread of this GPU's CPU share (host_threads; SURVEY.md §8d: all
+    host cores, count stated).  `value` and `cores` are that share's figures; `per_core_value`
+    and `host_cores` let a reader scale to the whole machine."""
     from oracle import oracle as O
     world = world if world.ndim == 2 else world[0]
     B = 32
@@ -121,7 +127,9 @@ def cpu_baseline(world, H, W, N, F, C, seconds):
     P = host_threads()
     allc, stepsP, dtP = _oracle_rate(O, cfg, world, B, seconds / 2, P) if P > 1 else (one, steps1, dt1)
     return {"value": round(allc, 1), "unit": "agent-steps/s", "cores": P, "kind": "port",
-            "single_thread_value": round(one, 1), "host": host_cpu(),
+            "cores_definition": "this GPU's CPU share of the host (OMP_NUM_THREADS, else the affinity mask)",
+            "single_thread_value": round(one, 1), "per_core_value": round(allc / P, 1),
+            "host_cores": os.cpu_count(), "host": host_cpu(),
             "sample": f"{P} threads x {B} envs x {N} agents, {H}x{W}, FOV {F}, {C} channels, random policy, "
                       f"{stepsP} lockstep env-batch steps (step+observe) in {dtP:.1f}s; one thread: {steps1} "
                       f"steps in {dt1:.1f}s; reference Python measured 3,442 agent-steps/s/core on the c2 "
@@ -190,6 +198,11 @@ def main():
                     help="fused/split paths: steps per captured hipGraph, a multiple of 3; 0 = direct")
     ap.add_argument("--kernel-launches", type=int, default=None,
                     help="launches timed with HIP events for the roofline kernel (default: per path)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --envs per GPU (SURVEY.md §8d: 4096 per GPU); strong: --envs in total, "
+                         "split evenly over the ranks")
+    ap.add_argument("--no-paths", action="store_true",
+                    help="skip the per-path breakdown (slot-buffer rollout, one launch per step)")
     args = ap.parse_args()
     if args.split:
         args.path = "split"
@@ -220,6 +233,10 @@ def main():
     from mapf_amd.env import BatchedMapfGym
 
     B, N, H, W, F, C = args.envs, args.agents, args.size, args.size, args.fov, args.channels
+    if args.scaling == "strong":
+        if B % world_size:
+            raise SystemExit(f"--scaling strong: {B} envs do not split over {world_size} ranks")
+        B //= world_size
     world, shared = make_maps(preset["maps"], B, H, W, rank)
     env = BatchedMapfGym(make_config(B, H, W, num_agents=N, fov=F, num_channel=C, human_mode="random",
                                      goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B,
@@ -332,6 +349,46 @@ def main():
     search_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(KS)]))
     obs_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KS)]))
     roll_ms = event_ms(lambda: rollout(T), KT) if path == "rollout" else None
+
+    # The same workload down each path, each with its own roofline fraction:
+    #  rollout_inplace  mapf_rollout_random, every step re-writes the [B]-leading buffers
+    #                   (95 MB at c2: they stay resident in the 256 MiB Infinity Cache);
+    #  rollout_slots    mapf_rollout_random, step t writes slot t of [T]-leading rollout
+    #                   buffers (runner.py:104-115's per-rollout arrays): every store is a
+    #                   fresh HBM line;
+    #  step_observe     one launch per step (the policy-in-the-loop path).
+    paths = None
+    if rank == 0 and not args.no_paths:
+        bpa_f = fused_bytes_per_agent(C, F, H, W, N)
+
+        def entry(ms_step, bpa, note):
+            gbs = bpa * B * N / (ms_step * 1e-3) / 1e9
+            return {"ms_per_step": round(ms_step, 5), "agent_steps_per_s": round(B * N / (ms_step * 1e-3), 1),
+                    "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "bytes_per_agent_step": round(bpa, 2), "timing": note}
+        paths = {}
+        if env.fused:
+            paths["step_observe"] = entry(fused_ms, bpa_f, f"HIP events, {KS} direct launches")
+        else:
+            paths["split"] = entry(step_ms + search_ms + obs_ms, bpa_f,
+                                   f"HIP events, {KS} x (step, search, observe) launches")
+        if env.rollout_fused:
+            if roll is None:
+                paths["rollout_inplace"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
+                TS = T
+                sl = dict(actions=torch.zeros(TS, B, N, dtype=torch.int32, device=dev),
+                          obs=torch.zeros(TS, B, N, C, F, F, device=dev), vec=torch.zeros(TS, B, N, 4, device=dev),
+                          out={k: torch.zeros((TS,) + tuple(v.shape), dtype=v.dtype, device=dev)
+                               for k, v in env.out.items()})
+                run_sl = lambda: env.rollout_random(TS, slots=True, **sl)   # noqa: E731
+                run_sl()
+                ms = event_ms(run_sl, max(2, min(8, KT)))
+                paths["rollout_slots"] = entry(ms / TS, bpa_f, f"HIP events, {max(2, min(8, KT))} launches of "
+                                                               f"{TS} steps, {TS} slots")
+                del sl
+                torch.cuda.empty_cache()
+            else:
+                paths["rollout_slots"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
     counters = env.counters()
 
     if rank == 0:
@@ -349,7 +406,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (seeded warehouse episodes on device, uniform random policy)",
             "config": {"workload": f"{args.config}: {B} envs x {N} agents per GPU, {H}x{W} "
                                    f"{'warehouse' if shared else 'random p=0.3 maps (one per env)'}, FOV {F}, "
@@ -358,6 +415,7 @@ def main():
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
                        "path": path + (f" (T={T} steps per launch{', slot buffers' if roll else ''})"
                                        if path == "rollout" else ""),
+                       "total_envs": B * world_size,
                        "parallelism": f"env-shards x{world_size}"},
             "breakdown_ms": {"rollout_launch": round(roll_ms, 4) if roll_ms else None,
                              "rollout_per_step": round(roll_ms / T, 5) if roll_ms else None,
@@ -376,6 +434,17 @@ def main():
                          "agents_per_step": B * N},
             "device_counters": [int(x) for x in counters[:8]],
         }
+        if paths:
+            line["paths"] = paths
+        # States the reference does not survive, counted and resolved on the device:
+        # empty viable sets (it raises) and fixActions deadlocks (it never returns).  Any other
+        # counter is an impossible state: the line is then marked invalid.
+        line["reference_unsurvivable_states"] = {"empty_viable": int(counters[2]), "fix_deadlock": int(counters[1])}
+        bad = {i: int(counters[i]) for i in (0, 3, 4, 5, 6) if counters[i]}
+        if bad:
+            line["valid"] = False
+            line["invalid_reason"] = f"device error counters {bad}"
+            print(f"bench: device error counters {bad}", file=sys.stderr)
         if world_size == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(world, H, W, N, F, C, args.cpu_seconds)
         else:

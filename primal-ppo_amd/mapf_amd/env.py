@@ -21,6 +21,23 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _check(t, dtype, numel, device, name):
+    """Every buffer handed to the kernels as a raw pointer: right dtype, contiguous,
+    the element count the kernel writes, on the handle's GPU (a wrong one would be
+    an out-of-bounds device write, not an error)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(t).__name__}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: not contiguous")
+    if t.numel() != numel:
+        raise ValueError(f"{name}: {t.numel()} elements, expected {numel}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    return t
+
+
 class BatchedMapfGym:
     """B environments x N agents on one GPU (one handle per process/GPU)."""
 
@@ -149,7 +166,7 @@ class BatchedMapfGym:
         steps (the device work lists rotate over 3 slots)."""
         if actions is None:
             actions = self.actions
-        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
+        _check(actions, torch.int32, self.B * self.N, self.device, "actions")
         _lib.check(_lib.lib().mapf_step(self.h, _ptr(actions), ctypes.byref(self._stepout),
                                         1 if commit else 0, _stream(self.device)))
         return self.out
@@ -158,7 +175,7 @@ class BatchedMapfGym:
         """Random-policy step: actions drawn on device (written to `actions`), then stepped, one launch."""
         if actions is None:
             actions = self.actions
-        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
+        _check(actions, torch.int32, self.B * self.N, self.device, "actions")
         _lib.check(_lib.lib().mapf_step_random(self.h, _ptr(actions), ctypes.byref(self._stepout),
                                                1 if commit else 0, _stream(self.device)))
         return self.out
@@ -167,8 +184,8 @@ class BatchedMapfGym:
         """getAllObservations for all envs: obs [B, N, C, F, F], vec [B, N, 4] (float32)."""
         obs = self.obs if obs is None else obs
         vec = self.vec if vec is None else vec
-        assert obs.is_contiguous() and vec.is_contiguous()
-        assert obs.numel() == self.B * self.N * self.C * self.F * self.F and vec.numel() == self.B * self.N * 4
+        _check(obs, torch.float32, self.B * self.N * self.C * self.F * self.F, self.device, "obs")
+        _check(vec, torch.float32, self.B * self.N * 4, self.device, "vec")
         _lib.check(_lib.lib().mapf_observe(self.h, _ptr(obs), _ptr(vec), _stream(self.device)))
         return obs, vec
 
@@ -183,10 +200,10 @@ class BatchedMapfGym:
             actions = self.actions
         obs = self.obs if obs is None else obs
         vec = self.vec if vec is None else vec
-        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == self.B * self.N
-        assert obs.is_contiguous() and vec.is_contiguous()
-        assert obs.numel() == self.B * self.N * self.C * self.F * self.F and vec.numel() == self.B * self.N * 4
-        fn = _lib.lib().mapf_step_observe_random if random_policy else _lib.lib().mapf_step_observe
+        _check(actions, torch.int32, self.B * self.N, self.device, "actions")
+        _check(obs, torch.float32, self.B * self.N * self.C * self.F * self.F, self.device, "obs")
+        _check(vec, torch.float32, self.B * self.N * 4, self.device, "vec")
+        fn =_lib.lib().mapf_step_observe_random if random_policy else _lib.lib().mapf_step_observe
         so = self._stepout if out is None else self._make_stepout(self._check_out(out))
         _lib.check(fn(self.h, _ptr(actions), ctypes.byref(so), _ptr(obs), _ptr(vec), _stream(self.device)))
         return (self.out if out is None else out), obs, vec
@@ -202,16 +219,17 @@ class BatchedMapfGym:
         actions = self.actions if actions is None else actions
         obs = self.obs if obs is None else obs
         vec = self.vec if vec is None else vec
-        assert actions.dtype == torch.int32 and actions.is_contiguous() and actions.numel() == k * self.B * self.N
-        assert obs.is_contiguous() and obs.numel() == k * self.B * self.N * self.C * self.F * self.F
-        assert vec.is_contiguous() and vec.numel() == k * self.B * self.N * 4
+        _check(actions, torch.int32, k * self.B * self.N, self.device, "actions")
+        _check(obs, torch.float32, k * self.B * self.N * self.C * self.F * self.F, self.device, "obs")
+        _check(vec, torch.float32, k * self.B * self.N * 4, self.device, "vec")
         if out is None:
-            assert not slots, "slots=True needs [T]-leading output buffers (out=...)"
+            if slots:
+                raise ValueError("slots=True needs [T]-leading output buffers (out=...)")
             so, out = self._stepout, self.out
         else:
             for key, t in out.items():
                 ref = self.out[key]
-                assert t.dtype == ref.dtype and t.is_contiguous() and t.numel() == k * ref.numel(), key
+                _check(t, ref.dtype, k * ref.numel(), self.device, key)
             so = self._make_stepout(out)
         _lib.check(_lib.lib().mapf_rollout_random(self.h, int(T), 1 if slots else 0, _ptr(actions), ctypes.byref(so),
                                                   _ptr(obs), _ptr(vec), _stream(self.device)))
@@ -220,7 +238,7 @@ class BatchedMapfGym:
     def _check_out(self, out):
         for k, t in out.items():
             ref = self.out[k]
-            assert t.dtype == ref.dtype and t.is_contiguous() and t.numel() == ref.numel() and t.device == self.device, k
+            _check(t, ref.dtype, ref.numel(), self.device, k)
         return out
 
     def flush(self):
@@ -229,6 +247,7 @@ class BatchedMapfGym:
 
     def random_actions(self, out=None):
         out = self.actions if out is None else out
+        _check(out, torch.int32, self.B * self.N, self.device, "actions")
         _lib.check(_lib.lib().mapf_random_actions(self.h, _ptr(out), _stream(self.device)))
         return out
 
@@ -290,6 +309,12 @@ def gae(rewards, values, last_values, gamma=0.95, lam=0.95):
     """runner.py:117-149 on device: rewards/values [T, ...] float32, last_values [...]."""
     T = rewards.shape[0]
     M = rewards[0].numel()
+    dev = rewards.device
+    if dev.type != "cuda":
+        raise ValueError("gae: tensors must be on the GPU")
+    _check(rewards, torch.float32, T * M, dev, "rewards")
+    _check(values, torch.float32, T * M, dev, "values")
+    _check(last_values, torch.float32, M, dev, "last_values")
     adv = torch.empty_like(rewards)
     ret = torch.empty_like(rewards)
     _lib.check(_lib.lib().mapf_gae(_ptr(rewards), _ptr(values), _ptr(last_values), _ptr(adv), _ptr(ret), T, M,
@@ -299,6 +324,12 @@ def gae(rewards, values, last_values, gamma=0.95, lam=0.95):
 
 def normalize_advantages(returns, values, cost_returns, cost_values, lagrange=0.0, mix=False):
     """model.py:106-113 on device; returns (advantage, cost_advantage)."""
+    dev, M = returns.device, returns.numel()
+    if dev.type != "cuda":
+        raise ValueError("normalize_advantages: tensors must be on the GPU")
+    for name, t in (("returns", returns), ("values", values), ("cost_returns", cost_returns),
+                    ("cost_values", cost_values)):
+        _check(t, torch.float32, M, dev, name)
     adv = torch.empty_like(returns)
     cadv = torch.empty_like(returns)
     _lib.check(_lib.lib().mapf_normalize_advantages(
@@ -310,8 +341,15 @@ def normalize_advantages(returns, values, cost_returns, cost_values, lagrange=0.
 def sample_actions(ps, seed, step, out32=None, out64=None):
     """model.py:38-40 on device: ps [..., 5] float32 -> actions."""
     ps2 = ps.reshape(-1, ps.shape[-1])
-    assert ps2.dtype == torch.float32 and ps2.stride(1) == 1
+    if ps2.dtype != torch.float32 or ps2.stride(1) != 1 or ps2.shape[-1] != 5 or ps2.device.type != "cuda":
+        raise ValueError("sample_actions: ps must be float32 [..., 5] on the GPU with unit stride in the last dim")
     M = ps2.shape[0]
+    if out32 is None and out64 is None:
+        raise ValueError("sample_actions: give out32 and/or out64")
+    if out32 is not None:
+        _check(out32, torch.int32, M, ps2.device, "out32")
+    if out64 is not None:
+        _check(out64, torch.int64, M, ps2.device, "out64")
     _lib.check(_lib.lib().mapf_sample_actions(_ptr(ps2), ps2.stride(0), _ptr(out32), _ptr(out64), M, seed, step,
                                               _stream(ps.device)))
     return out32 if out32 is not None else out64

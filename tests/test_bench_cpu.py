@@ -13,9 +13,20 @@ def test_cpu_baseline_reports_thread_count():
     from mapf_amd.maps import generate_warehouse
     line = bench.cpu_baseline(generate_warehouse(10, 10), 10, 10, 4, 11, 6, 1.0)
     assert line["kind"] == "port" and line["unit"] == "agent-steps/s"
-    assert line["cores"] == bench.host_threads() and 1 <= line["cores"] <= 16
+    assert line["cores"] == bench.host_threads() >= 1
     assert line["value"] > 0 and line["single_thread_value"] > 0
+    assert abs(line["per_core_value"] * line["cores"] - line["value"]) < 1.0 + 1e-6 * line["value"]
     assert f"{line['cores']} threads" in line["sample"] and "nproc" in line["host"]
+
+
+def test_host_threads_is_the_gpu_share(monkeypatch):
+    """On the GPU box OMP_NUM_THREADS names this GPU's CPU share (16): the baseline runs that
+    many threads, not nproc."""
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.host_threads() == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.host_threads() == len(os.sched_getaffinity(0))
 
 
 def test_roofline_bytes_match_design():
