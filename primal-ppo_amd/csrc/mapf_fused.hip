@@ -144,6 +144,7 @@ struct RolloutOut {
     StepOut out;
     float *obs, *vec;
     int slots;
+    int xcd_remap;
 };
 
 __host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
@@ -164,7 +165,14 @@ template <bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(DevEnv e, int T, RolloutOut ro) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int E = 4;                     // envs per workgroup, one per wave
-    const int b0 = (int)blockIdx.x * E;
+    // XCD-aware env order: workgroups are dealt round-robin over the 8 XCDs, so workgroup w
+    // takes env block (w % 8) * (grid / 8) + w / 8 -- each XCD owns one contiguous range of
+    // envs, and the output lines that several envs share (status: 16 envs per 128-B line)
+    // are completed in one XCD's L2 instead of leaving it as partial lines from several.
+    const int nb = (int)gridDim.x;
+    const int blk = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
+                                                    : (int)blockIdx.x;
+    const int b0 = blk * E;
     const int nenv = min(E, e.B - b0);
     const int le = (int)(threadIdx.x >> 6);
     ObsLds L = obs_layout(e, E, smem, true);
@@ -198,7 +206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
         if (o.constraints) o.constraints += s * BN;
         if (o.reward_total) o.reward_total += s * BN;
         PairsDeferred dfr;
-        step_pairs_env<8, true, true, true>(E, R.actions + s * BN, o, 3u, 0, (int)(blockIdx.x * 256 + threadIdx.x),
+        step_pairs_env<8, true, true, true>(E, R.actions + s * BN, o, 3u, 0, blk * 256 + (int)threadIdx.x,
                                             L, b0, RegMap{mreg, true}, dfr, &rs);
         if (le < nenv) {
             const ObsGroup g = obs_wave_init(E, L, le, mreg);
@@ -232,12 +240,14 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     size_t lds = rollout_lds_bytes(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
+    static int remap = -1;
+    if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
     if (slots)
         hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T,
-                           RolloutOut{actions, out, obs, vec, slots});
+                           RolloutOut{actions, out, obs, vec, slots, remap});
     else
         hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, e, T,
-                           RolloutOut{actions, out, obs, vec, slots});
+                           RolloutOut{actions, out, obs, vec, slots, remap});
     return true;
 }
 
