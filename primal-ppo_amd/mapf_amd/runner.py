@@ -13,12 +13,17 @@ the rollout is a device tensor written in place:
   advantages / returns <- mapf_gae for reward and cost (:121-149)
 
 Buffers are laid out [T, B, N, ...] (t-major: each step writes one contiguous
-slice); `batch()` exposes them with the BatchValues field names (util.py:41-54)
-reshaped to [T*B, N, ...] rows, the contract driver.py:101-121 concatenates on
-axis 0.  hiddenState is all zeros in the reference (runner.py:47-48, never read
-by the net) and is returned as an expanded zero view, not materialised.
-OneEpPerformance counters (util.py:56-65) are reduced on the device.
+slice).  `batch()` exposes them as util.BatchValues (util.py:41-54: attribute
+names, read by driver.py with getattr) whose rows are ENV-MAJOR [B*T, N, ...]
+views: env 0's T steps, then env 1's -- the order driver.py:101-121 produces by
+concatenating one runner's result after another, so driver.py:125-131's
+`inds = np.arange(N_STEPS)` selects env 0's rollout as it selects runner 0's.
+Indexing a view gathers only the minibatch rows.  hiddenState is all zeros in
+the reference (runner.py:47-48, never read by the net): expanded zero views.
+OneEpPerformance (util.py:56-65) is per env (the mean over the B envs; every
+env's counters via performance_per_env()).
 """
+import numpy as np
 import torch
 
 from .config import EnvParameters, NetParameters, TrainingParameters
@@ -40,24 +45,90 @@ def reference_maps(env: BatchedMapfGym, world_size=None, seed=0):
 
 
 class OneEpPerformance:
-    """util.py:56-65 (sums over all B envs of the rollout)."""
+    """util.py:56-65: the counters of ONE env's rollout (runner.py:66-99 sums them over one
+    env's steps).  DeviceRunner.run() returns the mean over its B envs: driver.py:108-117
+    passes one runner's object on (its loop overwrites `performance` with each result in
+    turn), and Model.train feeds performance.episodeCostReward to the Lagrangian
+    (model.py:180, lagrange.py) -- a per-env quantity.  performance_per_env() has all B."""
+
+    FIELDS = ("totalGoals", "shadowGoals", "episodeReward", "staticCollide", "humanCollide", "agentCollide",
+              "episodeCostReward", "constraintViolations")
 
     def __init__(self):
-        self.totalGoals = 0
-        self.shadowGoals = 0
-        self.episodeReward = 0
-        self.staticCollide = 0
-        self.humanCollide = 0
-        self.agentCollide = 0
-        self.episodeCostReward = 0
-        self.constraintViolations = 0
+        for f in self.FIELDS:
+            setattr(self, f, 0)
+
+
+class EnvMajorRows:
+    """The [B*T, ...] rows of a t-major [T, B, ...] rollout buffer in ENV-MAJOR order:
+    row r = env r // T, step r % T -- the order driver.py:101-121 builds by concatenating
+    the runners' results (runner k's T rows, then runner k+1's).  Rows [0, T) are env 0's
+    rollout, i.e. what `inds = np.arange(N_STEPS)` (driver.py:125) trains on, like the
+    reference's first runner.  Zero-copy: indexing gathers just the rows asked for (a
+    minibatch) from the buffer; materialize() copies all of them."""
+
+    def __init__(self, buf, T, B):
+        self.buf, self.T, self.B = buf, T, B
+        self.shape = torch.Size((B * T,) + tuple(buf.shape[2:]))
+        self.dtype, self.device = buf.dtype, buf.device
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __getitem__(self, idx):
+        n = self.shape[0]
+        if isinstance(idx, int):
+            if not -n <= idx < n:
+                raise IndexError(idx)
+            idx %= n
+            return self.buf[idx % self.T, idx // self.T]
+        if isinstance(idx, slice):
+            idx = torch.arange(*idx.indices(n), device=self.device)
+        else:
+            idx = torch.as_tensor(np.asarray(idx) if not isinstance(idx, torch.Tensor) else idx,
+                                  device=self.device).long()
+            if idx.numel() and (int(idx.min()) < -n or int(idx.max()) >= n):
+                raise IndexError("row index out of range")
+            idx = idx % n
+        return self.buf[idx % self.T, idx // self.T]
+
+    def materialize(self):
+        return self.buf.transpose(0, 1).reshape(self.shape)
+
+
+class ZeroRows:
+    """hiddenState rows: all zeros in the reference (runner.py:47-48, never read by the
+    net), handed out as expanded zero views, never materialised."""
+
+    def __init__(self, n, row_shape, device):
+        self.shape = torch.Size((n,) + tuple(row_shape))
+        self.dtype, self.device = torch.float32, device
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __getitem__(self, idx):
+        k = len(range(*idx.indices(self.shape[0]))) if isinstance(idx, slice) else len(np.atleast_1d(
+            idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)))
+        return torch.zeros((), device=self.device).expand((k,) + tuple(self.shape[1:]))
 
 
 class BatchValues:
-    """util.py:41-54 field names; tensors on the device."""
+    """util.py:41-54: the rollout's arrays by the reference's attribute names (driver.py reads
+    them with getattr), each an EnvMajorRows view over the device buffers; mb["name"] works too."""
 
     FIELDS = ("observations", "vectors", "rewards", "values", "ps", "actions", "hiddenState", "returns",
               "trainValid", "costRewards", "costValues", "costReturns")
+
+    def __init__(self, **fields):
+        for k in self.FIELDS:
+            setattr(self, k, fields[k])
+
+    def __getitem__(self, name):
+        return getattr(self, name)
+
+    def keys(self):
+        return self.FIELDS
 
 
 class DeviceRunner:
@@ -95,7 +166,8 @@ class DeviceRunner:
 
     @torch.no_grad()
     def run(self, weights=None):
-        """Runner.run: returns (BatchValues-like dict of device tensors, OneEpPerformance)."""
+        """Runner.run: returns (BatchValues, OneEpPerformance) -- env-major rows over the device
+        buffers, and the per-env mean of the episode counters."""
         if weights is not None:
             self.model.set_weights(weights)
         env, T = self.env, self.T
@@ -124,24 +196,31 @@ class DeviceRunner:
         return self.batch(), self.performance()
 
     def batch(self):
+        """BatchValues over this rollout's buffers, rows env-major (EnvMajorRows)."""
         T, B, N = self.T, self.env.B, self.env.N
-        rows = lambda x: x.reshape(T * B, N, *x.shape[3:])
-        return {
-            "observations": rows(self.obs[:T]), "vectors": rows(self.vec[:T]), "rewards": rows(self.rewards),
-            "values": rows(self.values), "ps": rows(self.ps), "actions": rows(self.actions),
-            "hiddenState": torch.zeros((), device=self.env.device).expand(T * B, 2, N, NetParameters.NET_SIZE),
-            "returns": rows(self.returns), "trainValid": rows(self.train_valid), "costRewards": rows(self.cost_rewards),
-            "costValues": rows(self.cost_values), "costReturns": rows(self.cost_returns)}
+        rows = lambda x: EnvMajorRows(x, T, B)   # noqa: E731
+        return BatchValues(
+            observations=rows(self.obs[:T]), vectors=rows(self.vec[:T]), rewards=rows(self.rewards),
+            values=rows(self.values), ps=rows(self.ps), actions=rows(self.actions),
+            hiddenState=ZeroRows(T * B, (2, N, NetParameters.NET_SIZE), self.env.device),
+            returns=rows(self.returns), trainValid=rows(self.train_valid), costRewards=rows(self.cost_rewards),
+            costValues=rows(self.cost_values), costReturns=rows(self.cost_returns))
+
+    def performance_per_env(self):
+        """OneEpPerformance's counters of every env (runner.py:66-99), float64 numpy [B] each."""
+        st = self.status
+        per = {
+            "staticCollide": (st == -1).sum(dim=(0, 2)), "humanCollide": (st == -2).sum(dim=(0, 2)),
+            "agentCollide": (st == -3).sum(dim=(0, 2)), "shadowGoals": self.shadow.sum(dim=0),
+            # np.sum over float32 rewards per step, accumulated in a python float (runner.py:95-98)
+            "episodeReward": self.rewards.sum(dim=2).double().sum(dim=0),
+            "episodeCostReward": self.cost_rewards.sum(dim=2).double().sum(dim=0),
+            "totalGoals": self.goals.sum(dim=(0, 2)), "constraintViolations": self.constraints.sum(dim=(0, 2))}
+        return {k: v.double().cpu().numpy() for k, v in per.items()}
 
     def performance(self):
+        """The mean over envs of performance_per_env() (see OneEpPerformance)."""
         p = OneEpPerformance()
-        st = self.status
-        p.staticCollide = int((st == -1).sum())
-        p.humanCollide = int((st == -2).sum())
-        p.agentCollide = int((st == -3).sum())
-        p.shadowGoals = int(self.shadow.sum())
-        p.episodeReward = float(self.rewards.sum())
-        p.episodeCostReward = float(self.cost_rewards.sum())
-        p.totalGoals = float(self.goals.sum())
-        p.constraintViolations = float(self.constraints.sum())
+        for k, v in self.performance_per_env().items():
+            setattr(p, k, float(np.mean(v)))
         return p
