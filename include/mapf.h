@@ -139,6 +139,31 @@ int mapf_step_observe_fused(const mapf_env *env);
 
 int mapf_reset(mapf_env *env, const mapf_reset_spec *spec, void *stream);
 
+/* Obstacle maps generated on the device, then a seeded reset on them (mode 1 of
+ * mapf_reset) -- no host maps, no upload, asynchronous on `stream`.
+ *   MAPF_MAPS_WAREHOUSE: MapfGym()'s map (mapf_gym.py:166 -> generateWarehouse(num_block=
+ *     [lo, hi]), map_generator.py:127-138): per env (one map if shared_map) a length L
+ *     uniform in [lo, hi], breadth int(L / (2/3)), shelves as the reference places them
+ *     (bit-exact for a given L), at the top-left of the H x W stack, the rest obstacles.
+ *     Needs H >= hi, W >= int(hi / (2/3)).
+ *   MAPF_MAPS_RANDOM: random_generator's rule -(rand < p) (map_generator.py:23) over H x W,
+ *     p = density.
+ *   largest = 1: free cells outside the largest 4-connected free component become
+ *     obstacles (H * W <= 8192).
+ * Draws: Philox (key = seed, or config.seed if 0; counters (env id, 10, epoch, k)).
+ * maps_out: optional DEVICE int8 [shared_map ? 1 : B][H][W] copy of the maps. */
+#define MAPF_MAPS_WAREHOUSE 0
+#define MAPF_MAPS_RANDOM 1
+typedef struct mapf_mapgen_spec {
+    int32_t kind;            /* MAPF_MAPS_*                                    */
+    int32_t lo, hi;          /* warehouse length range (EnvParameters.WORLD_SIZE) */
+    int32_t largest;         /* keep the largest 4-connected free component   */
+    float density;           /* random maps: obstacle probability             */
+    uint32_t epoch;          /* draw epoch (e.g. the rollout index)           */
+    uint64_t seed;           /* 0: config.seed                                */
+} mapf_mapgen_spec;
+int mapf_reset_generated(mapf_env *env, const mapf_mapgen_spec *spec, int8_t *maps_out, void *stream);
+
 /* One lockstep step for all B envs: actions are DEVICE int32 [B][N] in 0..4. */
 int mapf_step(mapf_env *env, const int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream);
 

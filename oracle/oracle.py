@@ -73,6 +73,9 @@ def lib():
         L.oc_get_fix_counts.argtypes = [P, P]
         L.oc_evict_order.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P]
         L.oc_evict_order.restype = ctypes.c_int
+        L.oc_gen_map.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32,
+                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, P]
+        L.oc_gen_map.restype = ctypes.c_int
         L.oc_py_hash_pair.argtypes = [ctypes.c_int64, ctypes.c_int64]
         L.oc_py_hash_pair.restype = ctypes.c_uint64
         L.oc_random_actions.argtypes = [P, P]
@@ -235,6 +238,14 @@ def evict_order(pairs, restricted):
     out = np.zeros(8, np.int32)
     n = lib().oc_evict_order(_p(pr), len(pr), _p(rj), _p(rb), len(rs), _p(out))
     return out[:n].tolist()
+
+
+def gen_map(kind, H, W, env_id, epoch=0, seed=1234, lo=10, hi=40, density=0.3):
+    """The device map generators (mapf_reset_generated) restated: kind 0 warehouse of a Philox
+    length in [lo, hi] padded into H x W (returns (map, L)); kind 1 random -(rand < p) (map, 0)."""
+    out = np.zeros((H, W), np.int8)
+    L = lib().oc_gen_map(kind, lo, hi, density, epoch, seed, env_id, H, W, _p(out))
+    return out, L
 
 
 def py_hash_pair(a, b):

@@ -51,6 +51,7 @@ struct mapf_env {
     int pending = -1;        // slot whose search work has not been launched yet
     bool ready = false;
     std::vector<void *> allocs;
+    int8_t *maps8 = nullptr;  // [nmaps][H][W] int8 maps on the device (uploaded or generated)
     template <class T>
     int alloc(T *&p, size_t n) {
         void *q = nullptr;
@@ -149,6 +150,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(d.bfs_list, 3 * BN);
     uint8_t *smask = nullptr;
     rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
+    rc |= e->alloc(e->maps8, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
     if (rc) {
         std::string m = g_err;
@@ -181,6 +183,20 @@ int mapf_step_observe_fused(const mapf_env *e) { return e && step_observe_fusabl
 static bool rollout_random_fused(const mapf_env *e) { return e && rollout_random_fusable(e->d); }
 int mapf_rollout_random_fused(const mapf_env *e) { return rollout_random_fused(e) ? 1 : 0; }
 
+// the searches that end every reset: first human paths + every agent's BFS map, then each
+// human's next path
+static int reset_searches(mapf_env *e, hipStream_t s) {
+    const DevEnv &d = e->d;
+    launch_search(d, 0, 1, s);     // first human paths (buffer 0) + every agent's BFS map
+    launch_plan(d, 1, s);          // promote them, plan each human's next path
+    launch_search(d, 0, 2, s);     // ... and search it (buffer 1)
+    HIPCHK(hipGetLastError());
+    e->parity = 1;
+    e->pending = -1;
+    e->ready = true;
+    return MAPF_OK;
+}
+
 int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     if (!e || !spec || !spec->maps) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
@@ -192,35 +208,10 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     if (spec->mode == 1 && d.human_mode == 2) return fail(MAPF_EINVAL, "seeded reset needs human_mode 0 or 1");
     if (spec->mode == 1 && spec->seed) d.seed = spec->seed;
 
-    // padded obstacle bitmaps
-    std::vector<uint32_t> bits(nmaps * d.Hp * d.WW, 0u);
-    for (size_t m = 0; m < nmaps; ++m) {
-        uint32_t *mb = bits.data() + m * d.Hp * d.WW;
-        for (int r = 0; r < d.Hp; ++r)
-            for (int c = 0; c < d.WW * 32; ++c) {
-                const int mr = r - d.P, mc = c - d.P;
-                bool ob;
-                if (mr < 0 || mr >= H || mc < 0 || mc >= W) ob = true;
-                else {
-                    const int8_t v = spec->maps[m * H * W + mr * W + mc];
-                    if (v != 0 && v != -1) return fail(MAPF_EINVAL, "map values must be 0 (free) or -1 (obstacle)");
-                    ob = v == -1;
-                }
-                if (ob) mb[r * d.WW + (c >> 5)] |= 1u << (c & 31);
-            }
-    }
-    // static-invalid action mask of every cell (getInvalidActions' first list, mapf_gym.py:349-352)
-    std::vector<uint8_t> smask(nmaps * H * W, 0);
-    for (size_t m = 0; m < nmaps; ++m)
-        for (int r = 0; r < H; ++r)
-            for (int c = 0; c < W; ++c) {
-                uint8_t mk = 0;
-                for (int a = 0; a < 5; ++a) {
-                    const int rr = r + dr(a), cc = c + dc(a);
-                    if (rr < 0 || rr >= H || cc < 0 || cc >= W || spec->maps[m * H * W + rr * W + cc] != 0) mk |= 1u << a;
-                }
-                smask[m * H * W + r * W + c] = mk;
-            }
+    // map values: 0 free / -1 obstacle (the padded bitmaps and static-action masks are built
+    // from them on the device, launch_build_maps)
+    for (size_t k = 0; k < nmaps * (size_t)H * W; ++k)
+        if (spec->maps[k] != 0 && spec->maps[k] != -1) return fail(MAPF_EINVAL, "map values must be 0 (free) or -1 (obstacle)");
     auto free_at = [&](int b, int r, int c) {
         if (r < 0 || r >= H || c < 0 || c >= W) return false;
         const size_t m = d.shared_map ? 0 : (size_t)b;
@@ -280,8 +271,8 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
         }
     }
 
-    HIPCHK(hipMemcpyAsync((void *)d.map_bits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync((void *)d.smask, smask.data(), smask.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(e->maps8, spec->maps, nmaps * (size_t)H * W, hipMemcpyHostToDevice, s));
+    launch_build_maps(d, e->maps8, s);
     HIPCHK(hipMemsetAsync(d.counters, 0, C_NUM * sizeof(uint32_t), s));
     if (spec->mode == 0) {
         HIPCHK(hipMemcpyAsync(d.seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice, s));
@@ -297,15 +288,39 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     } else {
         launch_reset_seeded(d, s);
     }
-    launch_search(d, 0, 1, s);     // first human paths (buffer 0) + every agent's BFS map
-    launch_plan(d, 1, s);          // promote them, plan each human's next path
-    launch_search(d, 0, 2, s);     // ... and search it (buffer 1)
-    HIPCHK(hipGetLastError());
+    const int rc = reset_searches(e, s);
+    if (rc != MAPF_OK) return rc;
     HIPCHK(hipStreamSynchronize(s));   // host staging buffers die at return
-    e->parity = 1;
-    e->pending = -1;
-    e->ready = true;
     return MAPF_OK;
+}
+
+int mapf_reset_generated(mapf_env *e, const mapf_mapgen_spec *spec, int8_t *maps_out, void *stream) {
+    if (!e || !spec) return fail(MAPF_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    DevEnv &d = e->d;
+    if (d.human_mode == 2) return fail(MAPF_EINVAL, "generated maps need human_mode 0 or 1 (seeded reset)");
+    MapGen g{spec->kind, spec->lo, spec->hi, spec->largest ? 1 : 0, spec->density, spec->epoch,
+             spec->seed ? spec->seed : d.seed};
+    if (spec->kind == MAPF_MAPS_WAREHOUSE) {
+        if (spec->lo < 3 || spec->hi < spec->lo) return fail(MAPF_EINVAL, "warehouse length range [lo, hi] invalid");
+        const int breadth = (int)((double)spec->hi / (2.0 / 3.0));
+        if (d.H < spec->hi || d.W < breadth) return fail(MAPF_EINVAL, "the H x W stack is smaller than the longest warehouse");
+    } else if (spec->kind == MAPF_MAPS_RANDOM) {
+        if (!(spec->density >= 0.f && spec->density <= 1.f)) return fail(MAPF_EINVAL, "density must be in [0, 1]");
+    } else {
+        return fail(MAPF_EINVAL, "unknown map kind");
+    }
+    if (spec->largest && d.H * d.W > LC_MAX_CELLS) return fail(MAPF_EINVAL, "largest component: at most 8192 cells");
+    if (spec->seed) d.seed = spec->seed;
+    const size_t nmaps = d.shared_map ? 1 : (size_t)d.B;
+    launch_mapgen(d, g, e->maps8, s);
+    if (maps_out)
+        HIPCHK(hipMemcpyAsync(maps_out, e->maps8, nmaps * (size_t)d.H * d.W, hipMemcpyDeviceToDevice, s));
+    launch_build_maps(d, e->maps8, s);
+    HIPCHK(hipMemsetAsync(d.counters, 0, C_NUM * sizeof(uint32_t), s));
+    launch_reset_seeded(d, s);
+    return reset_searches(e, s);       // asynchronous: nothing on the host to keep alive
 }
 
 static int step_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, uint32_t flags, void *stream) {

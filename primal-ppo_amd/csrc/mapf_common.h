@@ -31,7 +31,7 @@ __host__ __device__ constexpr int opp(int a) { return a == 0 ? 0 : (a == 1 ? 3 :
 
 // Philox purposes (shared spec with oracle/mapf_oracle.c).
 enum : uint32_t { P_ENTRANCE = 1, P_HGOAL0 = 2, P_START = 3, P_GOAL0 = 4, P_GOAL = 5,
-                  P_HGOAL = 6, P_FIX = 7, P_ACT = 8, P_SAMPLE = 9 };
+                  P_HGOAL = 6, P_FIX = 7, P_ACT = 8, P_SAMPLE = 9, P_MAPGEN = 10 };
 
 // counters[] slots
 enum : int { C_BAD_ACTION = 0, C_FIX_BOUND = 1, C_EMPTY_VIABLE = 2, C_FREECELL = 3,

@@ -39,6 +39,18 @@ void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, 
 bool rollout_random_fusable(const DevEnv &e);
 bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                            int slots, hipStream_t s);
+// obstacle maps on the device (mapf_maps.hip): kind 0 warehouse (length in [lo, hi]), 1 random
+// density p; largest: keep only the largest 4-connected free component (H * W <= LC_MAX_CELLS)
+struct MapGen {
+    int kind, lo, hi, largest;
+    float density;
+    uint32_t epoch;
+    uint64_t seed;
+};
+constexpr int LC_MAX_CELLS = 8192;
+void launch_mapgen(const DevEnv &e, const MapGen &g, int8_t *maps, hipStream_t s);
+// the padded obstacle bitmaps and static-action masks from int8 maps [nmaps][H][W] on the device
+void launch_build_maps(const DevEnv &e, const int8_t *maps, hipStream_t s);
 void launch_reset_fixed(const DevEnv &e, hipStream_t s);
 void launch_reset_seeded(const DevEnv &e, hipStream_t s);
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,

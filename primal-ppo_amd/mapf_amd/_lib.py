@@ -24,6 +24,15 @@ class ResetSpec(ctypes.Structure):
                 ("seed", ctypes.c_uint64)]
 
 
+class MapGenSpec(ctypes.Structure):
+    """include/mapf.h: mapf_mapgen_spec."""
+    _fields_ = [("kind", I32), ("lo", I32), ("hi", I32), ("largest", I32), ("density", ctypes.c_float),
+                ("epoch", U32), ("seed", ctypes.c_uint64)]
+
+
+MAPS_WAREHOUSE, MAPS_RANDOM = 0, 1
+
+
 class StepOut(ctypes.Structure):
     _fields_ = [(n, P) for n in ("status", "reward", "shadow_goals", "cost", "train_valid", "actions_fixed",
                                  "goals_reached", "constraints", "reward_total")]
@@ -42,6 +51,7 @@ SIGNATURES = {
     "mapf_path_capacity": (ctypes.c_int, [P]),
     "mapf_step_observe_fused": (ctypes.c_int, [P]),
     "mapf_reset": (ctypes.c_int, [P, ctypes.POINTER(ResetSpec), P]),
+    "mapf_reset_generated": (ctypes.c_int, [P, ctypes.POINTER(MapGenSpec), P, P]),
     "mapf_step": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_step_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), U32, P]),
     "mapf_observe": (ctypes.c_int, [P, P, P, P]),

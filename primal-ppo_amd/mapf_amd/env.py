@@ -156,6 +156,30 @@ class BatchedMapfGym:
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().mapf_reset(self.h, ctypes.byref(spec), _stream(self.device)))
 
+    def reset_generated(self, kind="warehouse", lo=None, hi=None, density=0.3, largest=False, epoch=0, seed=0,
+                        return_maps=False):
+        """MapfGym() on maps generated on the device (mapf_reset_generated): kind "warehouse"
+        draws each env's generateWarehouse length in [lo, hi] (default EnvParameters.WORLD_SIZE,
+        mapf_gym.py:166; the H x W stack must hold the longest), "random" fills H x W with
+        -(rand < density); largest keeps the largest 4-connected free component.  Then the
+        seeded reset (agents, goals, human) as reset_seeded.  Asynchronous; return_maps gives
+        the int8 maps as a device tensor [shared_map ? 1 : B, H, W]."""
+        from .config import EnvParameters
+        spec = _lib.MapGenSpec()
+        spec.kind = {"warehouse": _lib.MAPS_WAREHOUSE, "random": _lib.MAPS_RANDOM}[kind]
+        ws = EnvParameters.WORLD_SIZE
+        spec.lo = ws[0] if lo is None else lo
+        spec.hi = ws[1] if hi is None else hi
+        spec.largest, spec.density, spec.epoch, spec.seed = int(largest), float(density), int(epoch), int(seed)
+        maps = None
+        if return_maps:
+            maps = torch.empty(1 if self.cfg.shared_map else self.B, self.H, self.W, dtype=torch.int8,
+                               device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().mapf_reset_generated(self.h, ctypes.byref(spec), _ptr(maps),
+                                                       _stream(self.device)))
+        return maps
+
     # ----------------------------------------------------------------- step
     def step(self, actions=None, commit=True):
         """One lockstep step (runner.py:64-100 order).  actions: int32 [B, N] on device.

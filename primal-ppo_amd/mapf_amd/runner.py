@@ -30,6 +30,19 @@ from .config import EnvParameters, NetParameters, TrainingParameters
 from .env import BatchedMapfGym, gae
 
 
+class DeviceMaps:
+    """new_maps for DeviceRunner that never leaves the GPU: every rollout re-generates every
+    env's map on the device (env.reset_generated, epoch = rollout index) -- by default
+    MapfGym()'s random-length warehouse (mapf_gym.py:166, map_generator.py:127-138) --
+    then the seeded reset.  No host maps, no upload."""
+
+    def __init__(self, kind="warehouse", lo=None, hi=None, density=0.3, largest=False):
+        self.kind, self.lo, self.hi, self.density, self.largest = kind, lo, hi, density, largest
+
+    def reset(self, env, rollout, seed):
+        env.reset_generated(self.kind, self.lo, self.hi, self.density, self.largest, epoch=rollout, seed=seed)
+
+
 def reference_maps(env: BatchedMapfGym, world_size=None, seed=0):
     """new_maps for DeviceRunner: per rollout, every env gets its own MapfGym() warehouse
     (random length in EnvParameters.WORLD_SIZE) in the padded [B, Lmax, Wmax] stack the
@@ -132,10 +145,11 @@ class BatchValues:
 
 
 class DeviceRunner:
-    """new_maps: callable(rollout index) -> maps for env.reset_seeded at the start of every
-    run(), i.e. Runner.run's `env = MapfGym()` (runner.py:30: a NEW random-size warehouse
-    and new agents/human every rollout) -- e.g. reference_maps(env) below.  None: the
-    envs continue from where the previous rollout left them (lifelong)."""
+    """new_maps: DeviceMaps() (maps generated on the GPU) or a callable(rollout index) ->
+    host maps for env.reset_seeded, at the start of every run(), i.e. Runner.run's
+    `env = MapfGym()` (runner.py:30: a NEW random-size warehouse and new agents/human
+    every rollout) -- e.g. reference_maps(env).  None: the envs continue from where the
+    previous rollout left them (lifelong)."""
 
     def __init__(self, env: BatchedMapfGym, model, n_steps=None, seed=0, new_maps=None):
         self.env = env
@@ -171,7 +185,9 @@ class DeviceRunner:
         if weights is not None:
             self.model.set_weights(weights)
         env, T = self.env, self.T
-        if self.new_maps is not None:        # runner.py:30 -- a fresh MapfGym() per rollout
+        if isinstance(self.new_maps, DeviceMaps):   # runner.py:30 -- a fresh MapfGym() per rollout
+            self.new_maps.reset(env, self.rollouts, (self.seed << 20) + self.rollouts + 1)
+        elif self.new_maps is not None:
             env.reset_seeded(self.new_maps(self.rollouts), seed=(self.seed << 20) + self.rollouts + 1)
         env.observe(self.obs[0], self.vec[0])
         for t in range(T):

@@ -516,6 +516,17 @@ def g6_episodes():
     np.savez_compressed(os.path.join(folder, "expected.npz"), **out)
 
 
+def g7_warehouses():
+    """generateWarehouse(length=L) (map_generator.py:127-138) for every L of WORLD_SIZE
+    (10..40), the map MapfGym() builds once L is drawn (mapf_gym.py:166)."""
+    maps = {}
+    for L in range(10, 41):
+        w = mapgen.generateWarehouse(num_block=[-1, -1], length=L)
+        maps[f"L{L}"] = w.astype(np.int8)
+    np.savez_compressed(os.path.join(OUT, "g7_warehouses.npz"), **maps)
+    print("g7_warehouses:", {k: v.shape for k, v in maps.items()})
+
+
 def g2_evict():
     """One-step scenarios whose fixActions evicts two agents with one pick
     (mapf_gym.py:588-596): the eviction order is the iteration order of a
@@ -525,6 +536,9 @@ def g2_evict():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["g7"]:
+        g7_warehouses()
+        sys.exit(0)
     if sys.argv[1:] == ["g2_evict"]:
         g2_evict()
         sys.exit(0)
@@ -547,6 +561,7 @@ if __name__ == "__main__":
     run_episode("g1_fixedpath", warehouse(12, 12), 6, 9, 6, 150, 17, human_seq=12, use_da=True, use_hp=True)
     g2_fuzz(3000, 21)
     g2_evict()
+    g7_warehouses()
     g3_search(31)
     g4_gae()
     g6_episodes()

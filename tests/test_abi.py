@@ -32,15 +32,17 @@ def test_struct_layout_matches_c(tmp_path):
     from mapf_amd.config import MapfConfig
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mapf.h"\n'
-                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mapf_config),'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mapf_config),'
                    ' offsetof(mapf_config, seed), offsetof(mapf_config, goal_reward), sizeof(mapf_reset_spec),'
-                   ' offsetof(mapf_reset_spec, seed), sizeof(mapf_step_out), sizeof(mapf_state)); return 0;}\n')
+                   ' offsetof(mapf_reset_spec, seed), sizeof(mapf_step_out), sizeof(mapf_state), sizeof(mapf_mapgen_spec),'
+                   ' offsetof(mapf_mapgen_spec, density), offsetof(mapf_mapgen_spec, seed)); return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     want = [ctypes.sizeof(MapfConfig), MapfConfig.seed.offset, MapfConfig.goal_reward.offset,
             ctypes.sizeof(_lib.ResetSpec), _lib.ResetSpec.seed.offset, ctypes.sizeof(_lib.StepOut),
-            ctypes.sizeof(_lib.State)]
+            ctypes.sizeof(_lib.State), ctypes.sizeof(_lib.MapGenSpec), _lib.MapGenSpec.density.offset,
+            _lib.MapGenSpec.seed.offset]
     assert got == want
 
 
