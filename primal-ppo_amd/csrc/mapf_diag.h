@@ -1,0 +1,47 @@
+// primal-ppo_amd/csrc/mapf_diag.h -- profiling hooks of the diagnostic build.
+//
+// The product build (make) compiles every hook below to nothing.  `make stamps`
+// (-DMAPF_STAMPS) builds ../lib/libmapf_stamps.so, whose kernels record phase
+// cycles per wave and a per-workgroup timeline (tools/stamps.py, tools/timeline.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mapf {
+
+// In-kernel phase stamps (diagnostic build only, -DMAPF_STAMPS): lane 0 of
+// every wave adds the s_memtime delta of each phase into prof[k]; prof[15]
+// counts the waves.  The product build compiles them out.
+__device__ inline uint64_t stamp_now() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#ifdef MAPF_STAMPS
+// per-wave phase deltas kept in registers, one plain store per phase at the end
+// (prof[wave * 8 + k]; no atomics, so the stamps do not contend)
+#define STAMP_BEGIN() uint64_t _stamp_prev = stamp_now(); uint64_t _stamp_d[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define STAMP(k) do { __builtin_amdgcn_sched_barrier(0); const uint64_t _t = stamp_now(); \
+    _stamp_d[k] += _t - _stamp_prev; _stamp_prev = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
+#define STAMP_END() do { if ((threadIdx.x & 63) == 0) { \
+    const size_t _w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; \
+    if (_w < 65536) { for (int _k = 0; _k < 7; ++_k) e.prof[_w * 8 + _k] = _stamp_d[_k]; e.prof[_w * 8 + 7] = 1; } } } while (0)
+// block timeline (fused kernel): thread 0 of block k writes the constant-rate
+// (100 MHz) realtime counter of event t to prof[PROF_TL + k * 8 + t]; slot 6 =
+// HW_ID, slot 7 = XCC_ID of the block's CU.
+#define TL_STAMP(t) do { if (threadIdx.x == 0 && blockIdx.x < PROF_TL_BLOCKS) { uint64_t _r; \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_r)::"memory"); \
+    e.prof[PROF_TL + (size_t)blockIdx.x * 8 + (t)] = _r; } } while (0)
+#define TL_HWID() do { if (threadIdx.x == 0 && blockIdx.x < PROF_TL_BLOCKS) { uint32_t _h, _x; \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_h)); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_x)); \
+    e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 6] = _h; e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 7] = _x; } } while (0)
+#else
+#define TL_STAMP(t) do { } while (0)
+#define TL_HWID() do { } while (0)
+#define STAMP_BEGIN() do { } while (0)
+#define STAMP(k) do { } while (0)
+#define STAMP_END() do { } while (0)
+#endif
+
+}  // namespace mapf

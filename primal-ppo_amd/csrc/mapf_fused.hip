@@ -81,12 +81,8 @@ __global__ __launch_bounds__(256) void step_observe_kernel(DevEnv e, int32_t *__
     }
     const uint32_t mreg = obs_map_word(e, b0, nenv, regmap ? (int)(threadIdx.x & 63) : (int)threadIdx.x);
     PairsDeferred dfr;
-#ifdef MAPF_DIAG_NOSTEP   // timing diagnostic only (make diag): observe the pre-step state, no step
-    obs_load_agents(e, L, b0, nenv);
-#else
     step_pairs_env<NP, true>(e, actions, out, flags, slot, blk * 256 + (int)threadIdx.x, L, b0,
                              RegMap{mreg, regmap}, dfr);
-#endif
     TL_STAMP(1);
     if (per_wave) {
         const int le = (int)(threadIdx.x >> 6);

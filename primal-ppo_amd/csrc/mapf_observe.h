@@ -178,9 +178,6 @@ __device__ inline void obs_zero_band_store(const DevEnv &e, float *__restrict__ 
                                            size_t nt) {
     int z0, z1;
     if (!obs_zero_band(e, z0, z1)) return;
-#ifdef MAPF_DIAG_NOSTORE   // timing diagnostic only: no observation stores
-    if (k0 != 0x7FFFFFFF) return;
-#endif
     const size_t CFF = (size_t)e.C * e.F * e.F;
     float4 *o4 = reinterpret_cast<float4 *>(obs);
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -249,7 +246,6 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     const int E = G.nenv;
 
     // ---- phase 1: worldWithAgents as a padded bitmap per env + agent index grid ----
-#ifndef MAPF_DIAG_NOOBS123   // timing diagnostic only: phases 1-3 compiled out (the stream stays zero)
     const int HW = e.H * e.W;
     for (int k = tid; k < K; k += nt) {
         const int le = G.le0 + k / N;
@@ -383,11 +379,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     obs_sync(G);
     TL_STAMP(4);
 
-#endif
     // ---- phase 4: bit-stream -> float stores ----
-#ifdef MAPF_DIAG_NOSTORE   // timing diagnostic only: no observation stores
-    if (stream[0] != 0x12345678u) return;
-#endif
     const size_t total = (size_t)K * CFF;
     float *dst = obs + (size_t)b0 * N * CFF;
     if (G.wave && L.lut && !skip_band && ((K * CFF) & 3) == 0) {
@@ -442,12 +434,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
                 const uint32_t nib = (stream[bitpos >> 5] >> (bitpos & 31)) & 15u;
                 const float4 f = make_float4((float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u),
                                              (float)((nib >> 3) & 1u));
-#ifdef MAPF_NT_STORES   // store-policy experiment (make ntstores)
-                typedef float v4f __attribute__((ext_vector_type(4)));
-                __builtin_nontemporal_store(v4f{f.x, f.y, f.z, f.w}, reinterpret_cast<v4f *>(&d4[q]));
-#else
                 d4[q] = f;
-#endif
             }
             off += step;
             if (off >= CFF) off -= CFF;

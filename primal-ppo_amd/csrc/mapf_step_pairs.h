@@ -214,11 +214,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const int la = RES ? rs->la : (vi ? (int)e.last_act[ai] : -1);
     int a_i, a_j;
     if (flags & 2u) {                       // random policy: one env-uniform Philox draw for all N <= 8 agents
-#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 1)    // timing diagnostic only
-        const u32x4 o = {clock * 0x9E3779B9u + env_id, clock ^ env_id, clock + 7u, env_id * 3u};
-#else
         const u32x4 o = philox(env_id, P_ACT, clock, 0u, e.seed);
-#endif
         a_i = random_action(o, i);
         a_j = random_action(o, j);
         if (vi && head) actions[ai] = a_i;
@@ -343,11 +339,7 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     // two-agent eviction (mapf_pyset.h), empty viable set -> stay, deadlock after
     // fix_draws(N) draws -> unplaced agents stay, blocked movers revert.
     int fixed = a_i;
-#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 2)    // timing diagnostic only
-    const uint32_t need = 0;
-#else
     const uint32_t need = agents_of(eballot(head && vi && (st == -1 || st == -2 || st == -3)));
-#endif
     if (need) {
         const int st_j = (int)shfl32((uint32_t)st, base + j * NP);
         int asg_i = (vi && st == 1) ? a_i : -1;
@@ -460,10 +452,6 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t np = vi ? pack(nr, nc) : 0xFFFFFFFFu;
     const bool reached = vi && e.lifelong && np == gi;
     uint32_t ng = gi;
-#if defined(MAPF_DIAG_SKIP) && (MAPF_DIAG_SKIP & 4)    // timing diagnostic only
-    if (true) {
-    } else
-#endif
     if (gmode == 0) {
         if (reached && head) {
             int cur = e.seq_cur[ai];
