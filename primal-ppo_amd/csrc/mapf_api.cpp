@@ -52,6 +52,12 @@ struct mapf_env {
     bool ready = false;
     std::vector<void *> allocs;
     int8_t *maps8 = nullptr;  // [nmaps][H][W] int8 maps on the device (uploaded or generated)
+    // second stream for a search that runs beside the observe launch (fork/join inside
+    // one API call, so the caller's stream -- and a hipGraph capture of it -- sees one
+    // sequence); created on first use
+    hipStream_t aux = nullptr;
+    bool serial_search = false;   // MAPF_SERIAL_SEARCH=1: search, then observe, one stream (A/B timing)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     template <class T>
     int alloc(T *&p, size_t n) {
         void *q = nullptr;
@@ -116,6 +122,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }
     if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
     if (const char *v = std::getenv("MAPF_AGENT_LANES")) d.force_agent_lanes = std::atoi(v) != 0;
+    if (const char *v = std::getenv("MAPF_SERIAL_SEARCH")) e->serial_search = std::atoi(v) != 0;
     if (d.obs_envs > d.B) d.obs_envs = d.B;
 
     // fp64 lookup table, computed exactly like the reference (numpy sqrt)
@@ -173,6 +180,9 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
 int mapf_destroy(mapf_env *e) {
     if (!e) return MAPF_OK;
     (void)hipSetDevice(e->device);
+    if (e->aux) (void)hipStreamDestroy(e->aux);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (void *p : e->allocs) (void)hipFree(p);
     delete e;
     return MAPF_OK;
@@ -365,6 +375,28 @@ int mapf_step_random(mapf_env *e, int32_t *actions_out, const mapf_step_out *out
     return step_impl(e, actions_out, out, (flags & MAPF_STEP_COMMIT) | 2u, stream);
 }
 
+// The pending search (the last step's BFS maps and human paths) beside the observe launch:
+// fork it onto e->aux, observe on s, join.  Nothing the observation reads is written by the
+// search except the listed agents' BFS maps (C = 7), whose channel is rewritten after the join.
+static int observe_with_search(mapf_env *e, float *obs, float *vec, hipStream_t s) {
+    if (!e->aux) {
+        HIPCHK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+    const int parity = e->pending;
+    e->pending = -1;
+    HIPCHK(hipEventRecord(e->ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+    launch_search(e->d, parity, 0, e->aux);
+    HIPCHK(hipEventRecord(e->ev_join, e->aux));
+    launch_observe(e->d, obs, vec, 0, parity, s);
+    HIPCHK(hipStreamWaitEvent(s, e->ev_join, 0));
+    if (e->d.C >= 7 && e->d.keep_bfs) launch_bfs_fixup(e->d, parity, obs, s);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
 int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
     if (!e || !obs || !vec) return fail(MAPF_EINVAL, "null argument");
     if (!e->ready) return fail(MAPF_ESTATE, "mapf_observe before mapf_reset");
@@ -372,7 +404,8 @@ int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     int nsearch = 0, parity = 0;
     if (e->pending >= 0) {
-        if (e->d.C >= 7 || !observe_hosts_search(e->d)) {   // BFS channel needs the maps / wide grids: search first
+        if (!observe_hosts_search(e->d) || e->d.C >= 7) {   // wide grids / BFS channel: search beside the launch
+            if (!e->serial_search) return observe_with_search(e, obs, vec, s);
             if (int rc = flush_search(e, s)) return rc;
         } else {                       // search work rides in the observe launch
             nsearch = e->d.search_blocks;

@@ -29,6 +29,8 @@ void launch_plan(const DevEnv &e, int promote, hipStream_t s);
 // observations; the first nsearch workgroups run the search work of `parity`
 void launch_observe(const DevEnv &e, float *obs, float *vec, int nsearch, int parity, hipStream_t s);
 bool observe_hosts_search(const DevEnv &e);
+// after a concurrent search: rewrite the BFS channel of the agents in bfs_list[parity]
+void launch_bfs_fixup(const DevEnv &e, int parity, float *obs, hipStream_t s);
 // committed step + observations in one launch (mapf_fused.hip); the first nsearch
 // workgroups run the search work of list slot sslot (the previous step's)
 bool step_observe_fusable(const DevEnv &e);

@@ -46,6 +46,39 @@ __global__ __launch_bounds__(256) void observe_kernel(DevEnv e, float *__restric
     TL_STAMP(3);
 }
 
+// BFS channel (ch 6, C = 7) of the agents whose map the step's search rewrote
+// (bfs_list[parity]).  The search runs concurrently with the observe launch
+// (mapf_observe forks it onto a second stream), so the observe launch read
+// those agents' maps while they were being written; after the join this
+// launch rewrites exactly their channel 6 from the new maps -- the same
+// expression as obs_emit's.  One wave per listed agent, grid-strided.
+__global__ __launch_bounds__(256) void bfs_fixup_kernel(DevEnv e, int parity, float *__restrict__ obs) {
+    const uint32_t n = e.counters[C_BFS_COUNT + parity];
+    const int lane = lane_id(), F = e.F, FF = F * F, half = F / 2;
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); item < n; item += nw) {
+        const uint32_t ai = e.bfs_list[(size_t)parity * e.B * e.N + item];
+        const uint32_t p = e.pos[ai];
+        const int pr = prow(p), pc = pcol(p);
+        const int16_t *bm = e.bfs + (size_t)ai * e.H * e.W;
+        const int own = bm[pr * e.W + pc];
+        float *o = obs + (size_t)ai * e.C * FF + 6 * FF;
+        for (int q = lane; q < FF; q += 64) {
+            const int rr = pr - half + q / F, cc = pc - half + q % F;
+            float v = 0.f;
+            if (own >= 0 && rr >= 0 && rr < e.H && cc >= 0 && cc < e.W) {
+                const int d = bm[rr * e.W + cc];
+                if (d >= 0 && d < own) v = 1.f;
+            }
+            o[q] = v;
+        }
+    }
+}
+
+void launch_bfs_fixup(const DevEnv &e, int parity, float *obs, hipStream_t s) {
+    hipLaunchKernelGGL(bfs_fixup_kernel, dim3(64), dim3(256), 0, s, e, parity, obs);
+}
+
 size_t observe_lds(const DevEnv &e) { return ((obs_lds_bytes(e, e.obs_envs) + 15) & ~(size_t)15) + 256; }   // + nibble table
 
 bool observe_hosts_search(const DevEnv &e) { return e.W <= 32 && e.H <= 64; }
