@@ -43,9 +43,16 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
+def bfs_channel_bytes(C, F):
+    """The BFS channel (C = 7): the agent's bfsMap over its FOV window (F*F int16) and at its
+    own cell, read per agent-step -- bytes SURVEY.md §8(d)'s formula leaves out."""
+    return F * F * 2 + 2 if C >= 7 else 0
+
+
 def observe_bytes_per_agent(C, F, H, W, N):
-    """C*F^2*4 + 16 (obs + vec writes) + (ceil(H*W/8) + 8N + 8)/N (reads)."""
-    return C * F * F * 4 + 16 + (-(-H * W // 8) + 8 * N + 8) / N
+    """C*F^2*4 + 16 (obs + vec writes) + (ceil(H*W/8) + 8N + 8)/N (reads),
+    + the BFS channel's map reads."""
+    return C * F * F * 4 + 16 + (-(-H * W // 8) + 8 * N + 8) / N + bfs_channel_bytes(C, F)
 
 
 def fused_bytes_per_agent(C, F, H, W, N):
@@ -53,8 +60,8 @@ def fused_bytes_per_agent(C, F, H, W, N):
     obs + vec writes (C*F^2*4 + 16); agent state read (cell, goal, last action: 9)
     and written (9); random action (4) and step outputs (status 1, reward 4, cost 4,
     train_valid 20, fixed 4, goal flag 4, constraint 4, total reward 4: 45);
-    per env: obstacle bits ceil(H*W/8) + clock/human/path state 64."""
-    return C * F * F * 4 + 16 + 9 + 9 + 4 + 45 + (-(-H * W // 8) + 64) / N
+    per env: obstacle bits ceil(H*W/8) + clock/human/path state 64; the BFS channel's map reads."""
+    return C * F * F * 4 + 16 + 9 + 9 + 4 + 45 + (-(-H * W // 8) + 64) / N + bfs_channel_bytes(C, F)
 
 
 def _oracle_rate(O, cfg, world, B, seconds, threads):
@@ -277,11 +284,14 @@ def main():
         rollout(T)                   # every launch of the roofline kernel runs T steps (rocprof averages agree)
     torch.cuda.synchronize()
 
-    # fused/split: the K timed steps are replays of a hipGraph holding G consecutive
-    # steps (every kernel of every step runs; the graph only removes host launch cost)
+    # fused: the K timed steps are replays of a hipGraph holding G consecutive steps
+    # (every kernel of every step runs; the graph only removes host launch cost).  Not for
+    # configs that step and observe in separate launches (N > 8 or C = 7): their search
+    # work runs on a second stream joined two steps later, which a capture cannot hold
+    # open, and at 30-200 us per step the host's launch cost is hidden anyway.
     G = args.graph_steps
     graph = None
-    if path != "rollout" and G > 0:
+    if path != "rollout" and G > 0 and env.fused:
         assert G % 3 == 0, "--graph-steps must be a multiple of 3"
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
@@ -375,7 +385,7 @@ def main():
         if env.rollout_fused:
             if roll is None:
                 paths["rollout_inplace"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
-                TS = T
+                TS = min(T, max(8, int(25e9 // (B * N * (C * F * F + 4) * 4))))   # <= ~25 GB of slots
                 sl = dict(actions=torch.zeros(TS, B, N, dtype=torch.int32, device=dev),
                           obs=torch.zeros(TS, B, N, C, F, F, device=dev), vec=torch.zeros(TS, B, N, 4, device=dev),
                           out={k: torch.zeros((TS,) + tuple(v.shape), dtype=v.dtype, device=dev)
@@ -395,7 +405,8 @@ def main():
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
         if path == "rollout":
-            kname = "rollout_random_kernel" + ("<true> (nontemporal stores)" if roll else "")
+            kname = ("rollout_random_kernel" if env.rollout_kernel == 1 else "rollout_wide_kernel") + \
+                ("<true> (nontemporal stores)" if roll else "")
             bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, T
         elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one
             kname, bpa, kms, steps_pl = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms, 1

@@ -198,10 +198,13 @@ int mapf_step_observe_random(mapf_env *env, int32_t *actions_out, const mapf_ste
  * observe -> its own search work, so steps overlap other envs' store drains. */
 int mapf_rollout_random(mapf_env *env, int32_t T, int32_t slots, int32_t *actions_out, const mapf_step_out *out,
                         float *obs, float *vec, void *stream);
-/* 1 if mapf_rollout_random runs as one launch for this configuration: N in 5..8
- * with a whole number of float4s per env's observation, one shared map whose
- * padded bitmap fits 64 words (W + 2*(F/2) <= 32, H + 2*(F/2) <= 64), no BFS
- * channel, Human or LoopingHuman, random (MapfGym) goals. */
+/* Which kernel mapf_rollout_random runs for this configuration (0: T per-step
+ * launches).  1: the pair-lane kernel -- N in 5..8 with a whole number of float4s
+ * per env's observation, one shared map whose padded bitmap fits 64 words
+ * (W + 2*(F/2) <= 32, H + 2*(F/2) <= 64), no BFS channel, Human or LoopingHuman,
+ * random (MapfGym) goals.  2: the one-wave-per-env kernel -- every other
+ * configuration whose per-env LDS (map rows, observation bit-stream, BFS image)
+ * fits 64 KiB: up to 64 agents, per-env maps, the BFS channel (c4, c5). */
 int mapf_rollout_random_fused(const mapf_env *env);
 
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the

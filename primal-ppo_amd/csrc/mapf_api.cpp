@@ -55,9 +55,19 @@ struct mapf_env {
     // second stream for a search that runs beside the observe launch (fork/join inside
     // one API call, so the caller's stream -- and a hipGraph capture of it -- sees one
     // sequence); created on first use
-    hipStream_t aux = nullptr;
+    hipStream_t aux = nullptr, aux2 = nullptr;   // aux: BFS maps the observation reads; aux2: deferred work
     bool serial_search = false;   // MAPF_SERIAL_SEARCH=1: search, then observe, one stream (A/B timing)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+    // Deferred joins.  A human's next path is read no earlier than two steps after its
+    // step queued it (mapf_fused.hip), and agent BFS maps only by the BFS channel
+    // (C = 7, joined at once) and mapf_bfs: so the aux-stream search of committed step t
+    // runs beside step t+1 and is joined on the caller's stream before step t+2 -- or
+    // before anything else reads or rewrites the state (join_deferred).
+    long nsteps = 0;                       // committed steps since the reset
+    hipEvent_t ev_def[2] = {nullptr, nullptr};
+    long def_due[2] = {-1, -1};            // join before the step that would make nsteps exceed this
+    int def_next = 0;
+    bool no_defer = false;                 // MAPF_NO_DEFER=1: join every search in its own call (A/B timing)
     template <class T>
     int alloc(T *&p, size_t n) {
         void *q = nullptr;
@@ -123,6 +133,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
     if (const char *v = std::getenv("MAPF_AGENT_LANES")) d.force_agent_lanes = std::atoi(v) != 0;
     if (const char *v = std::getenv("MAPF_SERIAL_SEARCH")) e->serial_search = std::atoi(v) != 0;
+    if (const char *v = std::getenv("MAPF_NO_DEFER")) e->no_defer = std::atoi(v) != 0;
     if (d.obs_envs > d.B) d.obs_envs = d.B;
 
     // fp64 lookup table, computed exactly like the reference (numpy sqrt)
@@ -150,7 +161,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(d.hnext_start, d.B); rc |= e->alloc(d.hnext_goal, d.B);
     rc |= e->alloc(d.hseq, (size_t)d.B * d.HS); rc |= e->alloc(d.hseq_len, d.B); rc |= e->alloc(d.hseq_idx, d.B);
     rc |= e->alloc(d.hreplans, d.B); rc |= e->alloc(d.clock, d.B);
-    if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * d.H * d.W);
+    if (d.keep_bfs) rc |= e->alloc(d.bfs, BN * bfs_cells(d.H, d.W));
     rc |= e->alloc(d.counters, C_NUM);
     rc |= e->alloc(d.prof, PROF_WORDS);
     rc |= e->alloc(d.replan_list, 3 * (size_t)d.B);
@@ -180,9 +191,19 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
 int mapf_destroy(mapf_env *e) {
     if (!e) return MAPF_OK;
     (void)hipSetDevice(e->device);
-    if (e->aux) (void)hipStreamDestroy(e->aux);
+    if (e->aux) {
+        (void)hipStreamSynchronize(e->aux);
+        (void)hipStreamDestroy(e->aux);
+    }
+    if (e->aux2) {
+        (void)hipStreamSynchronize(e->aux2);
+        (void)hipStreamDestroy(e->aux2);
+    }
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->ev_join2) (void)hipEventDestroy(e->ev_join2);
+    for (hipEvent_t ev : e->ev_def)
+        if (ev) (void)hipEventDestroy(ev);
     for (void *p : e->allocs) (void)hipFree(p);
     delete e;
     return MAPF_OK;
@@ -190,13 +211,31 @@ int mapf_destroy(mapf_env *e) {
 
 int mapf_path_capacity(const mapf_env *e) { return e ? e->d.Lmax : 0; }
 int mapf_step_observe_fused(const mapf_env *e) { return e && step_observe_fusable(e->d) ? 1 : 0; }
-static bool rollout_random_fused(const mapf_env *e) { return e && rollout_random_fusable(e->d); }
-int mapf_rollout_random_fused(const mapf_env *e) { return rollout_random_fused(e) ? 1 : 0; }
+static bool rollout_random_fused(const mapf_env *e) {
+    return e && (rollout_random_fusable(e->d) || rollout_wide_fusable(e->d));
+}
+int mapf_rollout_random_fused(const mapf_env *e) {
+    if (!e) return 0;
+    return rollout_random_fusable(e->d) ? 1 : (rollout_wide_fusable(e->d) ? 2 : 0);
+}
+
+// s waits for the deferred aux-stream searches: every one (all), or those due before the
+// step about to be launched
+static int join_deferred(mapf_env *e, hipStream_t s, bool all) {
+    for (int k = 0; k < 2; ++k) {
+        if (e->def_due[k] >= 0 && (all || e->nsteps >= e->def_due[k])) {
+            HIPCHK(hipStreamWaitEvent(s, e->ev_def[k], 0));
+            e->def_due[k] = -1;
+        }
+    }
+    return MAPF_OK;
+}
 
 // the searches that end every reset: first human paths + every agent's BFS map, then each
 // human's next path
 static int reset_searches(mapf_env *e, hipStream_t s) {
     const DevEnv &d = e->d;
+    e->nsteps = 0;
     launch_search(d, 0, 1, s);     // first human paths (buffer 0) + every agent's BFS map
     launch_plan(d, 1, s);          // promote them, plan each human's next path
     launch_search(d, 0, 2, s);     // ... and search it (buffer 1)
@@ -211,6 +250,7 @@ int mapf_reset(mapf_env *e, const mapf_reset_spec *spec, void *stream) {
     if (!e || !spec || !spec->maps) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = join_deferred(e, s, true)) return rc;
     DevEnv &d = e->d;
     const int B = d.B, N = d.N, H = d.H, W = d.W;
     const size_t nmaps = d.shared_map ? 1 : (size_t)B;
@@ -308,6 +348,7 @@ int mapf_reset_generated(mapf_env *e, const mapf_mapgen_spec *spec, int8_t *maps
     if (!e || !spec) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = join_deferred(e, s, true)) return rc;
     DevEnv &d = e->d;
     if (d.human_mode == 2) return fail(MAPF_EINVAL, "generated maps need human_mode 0 or 1 (seeded reset)");
     MapGen g{spec->kind, spec->lo, spec->hi, spec->largest ? 1 : 0, spec->density, spec->epoch,
@@ -345,20 +386,24 @@ static int step_impl(mapf_env *e, int32_t *actions, const mapf_step_out *out, ui
         o.constraints = out->constraints; o.reward_total = out->reward_total;
     }
     if (e->pending >= 0) {             // previous step's search work was not observed-through
+        if (int rc = join_deferred(e, s, true)) return rc;
         launch_search(e->d, e->pending, 0, s);
         e->pending = -1;
     }
+    if (int rc = join_deferred(e, s, !(flags & MAPF_STEP_COMMIT))) return rc;
     const int parity = e->parity;
     launch_step(e->d, actions, o, flags, parity, s);
     if (flags & MAPF_STEP_COMMIT) {
         if (e->d.human_mode != 0 || e->d.keep_bfs) e->pending = parity;
         e->parity = (parity + 1) % 3;
+        ++e->nsteps;
     }
     HIPCHK(hipGetLastError());
     return MAPF_OK;
 }
 
 static int flush_search(mapf_env *e, hipStream_t s) {
+    if (int rc = join_deferred(e, s, true)) return rc;
     if (e->pending >= 0) {
         launch_search(e->d, e->pending, 0, s);
         e->pending = -1;
@@ -375,24 +420,51 @@ int mapf_step_random(mapf_env *e, int32_t *actions_out, const mapf_step_out *out
     return step_impl(e, actions_out, out, (flags & MAPF_STEP_COMMIT) | 2u, stream);
 }
 
-// The pending search (the last step's BFS maps and human paths) beside the observe launch:
-// fork it onto e->aux, observe on s, join.  Nothing the observation reads is written by the
-// search except the listed agents' BFS maps (C = 7), whose channel is rewritten after the join.
+// The pending search (the last step's BFS maps and human paths) beside the observe launch,
+// forked off s onto two streams.  Nothing the observation reads is written by the search
+// except the listed agents' BFS maps (C = 7): those are searched on e->aux, joined right
+// after the observe launch, and exactly their BFS channel is then rewritten (bfs_fixup).
+// The rest -- the humans' next paths, and BFS maps without the BFS channel -- runs on
+// e->aux2 and stays there past this call (join_deferred), unless s is being captured into
+// a graph (a capture must join every fork before it ends).
 static int observe_with_search(mapf_env *e, float *obs, float *vec, hipStream_t s) {
     if (!e->aux) {
         HIPCHK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&e->aux2, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_join2, hipEventDisableTiming));
+        for (hipEvent_t &ev : e->ev_def) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cap));
+    const bool defer = !e->no_defer && cap == hipStreamCaptureStatusNone;
+    const bool bfsch = e->d.C >= 7 && e->d.keep_bfs;
     const int parity = e->pending;
     e->pending = -1;
     HIPCHK(hipEventRecord(e->ev_fork, s));
-    HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
-    launch_search(e->d, parity, 0, e->aux);
-    HIPCHK(hipEventRecord(e->ev_join, e->aux));
+    if (bfsch) {
+        HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+        launch_search(e->d, parity, 4, e->aux);                 // the BFS maps the observation reads
+        HIPCHK(hipEventRecord(e->ev_join, e->aux));
+    }
+    HIPCHK(hipStreamWaitEvent(e->aux2, e->ev_fork, 0));
+    launch_search(e->d, parity, bfsch ? 3 : 0, e->aux2);        // human paths (+ BFS maps without the channel)
+    if (defer) {
+        // slot k's previous search was due before an earlier step: joined by now
+        const int k = e->def_next;
+        HIPCHK(hipEventRecord(e->ev_def[k], e->aux2));
+        e->def_due[k] = e->nsteps + 1;
+        e->def_next = k ^ 1;
+    } else {
+        HIPCHK(hipEventRecord(e->ev_join2, e->aux2));
+    }
     launch_observe(e->d, obs, vec, 0, parity, s);
-    HIPCHK(hipStreamWaitEvent(s, e->ev_join, 0));
-    if (e->d.C >= 7 && e->d.keep_bfs) launch_bfs_fixup(e->d, parity, obs, s);
+    if (bfsch) {
+        HIPCHK(hipStreamWaitEvent(s, e->ev_join, 0));
+        launch_bfs_fixup(e->d, parity, obs, s);
+    }
+    if (!defer) HIPCHK(hipStreamWaitEvent(s, e->ev_join2, 0));
     HIPCHK(hipGetLastError());
     return MAPF_OK;
 }
@@ -428,6 +500,8 @@ static int step_observe_impl(mapf_env *e, int32_t *actions, const mapf_step_out 
     }
     HIPCHK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = join_deferred(e, s, true)) return rc;
+    ++e->nsteps;
     StepOut o{};
     if (out) {
         o.status = out->status; o.reward = out->reward; o.shadow_goals = out->shadow_goals; o.cost = out->cost;
@@ -478,7 +552,8 @@ int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_
     if (T == 0) return MAPF_OK;
     if (rollout_random_fused(e)) {
         if (int rc = flush_search(e, s)) return rc;     // the kernel searches inline from here on
-        launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s);
+        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s))
+            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s);
         HIPCHK(hipGetLastError());
         return MAPF_OK;
     }
@@ -522,8 +597,8 @@ int mapf_bfs(mapf_env *e, int16_t *dist, void *stream) {
     if (!e->d.keep_bfs) return fail(MAPF_ESTATE, "keep_bfs is off");
     HIPCHK(hipSetDevice(e->device));
     if (int rc = flush_search(e, (hipStream_t)stream)) return rc;
-    const size_t n = (size_t)e->d.B * e->d.N * e->d.H * e->d.W * sizeof(int16_t);
-    HIPCHK(hipMemcpyAsync(dist, e->d.bfs, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    launch_bfs_export(e->d, dist, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
     return MAPF_OK;
 }
 

@@ -12,7 +12,9 @@
 //                                   the human will switch to at the end of it
 //                                   (precomputed off the critical path)
 //   hlen [B][2], hcur/hstep [B], hpos/hnext/hgoal/hentr [B], hnext_start/hnext_goal [B]
-//   bfs       [B*N*H*W] i16         agent.bfsMap (keep_bfs)
+//   bfs       [B*N][TH][TW][8][8] i16  agent.bfsMap (keep_bfs) in 8x8-cell tiles, one
+//                                   128-B L2 line each (bfs_at); cells past the map's
+//                                   edge inside a tile hold -1
 //   counters  [32] u32              error counters + work-list counts
 //   replan_list [3][B], bfs_list [3][B*N]  per-step work lists, slot = step count mod 3
 #pragma once
@@ -121,6 +123,14 @@ __device__ inline bool in_map(const DevEnv &e, int r, int c) { return r >= 0 && 
 
 __device__ inline const uint32_t *env_map(const DevEnv &e, int b) {
     return e.map_bits + (e.shared_map ? 0 : (size_t)b * e.Hp * e.WW);
+}
+
+// agent.bfsMap tiles: an F x F observation window (the BFS channel, ch 6) touches
+// ~5 lines of 128 B on average (F = 11) where row-major int16 rows touched ~13.
+__host__ __device__ inline int bfs_tw(int W) { return (W + 7) >> 3; }
+__host__ __device__ inline size_t bfs_cells(int H, int W) { return (size_t)((H + 7) >> 3) * bfs_tw(W) * 64; }
+__host__ __device__ inline int bfs_at(int W, int r, int c) {
+    return ((((r >> 3) * bfs_tw(W)) + (c >> 3)) << 6) | ((r & 7) << 3) | (c & 7);
 }
 
 __device__ inline uint32_t *human_path(const DevEnv &e, int b, int buf) {

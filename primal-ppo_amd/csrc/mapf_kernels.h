@@ -22,8 +22,11 @@ bool launch_step_pairs(const DevEnv &e, int32_t *actions, const StepOut &out, ui
                        hipStream_t s);   // N <= 8: one lane per agent pair; false if N > 8
 void launch_random_actions(const DevEnv &e, int32_t *actions, hipStream_t s);
 // humans' next paths (replan_list[parity]) + agent BFS maps (bfs_list[parity]);
-// all = 1: every env's next path and every agent's map, 2: every env's next path
+// all = 1: every env's next path and every agent's map, 2: every env's next path,
+// 3 / 4: the step's human paths / BFS maps only
 void launch_search(const DevEnv &e, int parity, int all, hipStream_t s);
+// agent.bfsMap of every agent, untiled: dist[B*N][H][W] (mapf_bfs)
+void launch_bfs_export(const DevEnv &e, int16_t *dist, hipStream_t s);
 // plan every human's next path from the state (promote: buffer hcur^1 becomes current first)
 void launch_plan(const DevEnv &e, int promote, hipStream_t s);
 // observations; the first nsearch workgroups run the search work of `parity`
@@ -41,6 +44,11 @@ void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, 
 bool rollout_random_fusable(const DevEnv &e);
 bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                            int slots, hipStream_t s);
+// the same for up to 64 agents / per-env maps / the BFS channel: one wave per env
+// (mapf_rollout_wide.hip); used where the pair-lane rollout does not apply
+bool rollout_wide_fusable(const DevEnv &e);
+void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                         int slots, hipStream_t s);
 // obstacle maps on the device (mapf_maps.hip): kind 0 warehouse (length in [lo, hi]), 1 random
 // density p; largest: keep only the largest 4-connected free component (H * W <= LC_MAX_CELLS)
 struct MapGen {

@@ -40,6 +40,7 @@ struct ObsLds {
     int32_t *bfsown;            //   bfsMap window, from column (tc & ~1); [E*N] bfsMap at the agent's cell
     const float4 *lut;          // optional [16] float4: nibble -> its 4 bits as 0.f / 1.f (obs_lut_init)
     int stream_words, rowsz;
+    bool bfs_win;               // BFS channel read through the LDS windows (else straight from HBM per task)
 };
 
 __host__ __device__ inline int obs_stream_words(const DevEnv &e, int E) { return (E * e.N * e.C * e.F * e.F + 31) / 32 + 1; }
@@ -79,6 +80,7 @@ __device__ inline ObsLds obs_layout(const DevEnv &e, int E, char *smem, bool per
     L.bfsown = reinterpret_cast<int32_t *>(L.bfsw + (obs_bfs_windows(e) ? (size_t)E * e.N * e.F * obs_bfs_wd(e) : 0));
     L.idg = reinterpret_cast<uint8_t *>(L.bfsown + (obs_bfs_windows(e) ? E * e.N : 0));
     L.lut = nullptr;
+    L.bfs_win = obs_bfs_windows(e);
     return L;
 }
 
@@ -255,7 +257,8 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         L.idg[le * HW + r * e.W + c] = (uint8_t)(k % N);
     }
     const int half = F / 2;
-    if (BFSCH && obs_bfs_windows(e)) {
+    const size_t bcells = bfs_cells(e.H, e.W);
+    if (BFSCH && L.bfs_win) {
         // the BFS channel's bfsMap windows: every load of the workgroup issued here
         // at once (one HBM latency, not one per FOV-row task), as aligned dwords
         const int WD = obs_bfs_wd(e);
@@ -264,11 +267,11 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             const int k = task / F, y = task - k * F;
             const int rr = min(max(prow(L.spos[kw + k]) - half + y, 0), e.H - 1);
             const int col = min(max(((pcol(L.spos[kw + k]) - half) & ~1) + 2 * w, 0), e.W - 2);
-            const int16_t *bm = e.bfs + ((size_t)b0 * N + k) * HW;
-            L.bfsw[kw * F * WD + idx] = *reinterpret_cast<const uint32_t *>(bm + rr * e.W + col);
+            const int16_t *bm = e.bfs + ((size_t)b0 * N + k) * bcells;
+            L.bfsw[kw * F * WD + idx] = *reinterpret_cast<const uint32_t *>(bm + bfs_at(e.W, rr, col));   // col even
         }
         for (int k = tid; k < K; k += nt)
-            L.bfsown[kw + k] = e.bfs[((size_t)b0 * N + k) * HW + prow(L.spos[kw + k]) * e.W + pcol(L.spos[kw + k])];
+            L.bfsown[kw + k] = e.bfs[((size_t)b0 * N + k) * bcells + bfs_at(e.W, prow(L.spos[kw + k]), pcol(L.spos[kw + k]))];
     }
     obs_sync(G);
 
@@ -309,7 +312,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
                 }
             }
         }
-        if (BFSCH && obs_bfs_windows(e) && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension), from LDS
+        if (BFSCH && L.bfs_win && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension), from LDS
             const int own = L.bfsown[kw + k];
             const uint32_t *win = L.bfsw + ((size_t)kw * F + task) * obs_bfs_wd(e);
             const int c0 = tc & ~1;
@@ -322,25 +325,26 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             if (own < 0) m = 0;
             or_bits(stream, base + 6 * FF, m, F);
         } else if (BFSCH && C >= 7 && e.keep_bfs && rr >= 0 && rr < e.H) {   // ch6 BFS descent (extension)
+            // the row's window straight from the tiled map: aligned dwords from column tc & ~1
+            // (a dword never straddles a tile; columns past the edge read the tile padding's -1
+            // or are masked), all loads issued before any is used
             const size_t ai = (size_t)b0 * N + k;
-            const int16_t *bm = e.bfs + ai * e.H * e.W;
-            const int16_t *row = bm + rr * e.W;
-            const int own = bm[pr * e.W + pc];
-            // the row's loads all issued before any is used (one HBM latency, not F)
-            int16_t v[16];
+            const int16_t *bm = e.bfs + ai * bcells;
+            const int own = bm[bfs_at(e.W, pr, pc)];
+            const int c0 = tc & ~1, cmax = bfs_tw(e.W) * 8 - 2;
+            uint32_t wv[9];
 #pragma unroll
-            for (int x = 0; x < 16; ++x) v[x] = x < F ? row[min(max(tc + x, 0), e.W - 1)] : (int16_t)-1;
+            for (int w = 0; w < 9; ++w)
+                if (2 * w < F + 1)
+                    wv[w] = *reinterpret_cast<const uint32_t *>(bm + bfs_at(e.W, rr, min(max(c0 + 2 * w, 0), cmax)));
             uint32_t m = 0;
 #pragma unroll
             for (int x = 0; x < 16; ++x) {
-                const int cc = tc + x;
-                if (x < F && cc >= 0 && cc < e.W && v[x] >= 0 && v[x] < own) m |= 1u << x;
-            }
-            for (int x = 16; x < F; ++x) {
-                const int cc = tc + x;
-                if (cc < 0 || cc >= e.W) continue;
-                const int w = row[cc];
-                if (w >= 0 && w < own) m |= 1u << x;
+                const int cc = tc + x, wi = cc - c0;
+                if (x < F) {
+                    const int v = (int16_t)(wv[wi >> 1] >> ((wi & 1) * 16));
+                    if (cc >= 0 && cc < e.W && v >= 0 && v < own) m |= 1u << x;
+                }
             }
             if (own < 0) m = 0;
             or_bits(stream, base + 6 * FF, m, F);

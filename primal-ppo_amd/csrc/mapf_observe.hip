@@ -60,14 +60,14 @@ __global__ __launch_bounds__(256) void bfs_fixup_kernel(DevEnv e, int parity, fl
         const uint32_t ai = e.bfs_list[(size_t)parity * e.B * e.N + item];
         const uint32_t p = e.pos[ai];
         const int pr = prow(p), pc = pcol(p);
-        const int16_t *bm = e.bfs + (size_t)ai * e.H * e.W;
-        const int own = bm[pr * e.W + pc];
+        const int16_t *bm = e.bfs + (size_t)ai * bfs_cells(e.H, e.W);
+        const int own = bm[bfs_at(e.W, pr, pc)];
         float *o = obs + (size_t)ai * e.C * FF + 6 * FF;
         for (int q = lane; q < FF; q += 64) {
             const int rr = pr - half + q / F, cc = pc - half + q % F;
             float v = 0.f;
             if (own >= 0 && rr >= 0 && rr < e.H && cc >= 0 && cc < e.W) {
-                const int d = bm[rr * e.W + cc];
+                const int d = bm[bfs_at(e.W, rr, cc)];
                 if (d >= 0 && d < own) v = 1.f;
             }
             o[q] = v;

@@ -1,0 +1,187 @@
+// primal-ppo_amd/csrc/mapf_rollout_wide.hip -- T committed random-policy steps +
+// observations in ONE launch for the configurations the pair-lane rollout kernel
+// (mapf_fused.hip, N in 5..8 on a shared map up to 30 wide) does not cover: up to
+// 64 agents, per-env maps up to 128 x 128, the BFS channel (C = 7) -- BASELINE
+// configs c4 (1024 x 16 per GPU, 40 x 40) and c5 (2048 x 64 per GPU, 80 x 80).
+//
+// runner.py:64-100 with the uniform policy, T times, per env:
+//     step (mapf_step.h: one lane per agent, the whole wave one group)
+//     -> agent.bfsMap of every agent whose goal changed (mapf_gym.py:623-627; the
+//        BFS channel of this step's observation reads them)
+//     -> getAllObservations of the env (mapf_observe.h: LDS bit-stream -> float4)
+//     -> the human's next path, if the step queued one (read two steps later at
+//        the earliest: mapf_fused.hip)
+// One workgroup = one wave = one env for the whole launch.  The split path runs
+// the same work as three launches per step in lockstep over all envs, so every
+// step waits for the slowest env's BFS chain and pays the launch gaps; here a
+// wave searching an 80 x 80 map for ~100 us holds back only its own env while
+// the other waves' observation stores keep HBM busy.
+//
+// State stays in HBM between steps (the step reads and writes it as the per-step
+// kernel does; a wave's own stores are visible to its later loads).  LDS per wave:
+// the nibble table, the env's padded map rows, and one scratch area shared by the
+// observation (bit-stream, occupancy, agent grid) and the search (BFS image).
+#include <cstdlib>
+#include <type_traits>
+
+#include "mapf_observe.h"
+#include "mapf_search.h"
+#include "mapf_step.h"
+
+namespace mapf {
+
+struct WideOut {
+    int32_t *actions;
+    StepOut out;
+    float *obs, *vec;
+    int slots;
+    int xcd_remap;
+};
+
+__host__ __device__ inline size_t wide_a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// observation part of the scratch area: stream | occ | spos | sgoal | shn | shp | shpn | idg
+__host__ __device__ inline size_t wide_obs_bytes(const DevEnv &e) {
+    const size_t words = (size_t)obs_env_stream_words(e) + (size_t)e.Hp * e.WW + 2 * (size_t)e.N + 1 + e.k_predict + 1;
+    return words * 4 + (((size_t)e.H * e.W + 3) & ~(size_t)3);
+}
+
+template <class T, int RW>
+__host__ __device__ inline size_t wide_scratch_bytes(const DevEnv &e) {
+    const size_t o = wide_obs_bytes(e), s = srch::wave_lds<T, RW>(e.H, e.W);
+    return wide_a16(o > s ? o : s);
+}
+
+// nibble table (256 B) | map rows | scratch
+template <class T, int RW>
+__host__ __device__ inline size_t wide_lds_bytes(const DevEnv &e) {
+    return 256 + wide_a16((size_t)e.Hp * e.WW * 4) + wide_scratch_bytes<T, RW>(e);
+}
+
+__device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, char *&scratch) {
+    ObsLds L;
+    const int rowsz = e.Hp * e.WW;
+    L.lut = reinterpret_cast<const float4 *>(smem);
+    L.mapc = reinterpret_cast<uint32_t *>(smem + 256);
+    scratch = smem + 256 + wide_a16((size_t)rowsz * 4);
+    L.swe = obs_env_stream_words(e);           // a multiple of 4 words
+    L.stream_words = L.swe;
+    L.rowsz = rowsz;
+    L.stream = reinterpret_cast<uint32_t *>(scratch);
+    L.occ = L.stream + L.swe;
+    L.spos = L.occ + rowsz;
+    L.sgoal = L.spos + e.N;
+    L.shn = L.sgoal + e.N;
+    L.shp = L.shn + 1;
+    L.shpn = reinterpret_cast<int32_t *>(L.shp + e.k_predict);
+    L.bfsw = nullptr;
+    L.bfsown = nullptr;
+    L.idg = reinterpret_cast<uint8_t *>(L.shpn + 1);
+    L.bfs_win = false;                         // BFS channel straight from the tiled maps
+    return L;
+}
+
+__device__ inline void wide_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <class T, int RW, bool NT>
+__global__ __launch_bounds__(64) void rollout_wide_kernel(DevEnv e, int T_steps, WideOut ro) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // XCD-aware env order (as the pair-lane rollout): workgroups are dealt round-robin
+    // over the 8 XCDs, so each XCD owns one contiguous range of envs
+    const int nb = (int)gridDim.x;
+    const int b = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
+                                                  : (int)blockIdx.x;
+    if (b >= e.B) return;
+    const int lane = lane_id();
+    char *scratch;
+    ObsLds L = wide_layout(e, smem, scratch);
+    obs_lut_init(const_cast<float4 *>(L.lut));
+    const uint32_t *mb = env_map(e, b);
+    for (int k = lane; k < L.rowsz; k += 64) L.mapc[k] = mb[k];
+    wide_sync();
+    const Group g(64);
+    const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;
+    for (int t = 0; t < T_steps; ++t) {
+        const size_t s = ro.slots ? (size_t)t : 0;
+        StepOut o = ro.out;
+        if (o.status) o.status += s * BN;
+        if (o.reward) o.reward += s * BN;
+        if (o.shadow_goals) o.shadow_goals += s * e.B;
+        if (o.cost) o.cost += s * BN;
+        if (o.train_valid) o.train_valid += s * BN * NA;
+        if (o.actions_fixed) o.actions_fixed += s * BN;
+        if (o.goals_reached) o.goals_reached += s * BN;
+        if (o.constraints) o.constraints += s * BN;
+        if (o.reward_total) o.reward_total += s * BN;
+        StepInline inl;
+        step_group(e, ro.actions + s * BN, o, 3u, 0, b, g, &inl);
+        // agent.bfsMap of the agents whose goal changed, before the observation reads them
+        for (uint64_t m = inl.bmask; m; m &= m - 1ull) {
+            const int l = ctz64(m);
+            const uint32_t gl = (uint32_t)__builtin_amdgcn_readlane((int)inl.goal, l);
+            srch::search_one<T, RW>(e, false, b, (uint32_t)b * (uint32_t)e.N + (uint32_t)l, gl, NO_CELL, 0, scratch,
+                                    L.mapc);
+        }
+        // observation: zero the stream and occupancy, stage the agents, emit
+        for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
+        obs_load_agents(e, L, b, 1);
+        wide_sync();
+        const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
+        obs_emit<true, NT>(e, L, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
+        wide_sync();
+        // the human's next path, into the buffer it is not walking
+        if (inl.replan)
+            srch::search_one<T, RW>(e, true, b, 0u, inl.rstart, inl.rgoal, inl.rbuf, scratch, L.mapc);
+        wide_sync();
+    }
+}
+
+template <class T, int RW>
+static bool wide_fits(const DevEnv &e) { return wide_lds_bytes<T, RW>(e) <= 64 * 1024; }
+
+template <class T, int RW>
+static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStream_t s) {
+    // persistent waves: every CU holds the same number of workgroups (the LDS request caps
+    // them at ceil(B / CUs) per CU, 160 KiB of LDS per CU), or the fuller CUs pace each step
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const int occ = (e.B + ncu - 1) / ncu;
+    size_t lds = wide_lds_bytes<T, RW>(e);
+    const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
+    if (cap > lds && cap <= 64 * 1024) lds = cap;
+    if (ro.slots)
+        hipLaunchKernelGGL((rollout_wide_kernel<T, RW, true>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
+    else
+        hipLaunchKernelGGL((rollout_wide_kernel<T, RW, false>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
+}
+
+// the search row type of a W-wide map; RW = 2 above 64 rows
+template <class F>
+static auto with_row_type(const DevEnv &e, F f) {
+    const bool two = e.H > 64;
+    if (e.W <= 32) return two ? f(uint32_t{}, std::integral_constant<int, 2>{}) : f(uint32_t{}, std::integral_constant<int, 1>{});
+    if (e.W <= 64) return two ? f(uint64_t{}, std::integral_constant<int, 2>{}) : f(uint64_t{}, std::integral_constant<int, 1>{});
+    return two ? f(srch::Row2{}, std::integral_constant<int, 2>{}) : f(srch::Row2{}, std::integral_constant<int, 1>{});
+}
+
+bool rollout_wide_fusable(const DevEnv &e) {
+    return with_row_type(e, [&](auto t, auto rw) { return wide_fits<decltype(t), decltype(rw)::value>(e); });
+}
+
+void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                         int slots, hipStream_t s) {
+    static int remap = -1;
+    if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
+    const WideOut ro{actions, out, obs, vec, slots, remap};
+    with_row_type(e, [&](auto t, auto rw) { launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, s); return 0; });
+}
+
+}  // namespace mapf

@@ -245,7 +245,7 @@ template <class T, int RW>
 __device__ int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
                           int buf, char *lds, const uint32_t *map = nullptr) {
     const int lane = lane_id();
-    const int W = e.W, H = e.H, cells = H * W;
+    const int W = e.W, H = e.H;
     int len = 0;
     {
         const uint32_t *bits = map ? map : env_map(e, b);
@@ -292,13 +292,26 @@ __device__ int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            int16_t *outp = e.bfs + (size_t)ai * cells;
-            if ((cells & 7) == 0) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(img);
-                uint4 *dst = reinterpret_cast<uint4 *>(outp);
-                for (int k = lane; k < cells / 8; k += 64) dst[k] = src[k];
-            } else {
-                for (int k = lane; k < cells; k += 64) outp[k] = img[k];
+            // out in 8x8 tiles (bfs_at): one 16-B store per tile row, -1 past the map's edge
+            uint4 *dst = reinterpret_cast<uint4 *>(e.bfs + (size_t)ai * bfs_cells(H, W));
+            const int TW = bfs_tw(W), nrows = (int)(bfs_cells(H, W) >> 3);
+            for (int k = lane; k < nrows; k += 64) {
+                const int t = k >> 3, r = ((t / TW) << 3) | (k & 7), c0 = (t % TW) << 3;
+                uint4 v;
+                if ((W & 7) == 0 && r < H) {
+                    v = *reinterpret_cast<const uint4 *>(img + r * W + c0);
+                } else {
+                    uint32_t q[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int ca = c0 + 2 * j, cb = ca + 1;
+                        const uint32_t lo = (r < H && ca < W) ? (uint16_t)img[r * W + ca] : 0xFFFFu;
+                        const uint32_t hi = (r < H && cb < W) ? (uint16_t)img[r * W + cb] : 0xFFFFu;
+                        q[j] = lo | (hi << 16);
+                    }
+                    v = make_uint4(q[0], q[1], q[2], q[3]);
+                }
+                dst[k] = v;
             }
         } else {
             const int gr = prow(stop_cell), gc = pcol(stop_cell);
@@ -381,25 +394,28 @@ __device__ int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint
 
 // All search items of one step (or of a reset), grid-strided over waves.
 //   all = 0: the step's work lists (parity); 1: every env's next path + every
-//   agent's BFS map; 2: every env's next path only.
+//   agent's BFS map; 2: every env's next path only; 3: the step's human paths
+//   only; 4: the step's BFS maps only.
 template <class T, int RW>
 __device__ void search_items(const DevEnv &e, int parity, int all, char *lds, uint32_t wave_id, uint32_t nwaves) {
-    const uint32_t n_replan = all ? (uint32_t)e.B : e.counters[C_REPLAN_COUNT + parity];
-    const uint32_t n_bfs = (!e.keep_bfs || all == 2) ? 0u : (all ? (uint32_t)(e.B * e.N) : e.counters[C_BFS_COUNT + parity]);
+    const bool every = all == 1 || all == 2;
+    const uint32_t n_replan = every ? (uint32_t)e.B : (all == 4 ? 0u : e.counters[C_REPLAN_COUNT + parity]);
+    const uint32_t n_bfs = (!e.keep_bfs || all == 2 || all == 3)
+                               ? 0u : (every ? (uint32_t)(e.B * e.N) : e.counters[C_BFS_COUNT + parity]);
     const uint32_t total = n_replan + n_bfs;
     for (uint32_t item = wave_id; item < total; item += nwaves) {
         const bool replan = item < n_replan;
         uint32_t ai = 0, sr_cell, stop_cell = NO_CELL;
         int b, buf = 0;
         if (replan) {
-            b = all ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];   // parity = list slot
+            b = every ? (int)item : (int)e.replan_list[(size_t)parity * e.B + item];   // parity = list slot
             stop_cell = e.hnext_goal[b];
             if (stop_cell == NO_CELL) continue;
             sr_cell = e.hnext_start[b];
             buf = e.hcur[b] ^ 1;
         } else {
             const uint32_t k = item - n_replan;
-            ai = all ? k : e.bfs_list[(size_t)parity * e.B * e.N + k];
+            ai = every ? k : e.bfs_list[(size_t)parity * e.B * e.N + k];
             b = (int)(ai / (uint32_t)e.N);
             sr_cell = e.goal[ai];
         }

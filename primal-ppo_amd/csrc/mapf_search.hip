@@ -50,7 +50,7 @@ static void launch_search_t(const DevEnv &e, int parity, int all, hipStream_t s)
     const size_t lds = 4 * srch::wave_lds<T, RW>(e.H, e.W);
     const long items = (long)e.B + (e.keep_bfs ? (long)e.B * e.N : 0);
     long grid = (items + 3) / 4;
-    const long cap = all ? 8192 : 128;
+    const long cap = (all == 1 || all == 2) ? 8192 : 128;
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((search_kernel<T, RW>), dim3((unsigned)grid), dim3(256), lds, s, e, parity, all);
@@ -65,6 +65,23 @@ void launch_search(const DevEnv &e, int parity, int all, hipStream_t s) {
     } else {
         if (two) launch_search_t<srch::Row2, 2>(e, parity, all, s); else launch_search_t<srch::Row2, 1>(e, parity, all, s);
     }
+}
+
+// the tiled maps (bfs_at) as row-major [B*N][H][W] int16
+__global__ __launch_bounds__(256) void bfs_export_kernel(DevEnv e, int16_t *__restrict__ dist) {
+    const size_t HW = (size_t)e.H * e.W, n = (size_t)e.B * e.N * HW, bc = bfs_cells(e.H, e.W);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t ai = i / HW;
+        const int cell = (int)(i - ai * HW), r = cell / e.W, c = cell - r * e.W;
+        dist[i] = e.bfs[ai * bc + bfs_at(e.W, r, c)];
+    }
+}
+
+void launch_bfs_export(const DevEnv &e, int16_t *dist, hipStream_t s) {
+    const size_t n = (size_t)e.B * e.N * e.H * e.W;
+    size_t grid = (n + 255) / 256;
+    if (grid > 16384) grid = 16384;
+    hipLaunchKernelGGL(bfs_export_kernel, dim3((unsigned)grid), dim3(256), 0, s, e, dist);
 }
 
 void launch_plan(const DevEnv &e, int promote, hipStream_t s) {

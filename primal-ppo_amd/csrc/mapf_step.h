@@ -1,0 +1,387 @@
+// primal-ppo_amd/csrc/mapf_step.h -- one env's lockstep step on a lane group (device code),
+// shared by step_kernel (mapf_step.hip) and the wide rollout kernel (mapf_rollout_wide.hip).
+//
+// Reference semantics (Nielsencu/primal-ppo mapf_gym.py), in runner.py:64-100
+// order: getActionStatus (:434-480) -> calculateActionReward (:483-511) ->
+// calculateCostReward (:528-533) -> getTrainValid (:535-550) -> jointStep
+// (:614-637: fixActions :552-612, takeStep :158-161, lifelong goals :623-627,
+// human.nextStep :25-31, constraintsViolated :631-633).  The masks that the
+// reference recomputes at the END of jointStep (getUnconditionallyGoodActions
+// :404-430) are a pure function of the state, so this kernel recomputes them
+// at the START of the next step instead of storing them.
+//
+// Mapping: lane = agent, G lanes per env (mapf_group.h).  Conflicts are never
+// materialised as the reference's restrictedAction dict: for distinct agent
+// positions (guaranteed: starts are validated distinct and resolved moves
+// never collide), the dict's content is exactly
+//   (j, b) in R_i[a]  <=>  p_i+d(a) == p_j+d(b)  or  (p_i+d(a) == p_j and p_j+d(b) == p_i)
+// and its key set is  a in keys(i) <=> exists j != i: |p_i+d(a) - p_j|_1 <= 1.
+// (The reference's pruning test, mapf_gym.py:387, never removes a true
+// conflict when positions differ.)
+//
+// HBM traffic per agent-step: ~16 B state read, ~50 B outputs (+ rare BFS /
+// replan work lists) -- latency bound, not bandwidth bound.
+#pragma once
+#include "mapf_group.h"
+#include "mapf_kernels.h"
+#include "mapf_pyset.h"
+
+namespace mapf {
+
+// The search work of one inline step (instead of the work lists): lanes of the agents
+// whose goal changed and, group-uniform, the human's next path to search.
+struct StepInline {
+    uint64_t bmask;        // agents whose bfsMap must be rebuilt (keep_bfs)
+    uint32_t goal;         // per lane: the agent's goal after the step
+    bool replan;           // the human's next path: rstart -> rgoal into path buffer rbuf
+    uint32_t rstart, rgoal;
+    int rbuf;
+};
+
+// One env's step on the group g (lane i of the group = agent i; G >= N).  The
+// search work a committed step creates (BFS maps of the agents whose goal
+// changed, the human's next path) goes to the work lists of slot `parity`, or,
+// with `inl`, to the caller, which searches it inline (mapf_rollout_wide.hip).
+__device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out, uint32_t flags,
+                                  int parity, int b, const Group &g, StepInline *inl) {
+    const int N = e.N;
+    STAMP_BEGIN();
+    const int i = g.i;
+    const bool act = i < N;
+    const size_t ai = (size_t)b * N + i;
+    const uint32_t env_id = e.env_offset + (uint32_t)b;
+    const uint32_t clock = e.clock[b];
+
+    // ---- state -----------------------------------------------------------
+    const uint32_t pp = act ? e.pos[ai] : 0xFFFFFFFFu;
+    const int pr = act ? prow(pp) : -100, pc = act ? pcol(pp) : -100;
+    const uint32_t gg = act ? e.goal[ai] : 0u;
+    const int la = act ? (int)e.last_act[ai] : -1;
+    int a = 0;
+    if (flags & 2u) {          // random policy fused in: same stream as random_actions_kernel
+        if (act) {
+            a = random_action(philox(env_id, P_ACT | ((uint32_t)(i >> 3) << 8), clock, 0u, e.seed), i);
+            actions[ai] = a;
+        }
+    } else if (act) {
+        a = actions[ai];
+        if (a < 0 || a >= NA) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
+    }
+    const uint32_t *bits = env_map(e, b);
+    const uint32_t hp = e.hpos[b], hn = human_next(e, b);
+
+    // ---- getInvalidActions (mapf_gym.py:339-360) ---------------------------
+    // static part: a per-cell 5-bit mask precomputed from the map (off-map / obstacle)
+    const unsigned st_mask = act ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc] : 0x1Fu;
+    unsigned hu_mask = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const int r = pr + dr(k), c = pc + dc(k);
+        if ((st_mask >> k) & 1u) continue;
+        if (pack(r, c) == hn) hu_mask |= 1u << k;
+        else if (pp == hn && pack(r, c) == hp) hu_mask |= 1u << k;
+    }
+    const unsigned rep_mask = la >= 0 ? 1u << opp(la) : 0u;
+
+    STAMP(0);
+    // ---- getRestrictedActions (:363-402), evaluated against actual actions --
+    const int Xr = pr + dr(a), Xc = pc + dc(a);
+    unsigned keys = 0, conf = 0;   // conf: my actions t that collide with some j's actual action
+    uint64_t M = 0;                // agents j colliding with my actual action
+    for (int j = 0; j < N; ++j) {
+        const uint32_t pj = g.shfl(pp, j);
+        const int aj = g.shfl_i(a, j);
+        if (!act || j == i) continue;
+        const int qr = prow(pj), qc = pcol(pj);
+        if (abs(qr - pr) + abs(qc - pc) > 2) continue;
+        const int Yr = qr + dr(aj), Yc = qc + dc(aj);
+        unsigned cj = 0;
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            const int tr = pr + dr(t), tc = pc + dc(t);
+            if (abs(tr - qr) + abs(tc - qc) <= 1) keys |= 1u << t;
+            if ((tr == Yr && tc == Yc) || (tr == qr && tc == qc && Yr == pr && Yc == pc)) cj |= 1u << t;
+        }
+        conf |= cj;
+        if ((cj >> a) & 1u) M |= 1ull << j;
+    }
+    const unsigned good = ~(st_mask | hu_mask | rep_mask | keys) & 0x1Fu;   // setdiff1d (:423)
+
+    STAMP(1);
+    // ---- getActionStatus (:434-480) ----------------------------------------
+    int s0;
+    bool cb = false;
+    if ((st_mask >> a) & 1u) s0 = -1;
+    else if ((hu_mask >> a) & 1u) s0 = -2;
+    else if ((good >> a) & 1u) s0 = 1;
+    else if (M) { s0 = -3; cb = true; }
+    else s0 = ((rep_mask >> a) & 1u) ? -4 : 1;
+    // sequential scan: agent k is skipped if an earlier agent already set it to
+    // -3; an agent taking the conflict branch sets itself and all of M_k to -3
+    // (overwriting earlier statuses, :471-472).
+    uint64_t T = 0;
+    for (uint64_t rem = g.ballot(act && cb); rem; rem &= rem - 1) {
+        const int k = ctz64(rem);
+        const uint64_t Mk = g.shfl64(M, k);
+        if (!((T >> k) & 1ull)) T |= Mk | (1ull << k);
+    }
+    const int st = ((T >> i) & 1ull) ? -3 : s0;
+
+    // ---- calculateActionReward (:483-511) ----------------------------------
+    float rw;
+    switch (st) {
+        case -1: rw = e.collision_cost; break;
+        case -2: rw = e.human_collision_cost; break;
+        case -3: rw = e.collision_cost; break;
+        case -4: rw = e.repeat_cost; break;
+        default: rw = e.action_cost; break;
+    }
+    const bool shadow_hit = act && st == 1 && Xr == prow(gg) && Xc == pcol(gg);
+    const uint64_t shadow_mask = g.ballot(shadow_hit);
+
+    // ---- calculateCostReward (:528-533): pre-step human next position -------
+    float cost = 0.f;
+    {
+        const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
+        const int d2 = d0 * d0 + d1 * d1;
+        if (d2 <= e.R * e.R) cost = e.cost_lut[d2];
+    }
+
+    if (act) {
+        if (out.status) out.status[ai] = (int8_t)st;
+        if (out.reward) out.reward[ai] = rw;
+        if (out.cost) out.cost[ai] = cost;
+        if (out.train_valid) {   // getTrainValid (:535-550)
+            float *tv = out.train_valid + ai * NA;
+#pragma unroll
+            for (int t = 0; t < NA; ++t)
+                tv[t] = (((good >> t) & 1u) || (((keys >> t) & 1u) && !((conf >> t) & 1u))) ? 1.f : 0.f;
+        }
+    }
+    if (i == 0 && out.shadow_goals) out.shadow_goals[b] = popc64(shadow_mask);
+    if (inl) inl->replan = false;
+    if (!(flags & 1u)) return;
+
+    STAMP(2);
+    // ---- jointStep: fixActions (:552-612) ----------------------------------
+    // Worklist semantics of the reference; evictions appended in its set order
+    // (mapf_pyset.h).  States the reference does not survive: an
+    // empty viable set (random.choice([]) raises, :588) stays and evicts as if 0
+    // had been drawn; a deadlock (the while loop never ends, :563) is declared
+    // after fix_draws(N) draws: the unplaced agents stay and blocked movers are
+    // reverted to stay until none is left (fix_revert_blocked).
+    int fixed = a;
+    const uint64_t need = g.ballot(act && (st == -1 || st == -2 || st == -3));
+    if (need) {
+        int assigned = (act && st == 1) ? a : -1;
+        const uint64_t qm = g.ballot(act && st < 0);
+        int q = (act && st < 0) ? popc64(qm & below(i)) : -1;
+        int next_q = popc64(qm), head = 0, draws = 0;
+        const unsigned viable_me = ~(st_mask | hu_mask) & 0x1Fu;
+        while (head < next_q) {
+            const uint64_t hm = g.ballot(act && q == head);
+            const int idx = ctz64(hm);
+            const unsigned good_idx = g.shfl(good, idx);
+            if (good_idx) {
+                ++head;
+                if (i == idx) { assigned = __builtin_ctz(good_idx); q = -1; }
+                continue;
+            }
+            const unsigned viable = g.shfl(viable_me, idx);
+            const uint32_t pidx = g.shfl(pp, idx);
+            const int ir = prow(pidx), ic = pcol(pidx);
+            unsigned cj = 0;   // idx's actions that collide with MY assigned action
+            if (act && i != idx && assigned >= 0 && abs(pr - ir) + abs(pc - ic) <= 2) {
+                const int Yr = pr + dr(assigned), Yc = pc + dc(assigned);
+#pragma unroll
+                for (int t = 0; t < NA; ++t) {
+                    const int tr = ir + dr(t), tc = ic + dc(t);
+                    if ((tr == Yr && tc == Yc) || (tr == pr && tc == pc && Yr == ir && Yc == ic)) cj |= 1u << t;
+                }
+            }
+            unsigned U = 0;
+#pragma unroll
+            for (int t = 0; t < NA; ++t)
+                if (g.ballot((cj >> t) & 1u)) U |= 1u << t;
+            const unsigned fr = viable & ~U;
+            if (fr) {
+                ++head;
+                if (i == idx) { assigned = __builtin_ctz(fr); q = -1; }
+                continue;
+            }
+            if (draws >= fix_draws(N)) {        // deadlock: idx stays queued
+                if (i == 0) atomicAdd(&e.counters[C_FIX_BOUND], 1u);
+                break;
+            }
+            const int nv = __popc(viable);
+            int rsel = 0;
+            if (nv == 0) {      // reference: random.choice([]) raises IndexError
+                if (i == idx) atomicAdd(&e.counters[C_EMPTY_VIABLE], 1u);
+            } else {
+                int pick;
+                if (e.fix_choice == 0) pick = draws % nv;
+                else pick = (int)__umulhi(philox(env_id, P_FIX | ((uint32_t)idx << 8), clock, (uint32_t)draws, e.seed).x,
+                                          (uint32_t)nv);
+                rsel = nth_bit(viable, pick);
+            }
+            ++draws;
+            ++head;
+            const uint64_t ev = g.ballot((cj >> rsel) & 1u);   // evicted agents (at most two)
+            int rank = popc64(ev & below(i));
+            if (__builtin_expect(popc64(ev) == 2, 0)) {
+                const int ja = ctz64(ev), jb = 63 - __builtin_clzll(ev);
+                // restrictedAction[idx][rsel] as (j, b) masks on lane j
+                const int Xr = ir + dr(rsel), Xc = ic + dc(rsel);
+                unsigned rb = 0;
+                if (act && i != idx) {
+#pragma unroll
+                    for (int t = 0; t < NA; ++t) {
+                        const int yr = pr + dr(t), yc = pc + dc(t);
+                        if ((yr == Xr && yc == Xc) || (Xr == pr && Xc == pc && yr == ir && yc == ic)) rb |= 1u << t;
+                    }
+                }
+                if (evict_pair_swapped(g, N, rb, assigned, ja, g.shfl_i(assigned, ja), jb, g.shfl_i(assigned, jb)))
+                    rank = 1 - rank;
+            }
+            if ((ev >> i) & 1ull) { assigned = -1; q = next_q + rank; }
+            next_q += popc64(ev);
+            if (i == idx) { assigned = rsel; q = -1; }
+        }
+        if (head < next_q) {
+            if (act && assigned < 0) assigned = 0;
+            fix_revert_blocked(g, act, pp, assigned);
+        }
+        fixed = assigned >= 0 ? assigned : 0;
+    }
+
+    STAMP(3);
+    // ---- takeStep (:158-161) + lifelong goals (:623-627) --------------------
+    const int nr = pr + dr(fixed), nc = pc + dc(fixed);
+    const uint32_t np = act ? pack(nr, nc) : 0xFFFFFFFFu;
+    const bool reached = act && e.lifelong && np == gg;
+    uint32_t ng = gg;
+    int cur = 0;
+    if (e.goal_mode == 0) {
+        if (reached) {   // Sequence.getNext (util.py:33-39)
+            cur = e.seq_cur[ai];
+            const int len = e.seq_len[ai];
+            const uint32_t *s = e.seq + ai * e.S;
+            if (cur >= len) ng = s[len - 1];
+            else ng = s[cur++];
+            e.seq_cur[ai] = cur;
+        }
+    } else {
+        // getNextGoal(worldWithAgentsAndGoals()) for the reached agents in
+        // index order: agents <= k at new positions, > k at old; goals of
+        // agents < k already replaced (mapf_gym.py:200-209, :620-627).
+        for (uint64_t rem = g.ballot(reached); rem; rem &= rem - 1) {
+            const int k = ctz64(rem);
+            const uint32_t mypos = (i <= k) ? np : pp;
+            const uint32_t mygoal = ng;
+            auto ok = [&](int r, int c) -> bool {
+                if (obstacle_at(e, bits, r, c)) return false;
+                const uint32_t cell = pack(r, c);
+                return g.ballot(act && (mypos == cell || mygoal == cell)) == 0ull;
+            };
+            int r, c;
+            if (!group_free_cell(e, env_id, P_GOAL, k, clock, ok, r, c)) {
+                if (i == k) atomicAdd(&e.counters[C_FREECELL], 1u);
+                r = prow(g.shfl(np, k)); c = pcol(g.shfl(np, k));
+            }
+            if (i == k) ng = pack(r, c);
+        }
+    }
+    const uint64_t bmask = g.ballot(reached && e.keep_bfs);
+    if (inl) {
+        inl->bmask = bmask;
+        inl->goal = ng;
+    }
+    if (act) {
+        e.pos[ai] = np;
+        e.goal[ai] = ng;
+        e.last_act[ai] = (int8_t)fixed;
+        if (reached && e.keep_bfs && !inl) {
+            const uint32_t slot = atomicAdd(&e.counters[C_BFS_COUNT + parity], 1u);
+            e.bfs_list[(size_t)parity * e.B * N + slot] = (uint32_t)ai;
+        }
+    }
+
+    STAMP(4);
+    // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94) -------------------
+    // The path switched to at an end-step was searched one path ahead (search
+    // kernel, buffer hcur ^ 1); here the human only advances, switches buffers
+    // and plans the path after the new one (same goal draw as the reference's).
+    uint32_t hp_new;
+    {
+        const int hs = e.hstep[b], cur = e.hcur[b];
+        const int L = e.hlen[b * 2 + cur];
+        int cur2 = cur, hs2 = hs + 1, seq_idx = 0;
+        bool swapped = false;
+        if (hs >= L - 1) {
+            hs2 = 0;
+            if (e.human_mode == 1) {
+                if (e.hnext_goal[b] != NO_CELL) {
+                    cur2 = cur ^ 1;
+                    swapped = true;
+                    if (i == 0) { e.hgoal[b] = e.hnext_goal[b]; e.hreplans[b] += 1u; }
+                }
+            } else if (e.human_mode == 2) {
+                const int idx = e.hseq_idx[b] + 1;
+                const int len = e.hseq_len[b];
+                seq_idx = idx;
+                if (idx >= len) {
+                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];   // path kept, restarts at [0]
+                } else {
+                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + idx];
+                    cur2 = cur ^ 1;
+                    swapped = true;
+                }
+                if (i == 0) e.hseq_idx[b] = idx;
+            }
+        }
+        const uint32_t *p2 = human_path(e, b, cur2);
+        const int L2 = e.hlen[b * 2 + cur2];
+        hp_new = p2[hs2];
+        const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
+        if (swapped) {
+            uint32_t ns, hg;
+            plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, hg, i == 0);
+            if (inl) {     // group-uniform: the search into the buffer the human is not using
+                inl->replan = hg != NO_CELL;
+                inl->rstart = ns;
+                inl->rgoal = hg;
+                inl->rbuf = cur2 ^ 1;
+            }
+            if (i == 0) {
+                e.hnext_start[b] = ns;
+                e.hnext_goal[b] = hg;
+                if (hg != NO_CELL && !inl) {
+                    const uint32_t slot = atomicAdd(&e.counters[C_REPLAN_COUNT + parity], 1u);
+                    e.replan_list[(size_t)parity * e.B + slot] = (uint32_t)b;
+                }
+            }
+        }
+        if (i == 0) {
+            e.hcur[b] = cur2;
+            e.hstep[b] = hs2;
+            e.hpos[b] = hp_new;
+            e.hnext[b] = hn_new;
+            e.clock[b] = clock + 1u;
+        }
+    }
+
+    STAMP(5);
+    // ---- outputs ------------------------------------------------------------
+    if (act) {
+        const int d0 = prow(hp_new) - nr, d1 = pcol(hp_new) - nc;
+        const float cv = (d0 * d0 + d1 * d1 <= e.constr_d2) ? 1.f : 0.f;   // (:632-633)
+        if (out.actions_fixed) out.actions_fixed[ai] = fixed;
+        if (out.goals_reached) out.goals_reached[ai] = reached ? 1.f : 0.f;
+        if (out.constraints) out.constraints[ai] = cv;
+        if (out.reward_total) out.reward_total[ai] = reached ? rw + e.goal_reward : rw;   // runner.py:89-91
+    }
+    STAMP(6);
+    STAMP_END();
+}
+
+}  // namespace mapf

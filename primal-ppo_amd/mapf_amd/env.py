@@ -57,7 +57,9 @@ class BatchedMapfGym:
         self.h = h
         self.path_capacity = _lib.lib().mapf_path_capacity(self.h)
         self.fused = bool(_lib.lib().mapf_step_observe_fused(self.h))   # step_observe = one launch
-        self.rollout_fused = bool(_lib.lib().mapf_rollout_random_fused(self.h))   # rollout_random = one launch
+        # rollout_random = one launch: 1 pair-lane kernel (c2), 2 one wave per env (c4, c5); 0 per-step launches
+        self.rollout_kernel = int(_lib.lib().mapf_rollout_random_fused(self.h))
+        self.rollout_fused = self.rollout_kernel != 0
         dev = self.device
         B, N = self.B, self.N
         self.out = dict(

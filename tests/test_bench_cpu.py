@@ -31,10 +31,12 @@ def test_host_threads_is_the_gpu_share(monkeypatch):
 
 def test_roofline_bytes_match_design():
     """DESIGN.md §4/§6: 3,001.25 B per agent-step for the rollout / step_observe kernels at c2;
-    SURVEY.md §8d's observe formula at c5 (3,424.6 B)."""
+    SURVEY.md §8d's observe formula at c5 (3,424.6 B) + the BFS channel's map reads
+    (F*F*2 + 2 = 244 B) = 3,668.6 B; the rollout kernels' at c5 3,728.5 B."""
     import bench
     assert bench.fused_bytes_per_agent(6, 11, 20, 20, 8) == 3001.25
-    assert abs(bench.observe_bytes_per_agent(7, 11, 80, 80, 64) - 3424.6) < 0.1
+    assert abs(bench.observe_bytes_per_agent(7, 11, 80, 80, 64) - 3668.6) < 0.1
+    assert abs(bench.fused_bytes_per_agent(7, 11, 80, 80, 64) - 3728.5) < 0.1
 
 
 def test_threaded_batches_match_single_thread():
