@@ -165,17 +165,20 @@ def make_maps(kind, B, H, W, rank):
     return np.stack([keep_largest_component(random_map(rng, H, W, 0.3)) for _ in range(B)]), False
 
 
-# committed rocprofv3 --pmc passes (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py) of the c2 workload
-PMC_REPORTS = {"observe_kernel": "r01_pmc_observe_c2.json",
-               "step_observe_kernel": "r01_pmc_step_observe_c2.json",
-               "rollout_random_kernel": "r01_pmc_rollout_c2.json"}   # (the [B]-buffer, plain-store launch)
+# committed rocprofv3 --pmc passes (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py), by the
+# workload's (B, N, H, W, F, C) and kernel
+PMC_REPORTS = {((4096, 8, 20, 20, 11, 6), "observe_kernel"): "r01_pmc_observe_c2.json",
+               ((4096, 8, 20, 20, 11, 6), "step_observe_kernel"): "r01_pmc_step_observe_c2.json",
+               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r01_pmc_rollout_c2.json",   # [B] buffers
+               ((1024, 16, 40, 40, 9, 6), "rollout_wide_kernel"): "r02_pmc_rollout_wide_c4.json",
+               ((2048, 64, 80, 80, 11, 7), "rollout_wide_kernel"): "r02_pmc_rollout_wide_c5.json"}
 
 
 def pmc_traffic_per_step(B, N, H, W, F, C, kernel):
-    """HBM bytes per lockstep step of `kernel` (MB) from the committed PMC report
-    (per launch / steps per launch), for the c2 workload only -- null otherwise."""
-    path = os.path.join(ROOT, "profiles", PMC_REPORTS.get(kernel, "-"))
-    if (B, N, H, W, F, C) != (4096, 8, 20, 20, 11, 6) or not os.path.exists(path):
+    """HBM bytes per lockstep step of `kernel` (MB) from the committed PMC report of this
+    workload (per launch / steps per launch) -- null where none is committed."""
+    path = os.path.join(ROOT, "profiles", PMC_REPORTS.get(((B, N, H, W, F, C), kernel), "-"))
+    if not os.path.exists(path):
         return None
     with open(path) as f:
         rep = json.load(f)
@@ -413,7 +416,7 @@ def main():
         else:
             kname, bpa, kms, steps_pl = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms, 1
         achieved = bpa * B * N * steps_pl / (kms * 1e-3) / 1e9
-        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname)
+        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname.split("<")[0])
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),

@@ -157,7 +157,11 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     size_t lds = wide_lds_bytes<T, RW>(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (cap > lds && cap <= 64 * 1024) lds = cap;
-    if (ro.slots)
+    // nontemporal observation stores for slot buffers (fresh lines every step) and for a
+    // re-written [B] buffer too large to stay resident in the 256 MiB Infinity Cache (c5:
+    // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4)
+    const bool nt = ro.slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20);
+    if (nt)
         hipLaunchKernelGGL((rollout_wide_kernel<T, RW, true>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
     else
         hipLaunchKernelGGL((rollout_wide_kernel<T, RW, false>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
