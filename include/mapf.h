@@ -290,14 +290,6 @@ int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, 
                        int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                        int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream);
 
-/* out = relu(conv3x3(x, w) + bias) for SCRIMPNet's conv1a / conv1b (net.py:101-122): B images of
- * 9x9 x 128 channels, padding 1, 128 output channels; NHWC fp16 in/out, fp32 accumulation, the
- * conv output and the bias add rounded to fp16 as the autocast path does.  w_taps fp16
- * [9][128 out][128 in] (tap = 3 * dy + dx), bias fp16 [128].  pool != 0: the 2x2 max-pool
- * (nn.MaxPool2d(2), 9x9 -> 4x4) is applied before the store.  x, w_taps, out 16-B aligned. */
-int mapf_conv3x3_c128_9x9(const uint16_t *x, const uint16_t *w_taps, const uint16_t *bias, uint16_t *out, int64_t B,
-                          int32_t pool, void *stream);
-
 /* ---- PPO loss (model.py:115-175) ------------------------------------------
  * All loss terms of one minibatch update over R = rows x agents elements with A actions each,
  * plus d(all_loss)/d(new_ps, new_v, new_cv, policy_sig), in one launch.  Device pointers: fp32

@@ -82,7 +82,6 @@ SIGNATURES = {
     "mapf_tokens": (ctypes.c_int, [P, P, P, P, P, I64, I32, I32, ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_tokens_layernorm": (ctypes.c_int, [P, P, P, P, P, I64, I32, I32, ctypes.c_float, ctypes.c_uint64, P, P,
                                               ctypes.c_float, P, P]),
-    "mapf_conv3x3_c128_9x9": (ctypes.c_int, [P, P, P, P, I64, I32, P]),
     "mapf_ppo_loss": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, I32, P, I64, I32, P, P, P, P, P, P, P,
                                      P]),
     "mapf_attention_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I32, I32, ctypes.c_float, P]),

@@ -180,7 +180,6 @@ class SCRIMPNet(nn.Module):
         self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
         self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
-        self.own_conv = False          # conv1a / conv1b on mapf_conv3x3_c128_9x9 (slower than MIOpen so far)
 
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
@@ -249,16 +248,6 @@ class SCRIMPNet(nn.Module):
             v = vector.reshape(-1, NetParameters.VECTOR_LEN)
 
             def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
-                B_, C_, H_, W_ = x.shape
-                if (self.own_conv and C_ == 128 and H_ == W_ == 9 and m.weight.shape == (128, 128, 3, 3)
-                        and m.stride == (1, 1) and m.padding == (1, 1) and x.dtype == torch.float16
-                        and x.is_contiguous(memory_format=torch.channels_last)):
-                    ho = 4 if pool else 9             # MFMA implicit GEMM, epilogue fused (csrc/mapf_conv.hip)
-                    out = torch.empty((B_, 128, ho, ho), dtype=torch.float16, device=dev,
-                                      memory_format=torch.channels_last)
-                    chk(lib.mapf_conv3x3_c128_9x9(ptr(x), ptr(h16(m.weight, "taps")), ptr(h16(m.bias)), ptr(out),
-                                                  B_, int(pool), st))
-                    return out
                 y = F.conv2d(x, h16(m.weight), None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
                 b = h16(m.bias)
                 B_, C_, H_, W_ = y.shape
@@ -306,7 +295,6 @@ class SCRIMPNet(nn.Module):
         return policy, value, blocking, policy_sig, x, logits, cost_value
 
     _HALF_VIEWS = {"sumT": lambda t: t.sum(0).transpose(0, 1), "sum": lambda t: t.sum(0),
-                   "taps": lambda t: t.permute(2, 3, 0, 1).reshape(9, t.shape[0], t.shape[1]),
                    "q": lambda t: t[:t.shape[0] // 3], "kv": lambda t: t[t.shape[0] // 3:]}
 
     def _half(self, t, view=None):

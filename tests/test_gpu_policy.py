@@ -23,12 +23,10 @@ def _net(n_agents=8):
     return Model(0, "cuda", numChannel=6, num_agents=n_agents, fov=9).network
 
 
-@pytest.mark.parametrize("B,own,conv", [(5, True, False), (256, True, False), (256, False, False),
-                                         (256, True, True)])
-def test_fused_acting_forward_matches_torch_path(B, own, conv):
+@pytest.mark.parametrize("B,own", [(5, True), (256, True), (256, False)])
+def test_fused_acting_forward_matches_torch_path(B, own):
     net = _net().eval()                        # dropout off: both paths deterministic
     net.fused_attention = net.fused_residual_ln = own
-    net.own_conv = conv
     g = torch.Generator(device="cuda").manual_seed(B)
     obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
     vec = torch.randn(B, 8, 4, device="cuda", generator=g)
@@ -197,26 +195,3 @@ def test_fp16_weight_cache_follows_in_place_updates():
         ref = net(obs, vec)
     torch.testing.assert_close(got[1].float(), ref[1].float(), rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(got[5].float(), ref[5].float(), rtol=3e-2, atol=3e-2)
-
-
-@pytest.mark.parametrize("B", [1, 3, 7, 1000])
-@pytest.mark.parametrize("pool", [False, True])
-def test_conv3x3_kernel_vs_torch(B, pool):
-    from mapf_amd import _lib
-    lib = _lib.lib()
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    g = torch.Generator(device="cuda").manual_seed(B + 17 * pool)
-    x = torch.relu(torch.randn(B, 128, 9, 9, device="cuda", generator=g)).half()
-    x = x.contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(128, 128, 3, 3, device="cuda", generator=g) / 24).half()
-    b = (torch.randn(128, device="cuda", generator=g) / 4).half()
-    taps = w.permute(2, 3, 0, 1).reshape(9, 128, 128).contiguous()
-    ref = torch.relu(torch.nn.functional.conv2d(x.float(), w.float(), None, 1, 1).half() + b.view(1, -1, 1, 1))
-    if pool:
-        ref = torch.nn.functional.max_pool2d(ref, 2)
-    ho = 4 if pool else 9
-    out = torch.full((B, 128, ho, ho), float("nan"), dtype=torch.float16, device="cuda").contiguous(
-        memory_format=torch.channels_last)
-    _lib.check(lib.mapf_conv3x3_c128_9x9(_p(x), _p(taps), _p(b), _p(out), B, int(pool), st))
-    # fp32 accumulation in another order than the reference conv, then the same fp16 roundings
-    torch.testing.assert_close(out.float(), ref.float(), rtol=2e-3, atol=2e-3)
