@@ -140,8 +140,8 @@ __device__ inline void obs_init(const DevEnv &e, const ObsLds &L, int E, int b0,
     for (int k = tid + nt; k < nw; k += nt) L.mapc[k] = obs_map_word(e, b0, nenv, k);
 }
 
-__device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0, int nenv) {
-    const int tid = threadIdx.x, nt = blockDim.x, N = e.N, K = nenv * N;
+__device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0, int nenv, int tid, int nt) {
+    const int N = e.N, K = nenv * N;
     for (int k = tid; k < K; k += nt) {
         L.spos[k] = e.pos[(size_t)b0 * N + k];
         L.sgoal[k] = e.goal[(size_t)b0 * N + k];
@@ -158,6 +158,9 @@ __device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0,
         }
         L.shpn[k] = cnt;
     }
+}
+__device__ inline void obs_load_agents(const DevEnv &e, const ObsLds &L, int b0, int nenv) {
+    obs_load_agents(e, L, b0, nenv, (int)threadIdx.x, (int)blockDim.x);
 }
 
 // The config-static zero band of an agent's [C][F][F] block: channel 5

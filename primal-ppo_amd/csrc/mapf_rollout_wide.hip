@@ -86,8 +86,32 @@ __device__ inline void wide_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Two-wave pipelined form (128-thread workgroups, where every env's two waves fit on the
+// chip at once): wave 0 steps, wave 1 observes the step before from the LDS snapshot,
+//     stepper  | step t | A | BFS maps t, snapshot t | B | human path t | step t+1 | A ...
+//     observer |  observe t-1  | A |  (waits)        | B |      observe t         | A ...
+// so a step's latency-bound chains run while the previous observation's stores issue.
+// BFS maps of step t are written between A (observation t-1, which reads the old maps,
+// is done) and B; both waves share one scratch area (the BFS image overlays the
+// observation's bit-stream, unused between A and B).  The stepper releases its stores
+// before each barrier; the observer arrives with no memory wait, so its stores keep
+// draining across the barriers.
+__device__ inline void wide_release_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ inline void wide_plain_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the LDS reads of the store loop are done
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// waves_per_eu(2): at most 256 VGPRs, so two waves of every SIMD stay resident (c5: 2,048
+// envs = 8 waves per CU; above 256 the launch would run in two rounds)
 template <class T, int RW, bool NT>
-__global__ __launch_bounds__(64) void rollout_wide_kernel(DevEnv e, int T_steps, WideOut ro) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(DevEnv e, int T_steps,
+                                                                                                     WideOut ro) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-aware env order (as the pair-lane rollout): workgroups are dealt round-robin
     // over the 8 XCDs, so each XCD owns one contiguous range of envs
@@ -96,16 +120,17 @@ __global__ __launch_bounds__(64) void rollout_wide_kernel(DevEnv e, int T_steps,
                                                   : (int)blockIdx.x;
     if (b >= e.B) return;
     const int lane = lane_id();
+    const bool pipe = blockDim.x == 128;
+    const int role = (int)(threadIdx.x >> 6);          // pipelined: 0 steps, 1 observes
     char *scratch;
     ObsLds L = wide_layout(e, smem, scratch);
     obs_lut_init(const_cast<float4 *>(L.lut));
     const uint32_t *mb = env_map(e, b);
-    for (int k = lane; k < L.rowsz; k += 64) L.mapc[k] = mb[k];
-    wide_sync();
+    for (int k = (int)threadIdx.x; k < L.rowsz; k += (int)blockDim.x) L.mapc[k] = mb[k];
+    __syncthreads();
     const Group g(64);
     const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;
-    for (int t = 0; t < T_steps; ++t) {
-        const size_t s = ro.slots ? (size_t)t : 0;
+    auto step_out = [&](size_t s) {
         StepOut o = ro.out;
         if (o.status) o.status += s * BN;
         if (o.reward) o.reward += s * BN;
@@ -116,27 +141,46 @@ __global__ __launch_bounds__(64) void rollout_wide_kernel(DevEnv e, int T_steps,
         if (o.goals_reached) o.goals_reached += s * BN;
         if (o.constraints) o.constraints += s * BN;
         if (o.reward_total) o.reward_total += s * BN;
-        StepInline inl;
-        step_group(e, ro.actions + s * BN, o, 3u, 0, b, g, &inl);
-        // agent.bfsMap of the agents whose goal changed, before the observation reads them
+        return o;
+    };
+    auto bfs_maps = [&](const StepInline &inl) {
         for (uint64_t m = inl.bmask; m; m &= m - 1ull) {
             const int l = ctz64(m);
             const uint32_t gl = (uint32_t)__builtin_amdgcn_readlane((int)inl.goal, l);
             srch::search_one<T, RW>(e, false, b, (uint32_t)b * (uint32_t)e.N + (uint32_t)l, gl, NO_CELL, 0, scratch,
                                     L.mapc);
         }
-        // observation: zero the stream and occupancy, stage the agents, emit
-        for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
-        obs_load_agents(e, L, b, 1);
-        wide_sync();
-        const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
-        obs_emit<true, NT>(e, L, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
-        wide_sync();
-        // the human's next path, into the buffer it is not walking
-        if (inl.replan)
+    };
+    // one loop for both forms (every function inlined once: the kernel's code stays
+    // within the instruction cache); unpipelined, the one wave takes both roles in the
+    // order step -> BFS maps -> snapshot -> human path -> observe
+    const bool stepper = !pipe || role == 0, observer = !pipe || role == 1;
+    WSTAMP_BEGIN();
+    for (int t = 0; t < T_steps; ++t) {
+        const size_t s = ro.slots ? (size_t)t : 0;
+        StepInline inl;
+        if (stepper) step_group(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl);
+        WSTAMP(0);
+        if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // A: observation t-1 done
+        if (stepper) {
+            bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
+            obs_load_agents(e, L, b, 1, lane, 64);       // snapshot of step t
+        }
+        WSTAMP(1);
+        if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // B: snapshot t in LDS
+        if (stepper && inl.replan)                       // the human's next path, into the other buffer
             srch::search_one<T, RW>(e, true, b, 0u, inl.rstart, inl.rgoal, inl.rbuf, scratch, L.mapc);
-        wide_sync();
+        WSTAMP(2);
+        if (observer) {
+            for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
+            wide_sync();
+            const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
+            obs_emit<true, NT>(e, L, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
+            wide_sync();
+        }
+        WSTAMP(3);
     }
+    WSTAMP_END(b);
 }
 
 template <class T, int RW>
@@ -161,10 +205,20 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     // re-written [B] buffer too large to stay resident in the 256 MiB Infinity Cache (c5:
     // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4)
     const bool nt = ro.slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20);
-    if (nt)
-        hipLaunchKernelGGL((rollout_wide_kernel<T, RW, true>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
-    else
-        hipLaunchKernelGGL((rollout_wide_kernel<T, RW, false>), dim3(e.B), dim3(64), lds, s, e, steps, ro);
+    auto kern = nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
+    // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
+    // (512 per lane) over the waves it must hold, 4 SIMDs per CU
+    static int vgprs[2] = {0, 0};
+    int &vg = vgprs[nt ? 1 : 0];
+    if (vg == 0) {
+        hipFuncAttributes fa{};
+        vg = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern)) == hipSuccess && fa.numRegs > 0
+                 ? fa.numRegs : 512;
+    }
+    const int fit = 512 / ((vg + 7) & ~7);
+    bool pipe = (2 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit;
+    if (const char *v = std::getenv("MAPF_WIDE_PIPE")) pipe = pipe && std::atoi(v) != 0;
+    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, ro);
 }
 
 // the search row type of a W-wide map; RW = 2 above 64 rows

@@ -276,6 +276,15 @@ def test_rollout_random_matches_oracle(name):
     run_random_case(name, case, "rollout", expect_rollout_kernel=kind)
 
 
+@pytest.mark.parametrize("name", ["c4_40x40_n16_f9_looping", "dense_12x12_n16_f9_dahp", "n7_24x24_f11_rand_dahp"])
+def test_rollout_wide_one_wave_form_matches_oracle(name, monkeypatch):
+    """The one-wave-per-env kernel in its unpipelined form (one wave steps and observes;
+    the form c5 runs in) -- small configs otherwise run the two-wave pipelined form."""
+    monkeypatch.setenv("MAPF_WIDE_PIPE", "0")
+    case = FUSED_CASES.get(name) or RANDOM_CASES[name]
+    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
+
+
 def run_random_case(name, case, path, expect_rollout_kernel=None):
     B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
     rng = np.random.default_rng(5)

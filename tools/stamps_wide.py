@@ -1,0 +1,46 @@
+"""Phase breakdown of rollout_wide_kernel from the MAPF_STAMPS diagnostic build.
+
+    make -C primal-ppo_amd/csrc stamps
+    MAPF_LIB=primal-ppo_amd/lib/libmapf_stamps.so CFG=c4 python tools/stamps_wide.py
+
+Per env: s_memtime cycles (100 MHz) of each phase summed over one launch of T steps;
+prints the mean per step over envs.  Phases: step, BFS maps, observe staging, observe
+emit (bit-stream + float4 stores issued), human path search."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd")]
+os.environ.setdefault("MAPF_LIB", os.path.join(ROOT, "primal-ppo_amd", "lib", "libmapf_stamps.so"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from mapf_amd.config import make_config  # noqa: E402
+from mapf_amd.env import BatchedMapfGym  # noqa: E402
+
+cfg = os.environ.get("CFG", "c4")
+T = int(os.environ.get("T", "128"))
+p = bench.PRESETS[cfg]
+B, N, H, F, C = p["envs"], p["agents"], p["size"], p["fov"], p["channels"]
+world, shared = bench.make_maps(p["maps"], B, H, H, 0)
+env = BatchedMapfGym(make_config(B, H, H, num_agents=N, fov=F, num_channel=C, human_mode="random",
+                                 goal_mode="random", fix_choice=1, seed=1234, shared_map=shared))
+env.reset_seeded(world)
+assert env.rollout_kernel == 2, "not a wide-kernel config"
+env.rollout_random(16)
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+env.rollout_random(T)
+b.record()
+torch.cuda.synchronize()
+ms = a.elapsed_time(b)
+tl = env.timeline(min(B, 8192)).astype(np.float64)
+assert (tl[:, 7] == 1).all(), "no stamps: MAPF_LIB is not the stamps build"
+us = tl[:, :4] / 100.0 / T          # s_memtime ticks at 100 MHz -> us per step
+names = ["step", "bfs + snapshot", "human path", "observe"]
+print(f"{cfg}: launch {ms * 1e3 / T:.2f} us/step (stamps build); per-env phase us/step, mean / p99 over envs:")
+for k, nm in enumerate(names):
+    print(f"  {nm:12s} {us[:, k].mean():7.2f} {np.percentile(us[:, k], 99):7.2f}")
+print(f"  total        {us.sum(1).mean():7.2f} {np.percentile(us.sum(1), 99):7.2f}")
