@@ -161,7 +161,8 @@ __host__ __device__ constexpr int fix_draws(int N) { return 16 * N + 64; }
 // conflict-free and staying agents occupy distinct cells, so the result has no
 // shared cell and no swap; the fixpoint is unique (the oracle computes it in
 // another order).  Only the newest stayers can block anyone: O(N) shuffles.
-__device__ inline void fix_revert_blocked(const Group &g, bool act, uint32_t pp, int &assigned) {
+template <class GR>
+__device__ inline void fix_revert_blocked(const GR &g, bool act, uint32_t pp, int &assigned) {
     uint64_t frontier = g.ballot(act && assigned == 0);
     while (frontier) {
         const uint32_t tgt = (act && assigned > 0) ? pack(prow(pp) + dr(assigned), pcol(pp) + dc(assigned)) : NO_CELL;

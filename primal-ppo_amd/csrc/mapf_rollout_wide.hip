@@ -36,6 +36,7 @@ struct WideOut {
     float *obs, *vec;
     int slots;
     int xcd_remap;
+    int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
 };
 
 __host__ __device__ inline size_t wide_a16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -52,18 +53,32 @@ __host__ __device__ inline size_t wide_scratch_bytes(const DevEnv &e) {
     return wide_a16(o > s ? o : s);
 }
 
-// nibble table (256 B) | map rows | scratch
-template <class T, int RW>
-__host__ __device__ inline size_t wide_lds_bytes(const DevEnv &e) {
-    return 256 + wide_a16((size_t)e.Hp * e.WW * 4) + wide_scratch_bytes<T, RW>(e);
+// the cost table (calculateCostReward's, R*R + 1 floats) gets an LDS copy up to 1 KiB
+__host__ __device__ inline size_t wide_cost_bytes(const DevEnv &e) {
+    const size_t n = ((size_t)e.R * e.R + 1) * 4;
+    return n <= 1024 ? wide_a16(n) : 0;
 }
 
-__device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, char *&scratch) {
+__host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide_a16((size_t)(e.H + 4) * (e.W + 4)); }
+
+// nibble table (256 B) | map rows | cost table | [neighbour grid] | scratch
+template <class T, int RW>
+__host__ __device__ inline size_t wide_lds_bytes(const DevEnv &e, int grid = 0) {
+    return 256 + wide_a16((size_t)e.Hp * e.WW * 4) + wide_cost_bytes(e) + (grid == 1 ? wide_grid_bytes(e) : 0) +
+           wide_scratch_bytes<T, RW>(e);
+}
+
+__device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, int gmode, char *&scratch, float *&cost,
+                                    uint8_t *&grid) {
     ObsLds L;
     const int rowsz = e.Hp * e.WW;
     L.lut = reinterpret_cast<const float4 *>(smem);
     L.mapc = reinterpret_cast<uint32_t *>(smem + 256);
-    scratch = smem + 256 + wide_a16((size_t)rowsz * 4);
+    char *cp = smem + 256 + wide_a16((size_t)rowsz * 4);
+    cost = wide_cost_bytes(e) ? reinterpret_cast<float *>(cp) : nullptr;
+    scratch = cp + wide_cost_bytes(e) + (gmode == 1 ? wide_grid_bytes(e) : 0);
+    grid = gmode == 1 ? reinterpret_cast<uint8_t *>(cp + wide_cost_bytes(e))
+                      : (gmode == 2 ? reinterpret_cast<uint8_t *>(scratch) : nullptr);
     L.swe = obs_env_stream_words(e);           // a multiple of 4 words
     L.stream_words = L.swe;
     L.rowsz = rowsz;
@@ -123,12 +138,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     const bool pipe = blockDim.x == 128;
     const int role = (int)(threadIdx.x >> 6);          // pipelined: 0 steps, 1 observes
     char *scratch;
-    ObsLds L = wide_layout(e, smem, scratch);
+    float *lcost;
+    uint8_t *grid;
+    ObsLds L = wide_layout(e, smem, ro.grid, scratch, lcost, grid);
     obs_lut_init(const_cast<float4 *>(L.lut));
     const uint32_t *mb = env_map(e, b);
     for (int k = (int)threadIdx.x; k < L.rowsz; k += (int)blockDim.x) L.mapc[k] = mb[k];
+    if (lcost)
+        for (int k = (int)threadIdx.x; k <= e.R * e.R; k += (int)blockDim.x) lcost[k] = e.cost_lut[k];
     __syncthreads();
-    const Group g(64);
+    const StepSrc src{L.mapc, lcost, grid};   // the step's obstacle tests, cost table, neighbour grid in LDS
+    const WaveGroup g;                     // the env is the whole wave: exchanges by v_readlane
     const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;
     auto step_out = [&](size_t s) {
         StepOut o = ro.out;
@@ -159,7 +179,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
         StepInline inl;
-        if (stepper) step_group(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl);
+        if (stepper) step_group(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl, src);
         WSTAMP(0);
         if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // A: observation t-1 done
         if (stepper) {
@@ -198,9 +218,7 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
             ncu = 256;
     }
     const int occ = (e.B + ncu - 1) / ncu;
-    size_t lds = wide_lds_bytes<T, RW>(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
-    if (cap > lds && cap <= 64 * 1024) lds = cap;
     // nontemporal observation stores for slot buffers (fresh lines every step) and for a
     // re-written [B] buffer too large to stay resident in the 256 MiB Infinity Cache (c5:
     // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4)
@@ -218,7 +236,16 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     const int fit = 512 / ((vg + 7) & ~7);
     bool pipe = (2 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit;
     if (const char *v = std::getenv("MAPF_WIDE_PIPE")) pipe = pipe && std::atoi(v) != 0;
-    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, ro);
+    // the step's neighbour grid: over the scratch when one wave takes both roles (the step
+    // runs while the scratch is free), else its own LDS if every env still fits
+    WideOut r = ro;
+    r.grid = 0;
+    if (!pipe && wide_grid_bytes(e) <= wide_scratch_bytes<T, RW>(e)) r.grid = 2;
+    else if (wide_lds_bytes<T, RW>(e, 1) <= (occ > 1 ? cap : (size_t)64 * 1024)) r.grid = 1;
+    if (const char *v = std::getenv("MAPF_WIDE_GRID")) { if (std::atoi(v) == 0) r.grid = 0; }
+    size_t lds = wide_lds_bytes<T, RW>(e, r.grid);
+    if (cap > lds && cap <= 64 * 1024) lds = cap;
+    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, r);
 }
 
 // the search row type of a W-wide map; RW = 2 above 64 rows
@@ -238,7 +265,7 @@ void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut
                          int slots, hipStream_t s) {
     static int remap = -1;
     if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
-    const WideOut ro{actions, out, obs, vec, slots, remap};
+    const WideOut ro{actions, out, obs, vec, slots, remap, 0};
     with_row_type(e, [&](auto t, auto rw) { launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, s); return 0; });
 }
 

@@ -38,12 +38,25 @@ struct StepInline {
     int rbuf;
 };
 
+// Where a step reads its static tables: the env's padded obstacle rows and the cost
+// table in LDS (the persistent rollout's copies; the static action mask is then derived
+// from the rows), or from HBM (nullptr).
+struct StepSrc {
+    const uint32_t *map = nullptr;
+    const float *cost = nullptr;
+    uint8_t *grid = nullptr;      // (H + 4) x (W + 4) bytes of LDS scratch, whole-wave envs only
+};
+
 // One env's step on the group g (lane i of the group = agent i; G >= N).  The
 // search work a committed step creates (BFS maps of the agents whose goal
 // changed, the human's next path) goes to the work lists of slot `parity`, or,
 // with `inl`, to the caller, which searches it inline (mapf_rollout_wide.hip).
+// Grp: Group (G lanes per env, exchanges through ds_bpermute) or, when the env is the
+// whole wave, WaveGroup (exchanges by v_readlane: the agent loops' indices are
+// wave-uniform, and a readlane costs a few cycles where a bpermute costs an LDS round trip).
+template <class Grp>
 __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out, uint32_t flags,
-                                  int parity, int b, const Group &g, StepInline *inl) {
+                                  int parity, int b, const Grp &g, StepInline *inl, StepSrc src = StepSrc{}) {
     const int N = e.N;
     STAMP_BEGIN();
     const int i = g.i;
@@ -51,6 +64,43 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     const size_t ai = (size_t)b * N + i;
     const uint32_t env_id = e.env_offset + (uint32_t)b;
     const uint32_t clock = e.clock[b];
+
+    // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94): where the human goes --
+    // It depends on nothing the agents do, so its state and path cells are read here,
+    // in the same round of loads as the agents' state (the writes stay at the end).
+    // The path switched to at an end-step was searched one path ahead (buffer hcur ^ 1).
+    const int hs = e.hstep[b], hcur = e.hcur[b];
+    const int hl0 = e.hlen[b * 2], hl1 = e.hlen[b * 2 + 1];
+    const int hL = hcur ? hl1 : hl0;
+    int cur2 = hcur, hs2 = hs + 1, seq_idx = 0;
+    bool swapped = false;
+    uint32_t hgoal_new = NO_CELL;
+    if (hs >= hL - 1) {
+        hs2 = 0;
+        if (e.human_mode == 1) {
+            const uint32_t hng = e.hnext_goal[b];
+            if (hng != NO_CELL) {
+                cur2 = hcur ^ 1;
+                swapped = true;
+                hgoal_new = hng;
+            }
+        } else if (e.human_mode == 2) {
+            const int idx = e.hseq_idx[b] + 1;
+            const int len = e.hseq_len[b];
+            seq_idx = idx;
+            if (idx >= len) {
+                hgoal_new = e.hseq[(size_t)b * e.HS + len - 1];   // path kept, restarts at [0]
+            } else {
+                hgoal_new = e.hseq[(size_t)b * e.HS + idx];
+                cur2 = hcur ^ 1;
+                swapped = true;
+            }
+        }
+    }
+    const int hL2 = cur2 ? hl1 : hl0;
+    const uint32_t *hpath2 = human_path(e, b, cur2);
+    const uint32_t hp_new = hpath2[hs2];
+    const uint32_t hn_new = hpath2[hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1];
 
     // ---- state -----------------------------------------------------------
     const uint32_t pp = act ? e.pos[ai] : 0xFFFFFFFFu;
@@ -67,12 +117,23 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
         a = actions[ai];
         if (a < 0 || a >= NA) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
     }
-    const uint32_t *bits = env_map(e, b);
+    const uint32_t *bits = src.map ? src.map : env_map(e, b);
     const uint32_t hp = e.hpos[b], hn = human_next(e, b);
 
     // ---- getInvalidActions (mapf_gym.py:339-360) ---------------------------
-    // static part: a per-cell 5-bit mask precomputed from the map (off-map / obstacle)
-    const unsigned st_mask = act ? (unsigned)e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc] : 0x1Fu;
+    // static part: a per-cell 5-bit mask precomputed from the map (off-map / obstacle),
+    // or the same five obstacle tests on the LDS rows
+    unsigned st_mask = 0x1Fu;
+    if (act) {
+        if (src.map) {
+            st_mask = 0;
+#pragma unroll
+            for (int k = 0; k < NA; ++k)
+                if (obstacle_at(e, bits, pr + dr(k), pc + dc(k))) st_mask |= 1u << k;
+        } else {
+            st_mask = e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc];
+        }
+    }
     unsigned hu_mask = 0;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
@@ -88,12 +149,8 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     const int Xr = pr + dr(a), Xc = pc + dc(a);
     unsigned keys = 0, conf = 0;   // conf: my actions t that collide with some j's actual action
     uint64_t M = 0;                // agents j colliding with my actual action
-    for (int j = 0; j < N; ++j) {
-        const uint32_t pj = g.shfl(pp, j);
-        const int aj = g.shfl_i(a, j);
-        if (!act || j == i) continue;
-        const int qr = prow(pj), qc = pcol(pj);
-        if (abs(qr - pr) + abs(qc - pc) > 2) continue;
+    // the pair test of agent j at (qr, qc) taking action aj (only pairs within distance 2 matter)
+    auto pair = [&](int j, int qr, int qc, int aj) {
         const int Yr = qr + dr(aj), Yc = qc + dc(aj);
         unsigned cj = 0;
 #pragma unroll
@@ -104,6 +161,41 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
         }
         conf |= cj;
         if ((cj >> a) & 1u) M |= 1ull << j;
+    };
+    if (src.grid) {
+        // The agents within distance 2 straight from an LDS grid of agent indices (the env
+        // is the whole wave, its lanes the agents): 12 neighbour cells per lane instead of
+        // a loop over all N agents.  Grid = (H + 4) x (W + 4) bytes, 2-cell border, 0xFF
+        // empty; positions are distinct, so a cell holds at most one agent.
+        const int GW = e.W + 4, gwords = ((e.H + 4) * GW + 3) >> 2;
+        const int lane = lane_id();
+        for (int k = lane; k < gwords; k += 64) reinterpret_cast<uint32_t *>(src.grid)[k] = 0xFFFFFFFFu;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int me = (pr + 2) * GW + pc + 2;
+        if (act) src.grid[me] = (uint8_t)i;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        constexpr int ODR[12] = {-2, -1, -1, -1, 0, 0, 0, 0, 1, 1, 1, 2};
+        constexpr int ODC[12] = {0, -1, 0, 1, -2, -1, 1, 2, -1, 0, 1, 0};
+        int nb[12];
+#pragma unroll
+        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)src.grid[me + ODR[o] * GW + ODC[o]] : 0xFF;
+#pragma unroll
+        for (int o = 0; o < 12; ++o) {
+            const int j = nb[o];
+            const int aj = (int)shfl32((uint32_t)a, j == 0xFF ? lane : j);   // every lane permutes
+            if (j != 0xFF) pair(j, pr + ODR[o], pc + ODC[o], aj);
+        }
+    } else {
+        for (int j = 0; j < N; ++j) {
+            const uint32_t pj = g.shfl(pp, j);
+            const int aj = g.shfl_i(a, j);
+            if (!act || j == i) continue;
+            const int qr = prow(pj), qc = pcol(pj);
+            if (abs(qr - pr) + abs(qc - pc) > 2) continue;
+            pair(j, qr, qc, aj);
+        }
     }
     const unsigned good = ~(st_mask | hu_mask | rep_mask | keys) & 0x1Fu;   // setdiff1d (:423)
 
@@ -144,7 +236,7 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     {
         const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
         const int d2 = d0 * d0 + d1 * d1;
-        if (d2 <= e.R * e.R) cost = e.cost_lut[d2];
+        if (d2 <= e.R * e.R) cost = src.cost ? src.cost[d2] : e.cost_lut[d2];
     }
 
     if (act) {
@@ -307,42 +399,13 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     }
 
     STAMP(4);
-    // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94) -------------------
-    // The path switched to at an end-step was searched one path ahead (search
-    // kernel, buffer hcur ^ 1); here the human only advances, switches buffers
-    // and plans the path after the new one (same goal draw as the reference's).
-    uint32_t hp_new;
+    // ---- human.nextStep, state writes (the move itself was read at the top) ------
     {
-        const int hs = e.hstep[b], cur = e.hcur[b];
-        const int L = e.hlen[b * 2 + cur];
-        int cur2 = cur, hs2 = hs + 1, seq_idx = 0;
-        bool swapped = false;
-        if (hs >= L - 1) {
-            hs2 = 0;
-            if (e.human_mode == 1) {
-                if (e.hnext_goal[b] != NO_CELL) {
-                    cur2 = cur ^ 1;
-                    swapped = true;
-                    if (i == 0) { e.hgoal[b] = e.hnext_goal[b]; e.hreplans[b] += 1u; }
-                }
-            } else if (e.human_mode == 2) {
-                const int idx = e.hseq_idx[b] + 1;
-                const int len = e.hseq_len[b];
-                seq_idx = idx;
-                if (idx >= len) {
-                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + len - 1];   // path kept, restarts at [0]
-                } else {
-                    if (i == 0) e.hgoal[b] = e.hseq[(size_t)b * e.HS + idx];
-                    cur2 = cur ^ 1;
-                    swapped = true;
-                }
-                if (i == 0) e.hseq_idx[b] = idx;
-            }
+        if (swapped || hs >= hL - 1) {
+            if (e.human_mode == 1 && swapped && i == 0) { e.hgoal[b] = hgoal_new; e.hreplans[b] += 1u; }
+            if (e.human_mode == 2 && i == 0) { e.hgoal[b] = hgoal_new; e.hseq_idx[b] = seq_idx; }
         }
-        const uint32_t *p2 = human_path(e, b, cur2);
-        const int L2 = e.hlen[b * 2 + cur2];
-        hp_new = p2[hs2];
-        const uint32_t hn_new = p2[hs2 + 1 < L2 ? hs2 + 1 : L2 - 1];
+        const int L2 = hL2;
         if (swapped) {
             uint32_t ns, hg;
             plan_next_path(e, b, env_id, clock + (uint32_t)L2, seq_idx, ns, hg, i == 0);

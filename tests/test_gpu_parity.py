@@ -276,11 +276,14 @@ def test_rollout_random_matches_oracle(name):
     run_random_case(name, case, "rollout", expect_rollout_kernel=kind)
 
 
-@pytest.mark.parametrize("name", ["c4_40x40_n16_f9_looping", "dense_12x12_n16_f9_dahp", "n7_24x24_f11_rand_dahp"])
-def test_rollout_wide_one_wave_form_matches_oracle(name, monkeypatch):
+@pytest.mark.parametrize("name,grid", [("c4_40x40_n16_f9_looping", 1), ("dense_12x12_n16_f9_dahp", 1),
+                                       ("n7_24x24_f11_rand_dahp", 1), ("dense_12x12_n16_f9_dahp", 0)])
+def test_rollout_wide_one_wave_form_matches_oracle(name, grid, monkeypatch):
     """The one-wave-per-env kernel in its unpipelined form (one wave steps and observes;
-    the form c5 runs in) -- small configs otherwise run the two-wave pipelined form."""
+    the form c5 runs in) -- small configs otherwise run the two-wave pipelined form --
+    with the step's neighbour grid over the scratch, and without it (the agent loop)."""
     monkeypatch.setenv("MAPF_WIDE_PIPE", "0")
+    monkeypatch.setenv("MAPF_WIDE_GRID", str(grid))
     case = FUSED_CASES.get(name) or RANDOM_CASES[name]
     run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
 

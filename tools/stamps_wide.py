@@ -44,3 +44,15 @@ print(f"{cfg}: launch {ms * 1e3 / T:.2f} us/step (stamps build); per-env phase u
 for k, nm in enumerate(names):
     print(f"  {nm:12s} {us[:, k].mean():7.2f} {np.percentile(us[:, k], 99):7.2f}")
 print(f"  total        {us.sum(1).mean():7.2f} {np.percentile(us.sum(1), 99):7.2f}")
+
+# step_group's own phases (STAMP 0-6, shader-clock cycles) of the LAST step of the launch,
+# per stepping wave (pipelined form: waves 2b; else b)
+wp = env.wave_profile(min(65536, 2 * B)).astype(np.float64)
+rows = wp[wp[:, 7] == 1][:, :7]
+PHASES = ["loads+masks", "conflicts(j-loop)", "status+reward+outputs", "fixActions", "move+goals", "human",
+          "final outputs"]
+if len(rows):
+    print(f"step_group phases, last step, {len(rows)} stepping waves (cycles): mean / p90")
+    for k, nm in enumerate(PHASES):
+        print(f"  {nm:24s} {rows[:, k].mean():9.0f} {np.percentile(rows[:, k], 90):9.0f}")
+    print(f"  {'total':24s} {rows.sum(1).mean():9.0f}")
