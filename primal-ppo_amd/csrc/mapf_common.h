@@ -113,8 +113,16 @@ __host__ __device__ inline int random_action(const u32x4 &o, int i) {
     return (int)((((w >> ((k & 1) * 16)) & 0xFFFFu) * (uint32_t)NA) >> 16);
 }
 
-// Obstacle test on the padded bitmap (off-map cells read as 1 within P cells).
-__device__ inline bool obstacle_at(const DevEnv &e, const uint32_t *bits, int r, int c) {
+// LDS-typed pointers.  A pointer the compiler cannot prove to be LDS is generic and its
+// accesses compile to flat_* instructions, which also count in vmcnt: a flat read of LDS
+// then waits behind the wave's outstanding global stores.
+template <class T> using lds_ptr = __attribute__((address_space(3))) T *;
+template <class T> __device__ inline lds_ptr<T> as_lds(T *p) { return (lds_ptr<T>)p; }
+
+// Obstacle test on the padded bitmap (off-map cells read as 1 within P cells); `bits` a
+// global, generic or LDS pointer.
+template <class P>
+__device__ inline bool obstacle_at(const DevEnv &e, P bits, int r, int c) {
     if (r < -e.P || r >= e.H + e.P || c < -e.P || c >= e.W + e.P) return true;
     int rr = r + e.P, cc = c + e.P;
     return (bits[rr * e.WW + (cc >> 5)] >> (cc & 31)) & 1u;

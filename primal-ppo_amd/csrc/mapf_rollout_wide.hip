@@ -147,7 +147,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     if (lcost)
         for (int k = (int)threadIdx.x; k <= e.R * e.R; k += (int)blockDim.x) lcost[k] = e.cost_lut[k];
     __syncthreads();
-    const StepSrc src{L.mapc, lcost, grid};   // the step's obstacle tests, cost table, neighbour grid in LDS
+    StepRegs rs;                           // the stepping wave keeps the env's state in registers
+    step_regs_load(e, b, lane, rs);
+    const StepSrc src{L.mapc, lcost, grid};   // obstacle tests, cost table, neighbour grid in LDS
     const WaveGroup g;                     // the env is the whole wave: exchanges by v_readlane
     const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;
     auto step_out = [&](size_t s) {
@@ -179,17 +181,32 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
         StepInline inl;
-        if (stepper) step_group(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl, src);
+        if (stepper) step_group<WaveGroup, true>(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs);
         WSTAMP(0);
         if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // A: observation t-1 done
         if (stepper) {
             bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
-            obs_load_agents(e, L, b, 1, lane, 64);       // snapshot of step t
+            // snapshot of step t for the observation: cells, goals, the human's next cell from
+            // the registers, the human's path cells (HP channel) from HBM
+            if (lane < e.N) { L.spos[lane] = rs.pp; L.sgoal[lane] = rs.gg; }
+            if (lane == 0) {
+                L.shn[0] = rs.hn;
+                int cnt = 0;
+                if (e.use_hp && e.C >= 6) {
+                    const int len = rs.hcur ? rs.hl1 : rs.hl0;
+                    const uint32_t *path = human_path(e, b, rs.hcur);
+                    for (int q = 1; q <= e.k_predict && q < len; ++q) L.shp[cnt++] = path[q];
+                }
+                L.shpn[0] = cnt;
+            }
         }
         WSTAMP(1);
         if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // B: snapshot t in LDS
-        if (stepper && inl.replan)                       // the human's next path, into the other buffer
-            srch::search_one<T, RW>(e, true, b, 0u, inl.rstart, inl.rgoal, inl.rbuf, scratch, L.mapc);
+        if (stepper && inl.replan) {                     // the human's next path, into the other buffer
+            const int len = srch::search_one<T, RW>(e, true, b, 0u, inl.rstart, inl.rgoal, inl.rbuf, scratch, L.mapc);
+            if (inl.rbuf) rs.hl1 = len;
+            else rs.hl0 = len;
+        }
         WSTAMP(2);
         if (observer) {
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ

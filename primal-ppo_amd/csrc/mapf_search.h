@@ -100,29 +100,38 @@ __device__ inline uint64_t rdlane(uint64_t x, int l) {
 }
 __device__ inline Row2 rdlane(Row2 x, int l) { return {rdlane(x.lo, l), rdlane(x.hi, l)}; }
 
-__device__ inline uint64_t bits64_at(const uint32_t *row, int WW, int off) {
+template <class P>
+__device__ inline uint64_t bits64_at(P row, int WW, int off) {
     const int w = off >> 5, s = off & 31;
     auto word = [&](int k) -> uint64_t { return (k < WW) ? (uint64_t)row[k] : 0xFFFFFFFFull; };
     const uint64_t a = word(w) | (word(w + 1) << 32);
     const uint64_t b = word(w + 2);
     return s == 0 ? a : ((a >> s) | (b << (64 - s)));
 }
-template <class T> __device__ inline T free_row(const DevEnv &e, const uint32_t *bits, int r);
-template <> __device__ inline uint64_t free_row<uint64_t>(const DevEnv &e, const uint32_t *bits, int r) {
+// free cells of map row r as a row mask; `bits` a global or LDS pointer to the padded rows
+template <class P> __device__ inline uint64_t free_row64(const DevEnv &e, P bits, int r) {
     if (r >= e.H) return 0;
     const uint64_t f = ~bits64_at(bits + (size_t)(r + e.P) * e.WW, e.WW, e.P);
     return e.W >= 64 ? f : (f & ((1ull << e.W) - 1));
 }
-template <> __device__ inline uint32_t free_row<uint32_t>(const DevEnv &e, const uint32_t *bits, int r) {
-    return (uint32_t)free_row<uint64_t>(e, bits, r);
-}
-template <> __device__ inline Row2 free_row<Row2>(const DevEnv &e, const uint32_t *bits, int r) {
-    if (r >= e.H) return {0, 0};
-    const uint32_t *row = bits + (size_t)(r + e.P) * e.WW;
-    Row2 f = {~bits64_at(row, e.WW, e.P), ~bits64_at(row, e.WW, e.P + 64)};
-    if (e.W < 128) f.hi &= (1ull << (e.W - 64)) - 1;
-    return f;
-}
+template <class T> struct FreeRow;
+template <> struct FreeRow<uint64_t> {
+    template <class P> __device__ static uint64_t get(const DevEnv &e, P bits, int r) { return free_row64(e, bits, r); }
+};
+template <> struct FreeRow<uint32_t> {
+    template <class P> __device__ static uint32_t get(const DevEnv &e, P bits, int r) {
+        return (uint32_t)free_row64(e, bits, r);
+    }
+};
+template <> struct FreeRow<Row2> {
+    template <class P> __device__ static Row2 get(const DevEnv &e, P bits, int r) {
+        if (r >= e.H) return {0, 0};
+        const P row = bits + (size_t)(r + e.P) * e.WW;
+        Row2 f = {~bits64_at(row, e.WW, e.P), ~bits64_at(row, e.WW, e.P + 64)};
+        if (e.W < 128) f.hi &= (1ull << (e.W - 64)) - 1;
+        return f;
+    }
+};
 
 // Level-synchronous BFS over free cells from (sr, sc).  V = visited rows,
 // D[k] = bit k of each visited cell's distance.  Stops after the level that
@@ -242,16 +251,24 @@ __host__ __device__ inline size_t wave_lds(int H, int W) {
 // `lds` = wave_lds<T, RW>(H, W) bytes of this wave's LDS; `map` = the env's padded
 // obstacle rows if the caller holds a copy (e.g. in LDS), else read from HBM.
 template <class T, int RW>
-__device__ int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
+__device__ __attribute__((always_inline)) inline int search_one(const DevEnv &e, bool replan, int b, uint32_t ai, uint32_t sr_cell, uint32_t stop_cell,
                           int buf, char *lds, const uint32_t *map = nullptr) {
     const int lane = lane_id();
     const int W = e.W, H = e.H;
     int len = 0;
     {
-        const uint32_t *bits = map ? map : env_map(e, b);
+        // the map rows from the caller's LDS copy (typed, so the reads are ds_* and never
+        // wait behind the wave's global stores), else from HBM
         T fre[RW];
+        if (map) {
+            const auto bits = as_lds(const_cast<uint32_t *>(map));
 #pragma unroll
-        for (int k = 0; k < RW; ++k) fre[k] = free_row<T>(e, bits, lane + 64 * k);
+            for (int k = 0; k < RW; ++k) fre[k] = FreeRow<T>::get(e, bits, lane + 64 * k);
+        } else {
+            const uint32_t *bits = env_map(e, b);
+#pragma unroll
+            for (int k = 0; k < RW; ++k) fre[k] = FreeRow<T>::get(e, bits, lane + 64 * k);
+        }
         const int sr = prow(sr_cell), sc = pcol(sr_cell);
         if (!replan) {
             // the map copy (-1 obstacle / -2 free), then the BFS levels on top, then one

@@ -41,6 +41,31 @@ struct StepInline {
 // Where a step reads its static tables: the env's padded obstacle rows and the cost
 // table in LDS (the persistent rollout's copies; the static action mask is then derived
 // from the rows), or from HBM (nullptr).
+// An env's state held in registers by a persistent caller (the wide rollout's stepping
+// wave): read instead of HBM at the start of a step and updated at its end (the HBM
+// copy is still written, for everything else that reads it).
+struct StepRegs {
+    uint32_t pp, gg;     // per lane: the agent's cell and goal
+    int la;              // per lane: its last action (-1 none)
+    uint32_t clock, hp, hn;
+    int hs, hcur, hl0, hl1;
+};
+
+__device__ inline void step_regs_load(const DevEnv &e, int b, int i, StepRegs &r) {
+    const bool act = i < e.N;
+    const size_t ai = (size_t)b * e.N + i;
+    r.pp = act ? e.pos[ai] : 0xFFFFFFFFu;
+    r.gg = act ? e.goal[ai] : 0u;
+    r.la = act ? (int)e.last_act[ai] : -1;
+    r.clock = e.clock[b];
+    r.hp = e.hpos[b];
+    r.hn = e.hnext[b];
+    r.hs = e.hstep[b];
+    r.hcur = e.hcur[b];
+    r.hl0 = e.hlen[b * 2];
+    r.hl1 = e.hlen[b * 2 + 1];
+}
+
 struct StepSrc {
     const uint32_t *map = nullptr;
     const float *cost = nullptr;
@@ -54,23 +79,27 @@ struct StepSrc {
 // Grp: Group (G lanes per env, exchanges through ds_bpermute) or, when the env is the
 // whole wave, WaveGroup (exchanges by v_readlane: the agent loops' indices are
 // wave-uniform, and a readlane costs a few cycles where a bpermute costs an LDS round trip).
-template <class Grp>
-__device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions, const StepOut &out, uint32_t flags,
-                                  int parity, int b, const Grp &g, StepInline *inl, StepSrc src = StepSrc{}) {
+// REGS: the env's state comes from and goes back to `rg` (register-resident, persistent
+// callers) instead of being loaded from HBM (it is still stored to HBM).
+template <class Grp, bool REGS = false>
+__device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e, int32_t *__restrict__ actions,
+                                                                const StepOut &out, uint32_t flags, int parity, int b,
+                                                                const Grp &g, StepInline *inl, StepSrc src,
+                                                                StepRegs &rg) {
     const int N = e.N;
     STAMP_BEGIN();
     const int i = g.i;
     const bool act = i < N;
     const size_t ai = (size_t)b * N + i;
     const uint32_t env_id = e.env_offset + (uint32_t)b;
-    const uint32_t clock = e.clock[b];
+    const uint32_t clock = REGS ? rg.clock : e.clock[b];
 
     // ---- human.nextStep (:25-31, :42-44, :65-70, :87-94): where the human goes --
     // It depends on nothing the agents do, so its state and path cells are read here,
     // in the same round of loads as the agents' state (the writes stay at the end).
     // The path switched to at an end-step was searched one path ahead (buffer hcur ^ 1).
-    const int hs = e.hstep[b], hcur = e.hcur[b];
-    const int hl0 = e.hlen[b * 2], hl1 = e.hlen[b * 2 + 1];
+    const int hs = REGS ? rg.hs : e.hstep[b], hcur = REGS ? rg.hcur : e.hcur[b];
+    const int hl0 = REGS ? rg.hl0 : e.hlen[b * 2], hl1 = REGS ? rg.hl1 : e.hlen[b * 2 + 1];
     const int hL = hcur ? hl1 : hl0;
     int cur2 = hcur, hs2 = hs + 1, seq_idx = 0;
     bool swapped = false;
@@ -103,10 +132,10 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     const uint32_t hn_new = hpath2[hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1];
 
     // ---- state -----------------------------------------------------------
-    const uint32_t pp = act ? e.pos[ai] : 0xFFFFFFFFu;
+    const uint32_t pp = REGS ? rg.pp : (act ? e.pos[ai] : 0xFFFFFFFFu);
     const int pr = act ? prow(pp) : -100, pc = act ? pcol(pp) : -100;
-    const uint32_t gg = act ? e.goal[ai] : 0u;
-    const int la = act ? (int)e.last_act[ai] : -1;
+    const uint32_t gg = REGS ? rg.gg : (act ? e.goal[ai] : 0u);
+    const int la = REGS ? rg.la : (act ? (int)e.last_act[ai] : -1);
     int a = 0;
     if (flags & 2u) {          // random policy fused in: same stream as random_actions_kernel
         if (act) {
@@ -117,19 +146,25 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
         a = actions[ai];
         if (a < 0 || a >= NA) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
     }
-    const uint32_t *bits = src.map ? src.map : env_map(e, b);
-    const uint32_t hp = e.hpos[b], hn = human_next(e, b);
+    // REGS callers hold the map rows, cost table and neighbour grid in LDS: typed as such
+    const uint32_t *bits = env_map(e, b);
+    const auto lmap = as_lds(src.map);
+    auto obstacle = [&](int r, int c) -> bool {
+        if constexpr (REGS) return obstacle_at(e, lmap, r, c);
+        else return obstacle_at(e, bits, r, c);
+    };
+    const uint32_t hp = REGS ? rg.hp : e.hpos[b], hn = REGS ? rg.hn : human_next(e, b);
 
     // ---- getInvalidActions (mapf_gym.py:339-360) ---------------------------
     // static part: a per-cell 5-bit mask precomputed from the map (off-map / obstacle),
     // or the same five obstacle tests on the LDS rows
     unsigned st_mask = 0x1Fu;
     if (act) {
-        if (src.map) {
+        if (REGS) {
             st_mask = 0;
 #pragma unroll
             for (int k = 0; k < NA; ++k)
-                if (obstacle_at(e, bits, pr + dr(k), pc + dc(k))) st_mask |= 1u << k;
+                if (obstacle(pr + dr(k), pc + dc(k))) st_mask |= 1u << k;
         } else {
             st_mask = e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc];
         }
@@ -162,25 +197,27 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
         conf |= cj;
         if ((cj >> a) & 1u) M |= 1ull << j;
     };
-    if (src.grid) {
+    if (REGS && src.grid) {
         // The agents within distance 2 straight from an LDS grid of agent indices (the env
         // is the whole wave, its lanes the agents): 12 neighbour cells per lane instead of
         // a loop over all N agents.  Grid = (H + 4) x (W + 4) bytes, 2-cell border, 0xFF
         // empty; positions are distinct, so a cell holds at most one agent.
         const int GW = e.W + 4, gwords = ((e.H + 4) * GW + 3) >> 2;
         const int lane = lane_id();
-        for (int k = lane; k < gwords; k += 64) reinterpret_cast<uint32_t *>(src.grid)[k] = 0xFFFFFFFFu;
+        const auto grid = as_lds(src.grid);
+        const auto grid32 = as_lds(reinterpret_cast<uint32_t *>(src.grid));
+        for (int k = lane; k < gwords; k += 64) grid32[k] = 0xFFFFFFFFu;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int me = (pr + 2) * GW + pc + 2;
-        if (act) src.grid[me] = (uint8_t)i;
+        if (act) grid[me] = (uint8_t)i;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         constexpr int ODR[12] = {-2, -1, -1, -1, 0, 0, 0, 0, 1, 1, 1, 2};
         constexpr int ODC[12] = {0, -1, 0, 1, -2, -1, 1, 2, -1, 0, 1, 0};
         int nb[12];
 #pragma unroll
-        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)src.grid[me + ODR[o] * GW + ODC[o]] : 0xFF;
+        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)grid[me + ODR[o] * GW + ODC[o]] : 0xFF;
 #pragma unroll
         for (int o = 0; o < 12; ++o) {
             const int j = nb[o];
@@ -236,7 +273,7 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     {
         const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
         const int d2 = d0 * d0 + d1 * d1;
-        if (d2 <= e.R * e.R) cost = src.cost ? src.cost[d2] : e.cost_lut[d2];
+        if (d2 <= e.R * e.R) cost = (REGS && src.cost) ? as_lds(src.cost)[d2] : e.cost_lut[d2];
     }
 
     if (act) {
@@ -371,7 +408,7 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
             const uint32_t mypos = (i <= k) ? np : pp;
             const uint32_t mygoal = ng;
             auto ok = [&](int r, int c) -> bool {
-                if (obstacle_at(e, bits, r, c)) return false;
+                if (obstacle(r, c)) return false;
                 const uint32_t cell = pack(r, c);
                 return g.ballot(act && (mypos == cell || mygoal == cell)) == 0ull;
             };
@@ -387,6 +424,13 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
     if (inl) {
         inl->bmask = bmask;
         inl->goal = ng;
+    }
+    if constexpr (REGS) {
+        if (act) {
+            rg.pp = np;
+            rg.gg = ng;
+            rg.la = fixed;
+        }
     }
     if (act) {
         e.pos[ai] = np;
@@ -430,6 +474,13 @@ __device__ inline void step_group(const DevEnv &e, int32_t *__restrict__ actions
             e.hpos[b] = hp_new;
             e.hnext[b] = hn_new;
             e.clock[b] = clock + 1u;
+        }
+        if constexpr (REGS) {
+            rg.hcur = cur2;
+            rg.hs = hs2;
+            rg.hp = hp_new;
+            rg.hn = hn_new;
+            rg.clock = clock + 1u;
         }
     }
 

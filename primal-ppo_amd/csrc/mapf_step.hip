@@ -14,8 +14,9 @@ __global__ __launch_bounds__(256) void step_kernel(DevEnv e, int32_t *__restrict
         e.counters[C_BFS_COUNT + (parity + 1) % 3] = 0;
     }
     if (b >= e.B) return;                 // whole group leaves together
-    if (G == 64) step_group(e, actions, out, flags, parity, b, WaveGroup(), nullptr);   // one env per wave
-    else step_group(e, actions, out, flags, parity, b, Group(G), nullptr);
+    StepRegs none;
+    if (G == 64) step_group(e, actions, out, flags, parity, b, WaveGroup(), nullptr, StepSrc{}, none);   // env = wave
+    else step_group(e, actions, out, flags, parity, b, Group(G), nullptr, StepSrc{}, none);
 }
 
 // Uniform random policy (random_action(): one Philox draw per 8 agents).
