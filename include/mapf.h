@@ -15,6 +15,7 @@
  *   jointStep(a, st)                mapf_gym.py:614-637             -> mapf_step (MAPF_STEP_COMMIT)
  *   jointStep + getAllObservations  runner.py:84-97                 -> mapf_step_observe (one launch)
  *   agent.bfsMap / makeBfsMap       mapf_gym.py:211-244             -> mapf_bfs
+ *   renderWorld / MapfGym._render   util.py:189-232, mapf_gym.py:639 -> mapf_render
  *   Runner.run GAE                  runner.py:117-149               -> mapf_gae
  *   Model.train normalisation       model.py:106-113                -> mapf_normalize_advantages
  *   Model.step sampling             model.py:38-40                  -> mapf_sample_actions
@@ -217,6 +218,14 @@ int mapf_random_actions(mapf_env *env, int32_t *actions, void *stream);
 
 /* Copy agent.bfsMap for every agent: DEVICE int16 [B][N][H][W] (requires keep_bfs). */
 int mapf_bfs(mapf_env *env, int16_t *dist, void *stream);
+
+/* renderWorld (util.py:189-232; MapfGym._render, mapf_gym.py:639-646) for n envs at once:
+ * envs = DEVICE int32 [n] env indices, frames = DEVICE uint8 [n][H*scale][W*scale][3] RGB.
+ * Cells white / black, the human's remaining path as grey arrows and a star, agents' cells
+ * in hsv(i / N, 1, 1), their goals as discs, the human as a grey triangle, painted in the
+ * reference's order.  Polygons cover the pixels inside or on them (the reference uses cv2,
+ * absent here: its edge rasterisation may differ by a pixel).  scale in 4..64. */
+int mapf_render(mapf_env *env, const int32_t *envs, int32_t n, int32_t scale, uint8_t *frames, void *stream);
 
 /* Counters of impossible states / clamped events (host uint32[16]); synchronises the stream. */
 int mapf_get_counters(mapf_env *env, uint32_t *host16, void *stream);

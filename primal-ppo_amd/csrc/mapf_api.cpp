@@ -602,6 +602,54 @@ int mapf_bfs(mapf_env *e, int16_t *dist, void *stream) {
     return MAPF_OK;
 }
 
+// hsv_to_rgb(h, 1, 1) (matplotlib.colors, util.init_colors) * 255, truncated like astype('uint8')
+static void hue_rgb(double h, uint8_t *rgb) {
+    const double h6 = h * 6.0;
+    const int i = (int)std::floor(h6) % 6;
+    const double f = h6 - std::floor(h6), q = 1.0 - f, t = f;
+    double r, g, b;
+    switch (i) {
+        case 0: r = 1; g = t; b = 0; break;
+        case 1: r = q; g = 1; b = 0; break;
+        case 2: r = 0; g = 1; b = t; break;
+        case 3: r = 0; g = q; b = 1; break;
+        case 4: r = t; g = 0; b = 1; break;
+        default: r = 1; g = 0; b = q; break;
+    }
+    rgb[0] = (uint8_t)(r * 255.0); rgb[1] = (uint8_t)(g * 255.0); rgb[2] = (uint8_t)(b * 255.0);
+}
+
+int mapf_render(mapf_env *e, const int32_t *envs, int32_t n, int32_t scale, uint8_t *frames, void *stream) {
+    if (!e || !envs || !frames) return fail(MAPF_EINVAL, "null argument");
+    if (!e->ready) return fail(MAPF_ESTATE, "mapf_render before mapf_reset");
+    if (n < 0 || n > 65535) return fail(MAPF_EINVAL, "n must be in 0..65535");
+    if (scale < 4 || scale > 64) return fail(MAPF_EINVAL, "scale must be in 4..64");
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (int rc = flush_search(e, s)) return rc;
+    if (n == 0) return MAPF_OK;
+    RenderSpec rs{};
+    rs.scale = scale;
+    const uint8_t fixed[9] = {255, 255, 255, 0, 0, 0, 127, 127, 127};   // colours[0], [-1], [-2] * 255
+    std::memcpy(rs.palette, fixed, 9);
+    for (int a = 0; a < e->d.N; ++a) hue_rgb((double)a / (double)e->d.N, rs.palette + 3 * (3 + a));
+    // drawStar(coord, S, S, 5): outerRad = S // 2, innerRad = int(outerRad * 3 / 8)
+    const double PI = 3.141592653589793, between = 2.0 * PI / 5.0;
+    const int outer = scale / 2, inner = (int)(outer * 3.0 / 8.0);
+    for (int i = 0; i < 5; ++i) {
+        const double pa = PI / 2.0 + i * between;
+        const double ang[3] = {pa - between / 2.0, pa, pa + between / 2.0};
+        const int rad[3] = {inner, outer, inner};
+        for (int k = 0; k < 3; ++k) {
+            rs.star_x[3 * i + k] = rad[k] * std::cos(ang[k]);
+            rs.star_y[3 * i + k] = rad[k] * std::sin(ang[k]);
+        }
+    }
+    launch_render(e->d, envs, n, rs, frames, s);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
 int mapf_get_counters(mapf_env *e, uint32_t *host16, void *stream) {
     if (!e || !host16) return fail(MAPF_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));

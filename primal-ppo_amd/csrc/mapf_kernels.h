@@ -49,6 +49,13 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
 bool rollout_wide_fusable(const DevEnv &e);
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, hipStream_t s);
+// renderWorld (util.py:189-232) on the device (mapf_render.hip): frames [n][H*S][W*S][3] u8
+struct RenderSpec {
+    int scale;
+    uint8_t palette[67 * 3];        // 0 free, 1 obstacle, 2 grey (human, path), 3 + i agent i
+    double star_x[15], star_y[15];  // drawStar's r cos(a), r sin(a) per vertex (host libm, as the reference's math)
+};
+void launch_render(const DevEnv &e, const int32_t *envs, int n, const RenderSpec &rs, uint8_t *frames, hipStream_t s);
 // obstacle maps on the device (mapf_maps.hip): kind 0 warehouse (length in [lo, hi]), 1 random
 // density p; largest: keep only the largest 4-connected free component (H * W <= LC_MAX_CELLS)
 struct MapGen {

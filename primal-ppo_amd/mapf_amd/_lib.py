@@ -62,6 +62,7 @@ SIGNATURES = {
     "mapf_flush": (ctypes.c_int, [P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),
+    "mapf_render": (ctypes.c_int, [P, P, I32, I32, P, P]),
     "mapf_get_counters": (ctypes.c_int, [P, P, P]),
     "mapf_get_profile": (ctypes.c_int, [P, P, ctypes.c_int, P]),
     "mapf_get_timeline": (ctypes.c_int, [P, P, ctypes.c_int32, P]),

@@ -282,6 +282,18 @@ class BatchedMapfGym:
         _lib.check(_lib.lib().mapf_bfs(self.h, _ptr(d), _stream(self.device)))
         return d
 
+    def render(self, envs=None, scale=20):
+        """renderWorld (util.py:189-232) of the given envs (default all) on the device:
+        uint8 RGB frames [n, H*scale, W*scale, 3] on this env's device."""
+        idx = torch.arange(self.B, dtype=torch.int32) if envs is None else torch.as_tensor(envs, dtype=torch.int32)
+        if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= self.B):
+            raise IndexError(f"env index out of range 0..{self.B - 1}")
+        idx = idx.to(self.device).contiguous()
+        out = torch.empty(idx.numel(), self.H * scale, self.W * scale, 3, dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.lib().mapf_render(self.h, _ptr(idx), idx.numel(), int(scale), _ptr(out),
+                                          _stream(self.device)))
+        return out
+
     def counters(self):
         c = np.zeros(16, np.uint32)
         _lib.check(_lib.lib().mapf_get_counters(self.h, ctypes.c_void_p(c.ctypes.data), _stream(self.device)))

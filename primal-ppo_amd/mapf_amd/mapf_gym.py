@@ -61,6 +61,11 @@ class _SingleEnv:
         self._pending = None
         return o["goals_reached"][0].astype(np.float64), o["constraints"][0].astype(np.float64)
 
+    def _render(self, scale=20):
+        """MapfGym._render (mapf_gym.py:639-646): renderWorld of this env, uint8 [H*20, W*20, 3],
+        drawn on the device (mapf_render)."""
+        return self._env.render([0], scale=scale)[0].cpu().numpy()
+
     # state views used by tests / rendering
     def agent_positions(self):
         return self._env.get_state()["pos"][0]
