@@ -459,6 +459,10 @@ def main():
             line["valid"] = False
             line["invalid_reason"] = f"device error counters {bad}"
             print(f"bench: device error counters {bad}", file=sys.stderr)
+        if B * N < 1024:
+            line["note"] = (f"{B * N} agents per GPU: one rollout step is a chain of dependent wave-level "
+                            "phases (latency-bound, a few us), so a single CPU thread stepping small "
+                            "batches can be faster; the GPU path is for thousands of envs (c2-c5)")
         if world_size == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(world, H, W, N, F, C, args.cpu_seconds)
         else:
