@@ -276,6 +276,68 @@ def test_rollout_random_matches_oracle(name):
     run_random_case(name, case, "rollout", expect_rollout_kernel=kind)
 
 
+# the one-wave-per-env kernel's other search row layouts (u32 rows on two lane slots, u64 on
+# two, 128-bit rows on one) and the BFS channel on a non-square map
+WIDE_SHAPES = {
+    "w_n12_70x30_f9": dict(B=11, H=70, W=30, n=12, fov=9, nch=6, steps=60, map="rand"),
+    "w_n20_48x90_f11_bfsch": dict(B=5, H=48, W=90, n=20, fov=11, nch=7, steps=50, map="rand"),
+    "w_n10_96x60_f7_looping": dict(B=7, H=96, W=60, n=10, fov=7, nch=6, steps=50, map="rand", human="looping"),
+}
+
+
+@pytest.mark.parametrize("name", list(WIDE_SHAPES))
+def test_rollout_wide_row_layouts_match_oracle(name):
+    run_random_case(name, WIDE_SHAPES[name], "rollout", expect_rollout_kernel=2)
+
+
+@pytest.mark.parametrize("name", G1_NAMES)
+def test_rollout_on_fixed_episodes_equals_step_observe(name):
+    """The reference's fixed episodes (agent goal sequences, LoopingHuman or FixedPathHuman)
+    under the random policy: one mapf_rollout_random launch of T steps == T launches of
+    mapf_step_observe_random, on two envs reset alike (every slot's actions, outputs and
+    observation; state and BFS maps after) -- the rollout kernels' goal_mode 0 and human
+    modes 0 / 2, which the seeded cases do not reach."""
+    z = load(name)
+    n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
+    world = z["map"]
+    H, W = world.shape
+    hmode = int(z["human_mode"])
+    B = 9
+    envs = []
+    for _ in range(2):
+        e = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=nch, use_da=int(z["use_da"]),
+                   use_hp=int(z["use_hp"]), human_mode=hmode, goal_mode="sequence", fix_choice=1,
+                   max_seq=z["seq"].shape[1], max_human_seq=max(2, len(z["hseq"])), seed=77)
+        seqs = [z["seq"][i, :z["seq_len"][i]] for i in range(n)]
+        if hmode == 2:
+            e.reset_fixed(world, [seqs] * B, human_seq=[z["hseq"]] * B)
+        else:
+            e.reset_fixed(world, [seqs] * B, [z["hstart"]] * B, [z["hgoal"]] * B)
+        envs.append(e)
+    ro, so = envs
+    assert ro.rollout_fused, name
+    T = 40
+    dev = ro.device
+    acts = torch.zeros(T, B, n, dtype=torch.int32, device=dev)
+    obs = torch.full((T, B, n, nch, fov, fov), float("nan"), device=dev)
+    vec = torch.full((T, B, n, 4), float("nan"), device=dev)
+    out = {key: torch.full((T,) + tuple(v.shape), -7, dtype=v.dtype, device=dev) for key, v in ro.out.items()}
+    ro.rollout_random(T, slots=True, actions=acts, obs=obs, vec=vec, out=out)
+    out = host(out)
+    for t in range(T):
+        o_s, obs_s, vec_s = so.step_observe(random_policy=True)
+        o_s = host(o_s)
+        np.testing.assert_array_equal(acts[t].cpu().numpy(), so.actions.cpu().numpy(), err_msg=f"{name} t={t}")
+        for key in o_s:
+            np.testing.assert_array_equal(out[key][t], o_s[key], err_msg=f"{name} t={t} {key}")
+        assert torch.equal(obs[t], obs_s) and torch.equal(vec[t], vec_s), f"{name} t={t} obs"
+    sr, ss = ro.get_state(), so.get_state()
+    for key in ss:
+        np.testing.assert_array_equal(sr[key], ss[key], err_msg=f"{name} state {key}")
+    assert torch.equal(ro.bfs(), so.bfs())
+    assert (ro.counters()[:8] == so.counters()[:8]).all()
+
+
 @pytest.mark.parametrize("name,grid", [("c4_40x40_n16_f9_looping", 1), ("dense_12x12_n16_f9_dahp", 1),
                                        ("n7_24x24_f11_rand_dahp", 1), ("dense_12x12_n16_f9_dahp", 0)])
 def test_rollout_wide_one_wave_form_matches_oracle(name, grid, monkeypatch):
