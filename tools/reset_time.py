@@ -26,6 +26,5 @@ for cfg in os.environ.get("CFGS", "c2,c4,c5").split(","):
     env.reset_seeded(world)
     b.record()
     torch.cuda.synchronize()
-    print(f"{cfg}: reset_seeded {a.elapsed_time(b):.1f} ms ({B * N} BFS maps, {B} human paths x 2; "
-          f"MAPF_BFS_ALL={os.environ.get('MAPF_BFS_ALL', '1')})", flush=True)
+    print(f"{cfg}: reset_seeded {a.elapsed_time(b):.1f} ms ({B * N} BFS maps, {B} human paths x 2)", flush=True)
     env.close()
