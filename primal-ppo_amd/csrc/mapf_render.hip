@@ -87,6 +87,11 @@ __global__ __launch_bounds__(256) void render_kernel(DevEnv e, const int32_t *__
     const int b = envs[f];
     const int pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= FH * FW) return;
+    if (b < 0 || b >= e.B) {                            // not an env of this handle: a black frame
+        uint8_t *o = frames + ((size_t)f * FH * FW + pix) * 3;
+        o[0] = o[1] = o[2] = 0;
+        return;
+    }
     const int py = pix / FW, px = pix - py * FW;
     const int r = py / S, c = px / S;
     const uint32_t *bits = env_map(e, b);
