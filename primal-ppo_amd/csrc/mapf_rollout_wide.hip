@@ -202,7 +202,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         }
         WSTAMP(1);
         if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // B: snapshot t in LDS
-        if (stepper && inl.replan) {                     // the human's next path, into the other buffer
+        // the human's next path, into the other buffer (registers only: the observer may be
+        // using the scratch by now)
+        if (stepper && inl.replan) {
             const int len = srch::search_one<T, RW>(e, true, b, 0u, inl.rstart, inl.rgoal, inl.rbuf, scratch, L.mapc);
             if (inl.rbuf) rs.hl1 = len;
             else rs.hl0 = len;
