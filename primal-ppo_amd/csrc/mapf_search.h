@@ -80,11 +80,13 @@ __device__ inline uint64_t r_pop(uint64_t a) { return a & (a - 1ull); }
 __device__ inline Row2 r_pop(Row2 a) { return a.lo ? Row2{a.lo & (a.lo - 1ull), a.hi} : Row2{0ull, a.hi & (a.hi - 1ull)}; }
 
 // lane i <- lane i-1 (DPP wave_shr:1) / lane i <- lane i+1 (wave_shl:1); edge lanes read 0
+// (bound_ctrl: the edge lane writes 0 itself, so no zeroed destination is needed -- one
+// v_mov fewer per word and BFS level)
 __device__ inline uint32_t from_below(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);
 }
 __device__ inline uint32_t from_above(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, true);
 }
 __device__ inline uint64_t from_below(uint64_t x) {
     return ((uint64_t)from_below((uint32_t)(x >> 32)) << 32) | from_below((uint32_t)x);
