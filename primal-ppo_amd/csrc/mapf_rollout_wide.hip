@@ -37,6 +37,7 @@ struct WideOut {
     int slots;
     int xcd_remap;
     int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
+    int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
 };
 
 __host__ __device__ inline size_t wide_a16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -176,7 +177,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     // one loop for both forms (every function inlined once: the kernel's code stays
     // within the instruction cache); unpipelined, the one wave takes both roles in the
     // order step -> BFS maps -> snapshot -> human path -> observe
-    const bool stepper = !pipe || role == 0, observer = !pipe || role == 1;
+    bool stepper = !pipe || role == 0, observer = !pipe || role == 1;
+#ifdef MAPF_STAMPS
+    // phase-cost experiment (no observations written): the stepping role alone
+    if (ro.exp == 1) observer = false;
+#endif
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
@@ -262,6 +267,9 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     if (!pipe && wide_grid_bytes(e) <= wide_scratch_bytes<T, RW>(e)) r.grid = 2;
     else if (wide_lds_bytes<T, RW>(e, 1) <= (occ > 1 ? cap : (size_t)64 * 1024)) r.grid = 1;
     if (const char *v = std::getenv("MAPF_WIDE_GRID")) { if (std::atoi(v) == 0) r.grid = 0; }
+#ifdef MAPF_STAMPS
+    if (const char *v = std::getenv("MAPF_WIDE_EXP")) r.exp = std::atoi(v);
+#endif
     size_t lds = wide_lds_bytes<T, RW>(e, r.grid);
     if (cap > lds && cap <= 64 * 1024) lds = cap;
     hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, r);
@@ -284,7 +292,7 @@ void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut
                          int slots, hipStream_t s) {
     static int remap = -1;
     if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
-    const WideOut ro{actions, out, obs, vec, slots, remap, 0};
+    const WideOut ro{actions, out, obs, vec, slots, remap, 0, 0};
     with_row_type(e, [&](auto t, auto rw) { launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, s); return 0; });
 }
 
