@@ -109,9 +109,9 @@ __device__ inline void wide_sync() {
 // so a step's latency-bound chains run while the previous observation's stores issue.
 // BFS maps of step t are written between A (observation t-1, which reads the old maps,
 // is done) and B; both waves share one scratch area (the BFS image overlays the
-// observation's bit-stream, unused between A and B).  The stepper releases its stores
-// before each barrier; the observer arrives with no memory wait, so its stores keep
-// draining across the barriers.
+// observation's bit-stream, unused between A and B).  Only a step that rebuilt BFS maps
+// releases its global stores before B; otherwise neither wave waits on memory at a
+// barrier, so the observer's stores and the stepper's outputs keep draining across them.
 __device__ inline void wide_release_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
@@ -188,7 +188,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         StepInline inl;
         if (stepper) step_group<WaveGroup, true>(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs);
         WSTAMP(0);
-        if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // A: observation t-1 done
+        // A: observation t-1 done.  Nothing the observer reads from HBM was written by the step
+        // (its outputs and state are not read back), so the stepper does not wait for them.
+        if (pipe) wide_plain_barrier();
         if (stepper) {
             bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
             // snapshot of step t for the observation: cells, goals, the human's next cell from
@@ -206,7 +208,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
             }
         }
         WSTAMP(1);
-        if (pipe) { if (stepper) wide_release_barrier(); else wide_plain_barrier(); }   // B: snapshot t in LDS
+        // B: snapshot t in LDS; the stepper releases only when it rebuilt BFS maps (the
+        // observation's BFS channel reads them from HBM)
+        if (pipe) { if (stepper && inl.bmask) wide_release_barrier(); else wide_plain_barrier(); }
         // the human's next path, into the other buffer (registers only: the observer may be
         // using the scratch by now)
         if (stepper && inl.replan) {
