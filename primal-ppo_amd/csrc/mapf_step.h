@@ -128,8 +128,14 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     }
     const int hL2 = cur2 ? hl1 : hl0;
     const uint32_t *hpath2 = human_path(e, b, cur2);
-    const uint32_t hp_new = hpath2[hs2];
-    const uint32_t hn_new = hpath2[hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1];
+    // REGS (the persistent caller keeps everything else in registers / LDS): read the two path
+    // cells as vector loads.  Uniform addresses would make them scalar loads, counted in
+    // lgkmcnt with the LDS operations -- and the first LDS wait of the step would then wait
+    // for these HBM reads.
+    int vz = 0;
+    if constexpr (REGS) asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+    const uint32_t hp_new = hpath2[hs2 + vz];
+    const uint32_t hn_new = hpath2[(hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1) + vz];
 
     // ---- state -----------------------------------------------------------
     const uint32_t pp = REGS ? rg.pp : (act ? e.pos[ai] : 0xFFFFFFFFu);
