@@ -382,9 +382,9 @@ def main():
         paths = {}
         if env.fused:
             paths["step_observe"] = entry(fused_ms, bpa_f, f"HIP events, {KS} direct launches")
-        else:
-            paths["split"] = entry(step_ms + search_ms + obs_ms, bpa_f,
-                                   f"HIP events, {KS} x (step, search, observe) launches")
+        else:   # mapf_step_observe = step launch, then observe with the step's search forked beside it
+            paths["split"] = entry(fused_ms, bpa_f, f"HIP events around {KS} mapf_step_observe calls (step, "
+                                                    f"observe + forked search; breakdown_ms.split has them serial)")
         if env.rollout_fused:
             if roll is None:
                 paths["rollout_inplace"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
