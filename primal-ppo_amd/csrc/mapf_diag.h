@@ -42,13 +42,15 @@ __device__ inline uint64_t stamp_rt() {   // constant-rate 100 MHz counter
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_x)); \
     e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 6] = _h; e.prof[PROF_TL + (size_t)blockIdx.x * 8 + 7] = _x; } } while (0)
 // wide rollout kernel: phase time (100 MHz ticks) per env summed over the launch's steps, written to
-// prof[PROF_TL + b * 8 + k] (k < 6; slot 7 = 1) by lane 0 of env b's wave
+// prof[PROF_TL + row * 8 + k] (k < 6; slot 7 = 1) by lane 0 of env b's first wave (row b) and, in
+// the pipelined form, of its observing wave (row B + b)
 #define WSTAMP_BEGIN() uint64_t _w_prev = stamp_rt(); uint64_t _w_d[6] = {0, 0, 0, 0, 0, 0}
 #define WSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const uint64_t _t = stamp_rt(); \
     _w_d[k] += _t - _w_prev; _w_prev = _t; __builtin_amdgcn_sched_barrier(0); } while (0)
-#define WSTAMP_END(b) do { if ((threadIdx.x & 63) == 0 && (size_t)(b) < PROF_TL_BLOCKS) { \
-    for (int _k = 0; _k < 6; ++_k) e.prof[PROF_TL + (size_t)(b) * 8 + _k] = _w_d[_k]; \
-    e.prof[PROF_TL + (size_t)(b) * 8 + 7] = 1; } } while (0)
+#define WSTAMP_END(b) do { const size_t _row = (size_t)(b) + (threadIdx.x >> 6) * (size_t)e.B; \
+    if ((threadIdx.x & 63) == 0 && _row < PROF_TL_BLOCKS) { \
+    for (int _k = 0; _k < 6; ++_k) e.prof[PROF_TL + _row * 8 + _k] = _w_d[_k]; \
+    e.prof[PROF_TL + _row * 8 + 7] = 1; } } while (0)
 #else
 #define WSTAMP_BEGIN() do { } while (0)
 #define WSTAMP(k) do { } while (0)

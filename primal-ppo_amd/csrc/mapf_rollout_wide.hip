@@ -37,6 +37,7 @@ struct WideOut {
     int slots;
     int xcd_remap;
     int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
+    int overlap;        // pipelined, no BFS channel: one barrier per step (wide_overlap_bytes)
     int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
 };
 
@@ -62,11 +63,19 @@ __host__ __device__ inline size_t wide_cost_bytes(const DevEnv &e) {
 
 __host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide_a16((size_t)(e.H + 4) * (e.W + 4)); }
 
-// nibble table (256 B) | map rows | cost table | [neighbour grid] | scratch
+// the overlapped pipeline's own areas: a second observation snapshot (spos | sgoal | shn |
+// shp | shpn) and the stepper's BFS image
+__host__ __device__ inline size_t wide_snap_bytes(const DevEnv &e) { return wide_a16((size_t)(2 * e.N + 2 + e.k_predict) * 4); }
 template <class T, int RW>
-__host__ __device__ inline size_t wide_lds_bytes(const DevEnv &e, int grid = 0) {
+__host__ __device__ inline size_t wide_overlap_bytes(const DevEnv &e) {
+    return wide_snap_bytes(e) + srch::wave_lds<T, RW>(e.H, e.W);
+}
+
+// nibble table (256 B) | map rows | cost table | [neighbour grid] | scratch | [snapshot 1 | BFS image]
+template <class T, int RW>
+__host__ __device__ inline size_t wide_lds_bytes(const DevEnv &e, int grid = 0, bool overlap = false) {
     return 256 + wide_a16((size_t)e.Hp * e.WW * 4) + wide_cost_bytes(e) + (grid == 1 ? wide_grid_bytes(e) : 0) +
-           wide_scratch_bytes<T, RW>(e);
+           wide_scratch_bytes<T, RW>(e) + (overlap ? wide_overlap_bytes<T, RW>(e) : 0);
 }
 
 __device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, int gmode, char *&scratch, float *&cost,
@@ -112,6 +121,11 @@ __device__ inline void wide_sync() {
 // observation's bit-stream, unused between A and B).  Only a step that rebuilt BFS maps
 // releases its global stores before B; otherwise neither wave waits on memory at a
 // barrier, so the observer's stores and the stepper's outputs keep draining across them.
+// Overlapped (no BFS channel, so the observation reads no BFS map): the stepper searches in
+// its own BFS image and writes snapshot t into copy t & 1, so one barrier per step suffices,
+//     stepper  | human path t-1 | step t | BFS maps t | snapshot t | B | human path t | ...
+//     observer |        observe t-1                               | B | observe t    | ...
+// and a step costs max(stepper, observer) instead of their sum over the A..B segment.
 __device__ inline void wide_release_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
@@ -142,6 +156,18 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     float *lcost;
     uint8_t *grid;
     ObsLds L = wide_layout(e, smem, ro.grid, scratch, lcost, grid);
+    const bool ovl = pipe && ro.overlap;
+    ObsLds L1 = L;                                     // snapshot copy 1 (overlapped form)
+    char *bimg = scratch;                              // where the stepper's BFS maps search
+    if (ovl) {
+        char *x = scratch + wide_scratch_bytes<T, RW>(e);
+        L1.spos = reinterpret_cast<uint32_t *>(x);
+        L1.sgoal = L1.spos + e.N;
+        L1.shn = L1.sgoal + e.N;
+        L1.shp = L1.shn + 1;
+        L1.shpn = reinterpret_cast<int32_t *>(L1.shp + e.k_predict);
+        bimg = x + wide_snap_bytes(e);
+    }
     obs_lut_init(const_cast<float4 *>(L.lut));
     const uint32_t *mb = env_map(e, b);
     for (int k = (int)threadIdx.x; k < L.rowsz; k += (int)blockDim.x) L.mapc[k] = mb[k];
@@ -170,7 +196,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         for (uint64_t m = inl.bmask; m; m &= m - 1ull) {
             const int l = ctz64(m);
             const uint32_t gl = (uint32_t)__builtin_amdgcn_readlane((int)inl.goal, l);
-            srch::search_one<T, RW>(e, false, b, (uint32_t)b * (uint32_t)e.N + (uint32_t)l, gl, NO_CELL, 0, scratch,
+            srch::search_one<T, RW>(e, false, b, (uint32_t)b * (uint32_t)e.N + (uint32_t)l, gl, NO_CELL, 0, bimg,
                                     L.mapc);
         }
     };
@@ -190,27 +216,25 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         WSTAMP(0);
         // A: observation t-1 done.  Nothing the observer reads from HBM was written by the step
         // (its outputs and state are not read back), so the stepper does not wait for them.
-        if (pipe) wide_plain_barrier();
+        if (pipe && !ovl) wide_plain_barrier();
+        const ObsLds &Lt = (ovl && (t & 1)) ? L1 : L;   // this step's snapshot
         if (stepper) {
             bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
-            // snapshot of step t for the observation: cells, goals, the human's next cell from
-            // the registers, the human's path cells (HP channel) from HBM
-            if (lane < e.N) { L.spos[lane] = rs.pp; L.sgoal[lane] = rs.gg; }
+            // snapshot of step t for the observation, all from the registers: cells, goals,
+            // the human's next cell and path cells [1..K] (HP channel)
+            if (lane < e.N) { Lt.spos[lane] = rs.pp; Lt.sgoal[lane] = rs.gg; }
+            const bool hp_ch = e.use_hp && e.C >= 6;
+            if (hp_ch && rs.hq != NO_CELL) Lt.shp[lane - 1] = rs.hq;
             if (lane == 0) {
-                L.shn[0] = rs.hn;
-                int cnt = 0;
-                if (e.use_hp && e.C >= 6) {
-                    const int len = rs.hcur ? rs.hl1 : rs.hl0;
-                    const uint32_t *path = human_path(e, b, rs.hcur);
-                    for (int q = 1; q <= e.k_predict && q < len; ++q) L.shp[cnt++] = path[q];
-                }
-                L.shpn[0] = cnt;
+                Lt.shn[0] = rs.hn;
+                const int len = rs.hcur ? rs.hl1 : rs.hl0;
+                Lt.shpn[0] = hp_ch ? max(0, min(e.k_predict, len - 1)) : 0;
             }
         }
         WSTAMP(1);
         // B: snapshot t in LDS; the stepper releases only when it rebuilt BFS maps (the
         // observation's BFS channel reads them from HBM)
-        if (pipe) { if (stepper && inl.bmask) wide_release_barrier(); else wide_plain_barrier(); }
+        if (pipe) { if (stepper && inl.bmask && !ovl) wide_release_barrier(); else wide_plain_barrier(); }
         // the human's next path, into the other buffer (registers only: the observer may be
         // using the scratch by now)
         if (stepper && inl.replan) {
@@ -223,7 +247,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
             wide_sync();
             const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
-            obs_emit<true, NT>(e, L, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
+            obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
         }
         WSTAMP(3);
@@ -271,10 +295,13 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     if (!pipe && wide_grid_bytes(e) <= wide_scratch_bytes<T, RW>(e)) r.grid = 2;
     else if (wide_lds_bytes<T, RW>(e, 1) <= (occ > 1 ? cap : (size_t)64 * 1024)) r.grid = 1;
     if (const char *v = std::getenv("MAPF_WIDE_GRID")) { if (std::atoi(v) == 0) r.grid = 0; }
+    // one barrier per step where the observation reads no BFS map and the extra LDS fits
+    r.overlap = pipe && e.C < 7 && wide_lds_bytes<T, RW>(e, r.grid, true) <= (occ > 1 ? cap : (size_t)64 * 1024);
+    if (const char *v = std::getenv("MAPF_WIDE_OVERLAP")) r.overlap = r.overlap && std::atoi(v) != 0;
 #ifdef MAPF_STAMPS
     if (const char *v = std::getenv("MAPF_WIDE_EXP")) r.exp = std::atoi(v);
 #endif
-    size_t lds = wide_lds_bytes<T, RW>(e, r.grid);
+    size_t lds = wide_lds_bytes<T, RW>(e, r.grid, r.overlap);
     if (cap > lds && cap <= 64 * 1024) lds = cap;
     hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, r);
 }
@@ -296,7 +323,7 @@ void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut
                          int slots, hipStream_t s) {
     static int remap = -1;
     if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
-    const WideOut ro{actions, out, obs, vec, slots, remap, 0, 0};
+    const WideOut ro{actions, out, obs, vec, slots, remap, 0, 0, 0};
     with_row_type(e, [&](auto t, auto rw) { launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, s); return 0; });
 }
 

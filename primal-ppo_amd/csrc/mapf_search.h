@@ -238,6 +238,69 @@ __device__ inline uint32_t row_bit(const T (&m)[RW], int sl, int ln, int c) {
     return ((uint32_t)__builtin_amdgcn_readlane((int)w, ln) >> (c & 31)) & 1u;
 }
 
+// byte t (cells 8t .. 8t+7) of a row mask
+__device__ inline uint32_t row_byte(uint32_t x, int t) { return (x >> (8 * t)) & 0xFFu; }
+__device__ inline uint32_t row_byte(uint64_t x, int t) { return (uint32_t)(x >> (8 * t)) & 0xFFu; }
+__device__ inline uint32_t row_byte(Row2 x, int t) { return row_byte(t < 8 ? x.lo : x.hi, t & 7); }
+
+// 8 x 8 bit-matrix transpose: bit j of byte i <-> bit i of byte j
+__device__ inline uint64_t transpose8(uint64_t x) {
+    uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x ^= t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x ^= t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    return x ^ t ^ (t << 28);
+}
+
+// makeBfsMap out of registers: the distance bit planes D (bfs_planes), visited V and free
+// rows `fre` of the rows this lane holds, decoded straight into the 8x8 tiles (bfs_at) --
+// one 16-B store per tile row, issued by the lane holding that row.  Per tile row: the
+// byte of each plane over its 8 cells, one 8 x 8 transpose per 8 planes (cell j's
+// distance bits), then -2 / -1 for the unreached free / obstacle cells.  Replaces the
+// level-by-level LDS image, whose per-level cell stores (a divergent loop per level) set
+// the BFS's pace.
+template <class T, int RW, int K>
+__device__ inline void planes_to_tiles(const T (&V)[RW], const T (&fre)[RW], const T (&D)[K][RW], int kq, int H,
+                                       int W, uint4 *__restrict__ dst) {
+    const int lane = lane_id();
+    const int TW = bfs_tw(W), rows = ((H + 7) >> 3) << 3;
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const int r = lane + 64 * k;
+        if (r >= rows) continue;                     // rows H .. rows-1 decode to -1 (no free / visited bits)
+        uint4 *row = dst + (size_t)(r >> 3) * TW * 8 + (r & 7);
+        for (int tc = 0; tc < TW; ++tc) {
+            const uint32_t un = ~row_byte(V[k], tc) & 0xFFu, fb = row_byte(fre[k], tc);
+            uint64_t lo = 0, hi = 0;
+#pragma unroll
+            for (int q = 0; q < (K < 8 ? K : 8); ++q) lo |= (uint64_t)row_byte(D[q][k], tc) << (8 * q);
+            lo = transpose8(lo);
+            if (K > 8 && kq > 8) {
+#pragma unroll
+                for (int q = 8; q < K; ++q) hi |= (uint64_t)row_byte(D[q][k], tc) << (8 * (q - 8));
+                hi = transpose8(hi);
+            }
+            uint32_t o[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t lw = (uint32_t)(lo >> (32 * (m >> 1))), hw = (uint32_t)(hi >> (32 * (m >> 1)));
+                const int a = (2 * m) & 3, j = 2 * m;
+                const uint32_t x = ((lw >> (8 * a)) & 0xFFu) | (((hw >> (8 * a)) & 0xFFu) << 8) |
+                                   (((lw >> (8 * a + 8)) & 0xFFu) << 16) | (((hw >> (8 * a + 8)) & 0xFFu) << 24);
+                const uint32_t um = (((un >> j) & 1u) ? 0xFFFFu : 0u) | (((un >> (j + 1)) & 1u) ? 0xFFFF0000u : 0u);
+                const uint32_t fm = ((fb >> j) & 1u) | (((fb >> (j + 1)) & 1u) << 16);
+                o[m] = x | (um & ~fm);                 // unreached: free -2, obstacle -1
+            }
+            row[tc * 8] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
+}
+
+// distance planes of the register BFS map of u64 / two-u64 rows: distances < 512 (mazes
+// deeper than that take the LDS image)
+constexpr int KWIDE = 9;
+
 // LDS bytes one wave needs
 template <class T, int RW>
 __host__ __device__ inline size_t wave_lds(int H, int W) {
@@ -273,32 +336,22 @@ __device__ __attribute__((always_inline)) inline int search_one(const DevEnv &e,
         }
         const int sr = prow(sr_cell), sc = pcol(sr_cell);
         if (!replan) {
-            // the map copy (-1 obstacle / -2 free), then the BFS levels on top, then one
-            // coalesced sweep out
-            int16_t *img = reinterpret_cast<int16_t *>(lds);
-            if constexpr (sizeof(T) == 4) {
-                // narrow rows (shallow BFS): distances as bit planes in registers, decoded per row
-                T V[RW], D[KNARROW][RW];
-                const int maxd = bfs_planes<T, RW, KNARROW>(fre, sr, sc, -1, -1, V, D);
-                const int kq = 32 - __builtin_clz((unsigned)maxd | 1u);   // planes in use
-#pragma unroll
-                for (int k = 0; k < RW; ++k) {
-                    const int r = lane + 64 * k;
-                    if (r < H)
-                        for (int c = 0; c < W; ++c) {
-                            int v;
-                            if (r_get(V[k], c)) {
-                                v = 0;
-#pragma unroll
-                                for (int q = 0; q < KNARROW; ++q)
-                                    if (q < kq) v |= (int)r_get(D[q][k], c) << q;
-                            } else {
-                                v = r_get(fre[k], c) ? -2 : -1;
-                            }
-                            img[r * W + c] = (int16_t)v;
-                        }
+            uint4 *dst = reinterpret_cast<uint4 *>(e.bfs + (size_t)ai * bfs_cells(H, W));
+            // distances as bit planes in registers, decoded straight into the tiles
+            constexpr int K = sizeof(T) == 4 ? KNARROW : KWIDE;
+            bool done = false;
+            {
+                T V[RW], D[K][RW];
+                const int maxd = bfs_planes<T, RW, K>(fre, sr, sc, -1, -1, V, D);
+                if (sizeof(T) == 4 || maxd < (1 << K)) {
+                    planes_to_tiles<T, RW, K>(V, fre, D, 32 - __builtin_clz((unsigned)maxd | 1u), H, W, dst);
+                    done = true;
                 }
-            } else {
+            }
+            if (!done) {
+                // deeper than the planes hold: the map copy (-1 obstacle / -2 free) in an LDS
+                // image, the BFS levels on top, then one coalesced sweep out
+                int16_t *img = reinterpret_cast<int16_t *>(lds);
 #pragma unroll
                 for (int k = 0; k < RW; ++k) {
                     const int r = lane + 64 * k;
@@ -308,29 +361,28 @@ __device__ __attribute__((always_inline)) inline int search_one(const DevEnv &e,
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 bfs_to_img<T, RW>(fre, sr, sc, img, W);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            // out in 8x8 tiles (bfs_at): one 16-B store per tile row, -1 past the map's edge
-            uint4 *dst = reinterpret_cast<uint4 *>(e.bfs + (size_t)ai * bfs_cells(H, W));
-            const int TW = bfs_tw(W), nrows = (int)(bfs_cells(H, W) >> 3);
-            for (int k = lane; k < nrows; k += 64) {
-                const int t = k >> 3, r = ((t / TW) << 3) | (k & 7), c0 = (t % TW) << 3;
-                uint4 v;
-                if ((W & 7) == 0 && r < H) {
-                    v = *reinterpret_cast<const uint4 *>(img + r * W + c0);
-                } else {
-                    uint32_t q[4];
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // out in 8x8 tiles (bfs_at): one 16-B store per tile row, -1 past the map's edge
+                const int TW = bfs_tw(W), nrows = (int)(bfs_cells(H, W) >> 3);
+                for (int k = lane; k < nrows; k += 64) {
+                    const int t = k >> 3, r = ((t / TW) << 3) | (k & 7), c0 = (t % TW) << 3;
+                    uint4 v;
+                    if ((W & 7) == 0 && r < H) {
+                        v = *reinterpret_cast<const uint4 *>(img + r * W + c0);
+                    } else {
+                        uint32_t q[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int ca = c0 + 2 * j, cb = ca + 1;
-                        const uint32_t lo = (r < H && ca < W) ? (uint16_t)img[r * W + ca] : 0xFFFFu;
-                        const uint32_t hi = (r < H && cb < W) ? (uint16_t)img[r * W + cb] : 0xFFFFu;
-                        q[j] = lo | (hi << 16);
+                        for (int j = 0; j < 4; ++j) {
+                            const int ca = c0 + 2 * j, cb = ca + 1;
+                            const uint32_t lo = (r < H && ca < W) ? (uint16_t)img[r * W + ca] : 0xFFFFu;
+                            const uint32_t hi = (r < H && cb < W) ? (uint16_t)img[r * W + cb] : 0xFFFFu;
+                            q[j] = lo | (hi << 16);
+                        }
+                        v = make_uint4(q[0], q[1], q[2], q[3]);
                     }
-                    v = make_uint4(q[0], q[1], q[2], q[3]);
+                    dst[k] = v;
                 }
-                dst[k] = v;
             }
         } else {
             const int gr = prow(stop_cell), gc = pcol(stop_cell);

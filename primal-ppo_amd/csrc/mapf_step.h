@@ -49,6 +49,7 @@ struct StepRegs {
     int la;              // per lane: its last action (-1 none)
     uint32_t clock, hp, hn;
     int hs, hcur, hl0, hl1;
+    uint32_t hq;         // per lane q in 1..k_predict: human.path[q] after the step (NO_CELL past its end)
 };
 
 __device__ inline void step_regs_load(const DevEnv &e, int b, int i, StepRegs &r) {
@@ -64,7 +65,37 @@ __device__ inline void step_regs_load(const DevEnv &e, int b, int i, StepRegs &r
     r.hcur = e.hcur[b];
     r.hl0 = e.hlen[b * 2];
     r.hl1 = e.hlen[b * 2 + 1];
+    r.hq = NO_CELL;
 }
+
+// The cells within distance 2 of an agent (the neighbour grid's 12 slots) and, per slot, the
+// folded pair tests of step_group (keys / conflicts of an agent there, see pair()).
+constexpr int NBR_DR[12] = {-2, -1, -1, -1, 0, 0, 0, 0, 1, 1, 1, 2};
+constexpr int NBR_DC[12] = {0, -1, 0, 1, -2, -1, 1, 2, -1, 0, 1, 0};
+constexpr int cabs(int x) { return x < 0 ? -x : x; }
+constexpr unsigned nbr_keys(int R, int C) {
+    unsigned m = 0;
+    for (int t = 0; t < NA; ++t)
+        if (cabs(dr(t) - R) + cabs(dc(t) - C) <= 1) m |= 1u << t;
+    return m;
+}
+constexpr uint32_t nbr_conf(int R, int C) {
+    uint32_t tab = 0;
+    for (int aj = 0; aj < NA; ++aj) {
+        const int YR = R + dr(aj), YC = C + dc(aj);
+        for (int t = 0; t < NA; ++t)
+            if ((dr(t) == YR && dc(t) == YC) || (dr(t) == R && dc(t) == C && YR == 0 && YC == 0))
+                tab |= 1u << (5 * aj + t);
+    }
+    return tab;
+}
+#define MAPF_NBR12(F) {F(NBR_DR[0], NBR_DC[0]), F(NBR_DR[1], NBR_DC[1]), F(NBR_DR[2], NBR_DC[2]), \
+    F(NBR_DR[3], NBR_DC[3]), F(NBR_DR[4], NBR_DC[4]), F(NBR_DR[5], NBR_DC[5]), F(NBR_DR[6], NBR_DC[6]), \
+    F(NBR_DR[7], NBR_DC[7]), F(NBR_DR[8], NBR_DC[8]), F(NBR_DR[9], NBR_DC[9]), F(NBR_DR[10], NBR_DC[10]), \
+    F(NBR_DR[11], NBR_DC[11])}
+constexpr unsigned NKEYS[12] = MAPF_NBR12(nbr_keys);
+constexpr uint32_t NCONF[12] = MAPF_NBR12(nbr_conf);
+#undef MAPF_NBR12
 
 struct StepSrc {
     const uint32_t *map = nullptr;
@@ -136,6 +167,9 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     if constexpr (REGS) asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
     const uint32_t hp_new = hpath2[hs2 + vz];
     const uint32_t hn_new = hpath2[(hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1) + vz];
+    // and the observation's predicted cells human.path[1..K] (getObservations :293-297), in
+    // the same round: read after the step's output stores they would wait for those stores
+    if constexpr (REGS) rg.hq = (i >= 1 && i <= e.k_predict && i < hL2) ? hpath2[i] : NO_CELL;
 
     // ---- state -----------------------------------------------------------
     const uint32_t pp = REGS ? rg.pp : (act ? e.pos[ai] : 0xFFFFFFFFu);
@@ -219,16 +253,22 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         if (act) grid[me] = (uint8_t)i;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        constexpr int ODR[12] = {-2, -1, -1, -1, 0, 0, 0, 0, 1, 1, 1, 2};
-        constexpr int ODC[12] = {0, -1, 0, 1, -2, -1, 1, 2, -1, 0, 1, 0};
+        // A neighbour's offset is fixed by its slot, so pair()'s tests fold into constants:
+        // NKEYS[o] = the keys it contributes, NCONF[o] bits 5aj..5aj+4 = my actions colliding
+        // with its action aj (same target, or a swap).
         int nb[12];
 #pragma unroll
-        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)grid[me + ODR[o] * GW + ODC[o]] : 0xFF;
+        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)grid[me + NBR_DR[o] * GW + NBR_DC[o]] : 0xFF;
 #pragma unroll
         for (int o = 0; o < 12; ++o) {
             const int j = nb[o];
             const int aj = (int)shfl32((uint32_t)a, j == 0xFF ? lane : j);   // every lane permutes
-            if (j != 0xFF) pair(j, pr + ODR[o], pc + ODC[o], aj);
+            if (j != 0xFF) {
+                const unsigned cj = (NCONF[o] >> (5 * aj)) & 0x1Fu;
+                keys |= NKEYS[o];
+                conf |= cj;
+                if ((cj >> a) & 1u) M |= 1ull << j;
+            }
         }
     } else {
         for (int j = 0; j < N; ++j) {
