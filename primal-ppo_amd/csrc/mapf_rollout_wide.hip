@@ -17,8 +17,9 @@
 // wave searching an 80 x 80 map for ~100 us holds back only its own env while
 // the other waves' observation stores keep HBM busy.
 //
-// State stays in HBM between steps (the step reads and writes it as the per-step
-// kernel does; a wave's own stores are visible to its later loads).  LDS per wave:
+// The stepping wave keeps the env's state in registers (StepRegs) and stores it to HBM
+// once, after its last step; the human's path buffers and lengths, the work the step
+// reads back, stay in HBM (a wave's own stores are visible to its later loads).  LDS per wave:
 // the nibble table, the env's padded map rows, and one scratch area shared by the
 // observation (bit-stream, occupancy, agent grid) and the search (BFS image).
 #include <cstdlib>
@@ -252,6 +253,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         }
         WSTAMP(3);
     }
+    if (stepper) step_regs_store(e, b, lane, rs);
     WSTAMP_END(b);
 }
 

@@ -97,6 +97,23 @@ constexpr unsigned NKEYS[12] = MAPF_NBR12(nbr_keys);
 constexpr uint32_t NCONF[12] = MAPF_NBR12(nbr_conf);
 #undef MAPF_NBR12
 
+// the registers back to HBM (the REGS caller, once after its last step)
+__device__ inline void step_regs_store(const DevEnv &e, int b, int i, const StepRegs &r) {
+    if (i < e.N) {
+        const size_t ai = (size_t)b * e.N + i;
+        e.pos[ai] = r.pp;
+        e.goal[ai] = r.gg;
+        e.last_act[ai] = (int8_t)r.la;
+    }
+    if (i == 0) {
+        e.hcur[b] = r.hcur;
+        e.hstep[b] = r.hs;
+        e.hpos[b] = r.hp;
+        e.hnext[b] = r.hn;
+        e.clock[b] = r.clock;
+    }
+}
+
 struct StepSrc {
     const uint32_t *map = nullptr;
     const float *cost = nullptr;
@@ -479,9 +496,11 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         }
     }
     if (act) {
-        e.pos[ai] = np;
-        e.goal[ai] = ng;
-        e.last_act[ai] = (int8_t)fixed;
+        if constexpr (!REGS) {      // REGS: the caller stores the registers once, at its end
+            e.pos[ai] = np;
+            e.goal[ai] = ng;
+            e.last_act[ai] = (int8_t)fixed;
+        }
         if (reached && e.keep_bfs && !inl) {
             const uint32_t slot = atomicAdd(&e.counters[C_BFS_COUNT + parity], 1u);
             e.bfs_list[(size_t)parity * e.B * N + slot] = (uint32_t)ai;
@@ -514,7 +533,7 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
                 }
             }
         }
-        if (i == 0) {
+        if (!REGS && i == 0) {
             e.hcur[b] = cur2;
             e.hstep[b] = hs2;
             e.hpos[b] = hp_new;
