@@ -177,6 +177,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     __syncthreads();
     StepRegs rs;                           // the stepping wave keeps the env's state in registers
     step_regs_load(e, b, lane, rs);
+    // the registers' loads done before the loop: with one still counted at the loop header,
+    // the top of every step waited vmcnt(0), i.e. for the previous step's output stores too
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt/lgkmcnt untouched
     const StepSrc src{L.mapc, lcost, grid};   // obstacle tests, cost table, neighbour grid in LDS
     const WaveGroup g;                     // the env is the whole wave: exchanges by v_readlane
     const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;

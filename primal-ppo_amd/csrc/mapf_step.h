@@ -218,10 +218,14 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     unsigned st_mask = 0x1Fu;
     if (act) {
         if (REGS) {
+            // an agent's four neighbours lie inside the padded rows (P >= 1, mapf_api.cpp), so
+            // the five words load with no bounds test: five reads in flight, one wait
             st_mask = 0;
+            uint32_t w[NA];
 #pragma unroll
-            for (int k = 0; k < NA; ++k)
-                if (obstacle(pr + dr(k), pc + dc(k))) st_mask |= 1u << k;
+            for (int k = 0; k < NA; ++k) w[k] = lmap[(pr + dr(k) + e.P) * e.WW + ((pc + dc(k) + e.P) >> 5)];
+#pragma unroll
+            for (int k = 0; k < NA; ++k) st_mask |= ((w[k] >> ((pc + dc(k) + e.P) & 31)) & 1u) << k;
         } else {
             st_mask = e.smask[(e.shared_map ? 0 : (size_t)b * e.H * e.W) + pr * e.W + pc];
         }
@@ -273,19 +277,20 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         // A neighbour's offset is fixed by its slot, so pair()'s tests fold into constants:
         // NKEYS[o] = the keys it contributes, NCONF[o] bits 5aj..5aj+4 = my actions colliding
         // with its action aj (same target, or a swap).
-        int nb[12];
+        // All twelve permutes issue back to back (every lane permutes), then one wait and a
+        // branch-free fold: interleaved with per-slot branches, each waited on its own.
+        int nb[12], aj[12];
 #pragma unroll
         for (int o = 0; o < 12; ++o) nb[o] = act ? (int)grid[me + NBR_DR[o] * GW + NBR_DC[o]] : 0xFF;
 #pragma unroll
+        for (int o = 0; o < 12; ++o) aj[o] = (int)shfl32((uint32_t)a, nb[o] == 0xFF ? lane : nb[o]);
+#pragma unroll
         for (int o = 0; o < 12; ++o) {
-            const int j = nb[o];
-            const int aj = (int)shfl32((uint32_t)a, j == 0xFF ? lane : j);   // every lane permutes
-            if (j != 0xFF) {
-                const unsigned cj = (NCONF[o] >> (5 * aj)) & 0x1Fu;
-                keys |= NKEYS[o];
-                conf |= cj;
-                if ((cj >> a) & 1u) M |= 1ull << j;
-            }
+            const bool h = nb[o] != 0xFF;
+            const unsigned cj = h ? (NCONF[o] >> (5 * aj[o])) & 0x1Fu : 0u;
+            keys |= h ? NKEYS[o] : 0u;
+            conf |= cj;
+            M |= (uint64_t)((cj >> a) & 1u) << (nb[o] & 63);
         }
     } else {
         for (int j = 0; j < N; ++j) {
@@ -332,17 +337,26 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const uint64_t shadow_mask = g.ballot(shadow_hit);
 
     // ---- calculateCostReward (:528-533): pre-step human next position -------
-    float cost = 0.f;
-    {
-        const int d0 = prow(hn) - Xr, d1 = pcol(hn) - Xc;
-        const int d2 = d0 * d0 + d1 * d1;
-        if (d2 <= e.R * e.R) cost = (REGS && src.cost) ? as_lds(src.cost)[d2] : e.cost_lut[d2];
+    // REGS callers with the table in LDS never touch the HBM copy: a value that MAY come
+    // from a global load makes every later use (and every reuse of its register) wait
+    // vmcnt(0), i.e. for the whole step's stores, even on the LDS path.
+    const int cd0 = prow(hn) - Xr, cd1 = pcol(hn) - Xc;
+    const int cd2 = cd0 * cd0 + cd1 * cd1;
+    const bool cin = cd2 <= e.R * e.R;
+    if (act && out.cost) {
+        if (REGS && src.cost) {
+            out.cost[ai] = cin ? as_lds(src.cost)[cd2] : 0.f;
+        } else {
+            const float c = cin ? e.cost_lut[cd2] : 0.f;
+            // REGS: the load's wait here, on this path only, so nothing is pending at the join
+            if constexpr (REGS) __builtin_amdgcn_s_waitcnt(0x0F70);
+            out.cost[ai] = c;
+        }
     }
 
     if (act) {
         if (out.status) out.status[ai] = (int8_t)st;
         if (out.reward) out.reward[ai] = rw;
-        if (out.cost) out.cost[ai] = cost;
         if (out.train_valid) {   // getTrainValid (:535-550)
             float *tv = out.train_valid + ai * NA;
 #pragma unroll
