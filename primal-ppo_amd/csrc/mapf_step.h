@@ -325,14 +325,11 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const int st = ((T >> i) & 1ull) ? -3 : s0;
 
     // ---- calculateActionReward (:483-511) ----------------------------------
-    float rw;
-    switch (st) {
-        case -1: rw = e.collision_cost; break;
-        case -2: rw = e.human_collision_cost; break;
-        case -3: rw = e.collision_cost; break;
-        case -4: rw = e.repeat_cost; break;
-        default: rw = e.action_cost; break;
-    }
+    // selects, not a switch: each case's branch reloaded the env's spilled scalars
+    float rw = e.action_cost;
+    rw = st == -4 ? e.repeat_cost : rw;
+    rw = (st == -1 || st == -3) ? e.collision_cost : rw;
+    rw = st == -2 ? e.human_collision_cost : rw;
     const bool shadow_hit = act && st == 1 && Xr == prow(gg) && Xc == pcol(gg);
     const uint64_t shadow_mask = g.ballot(shadow_hit);
 
