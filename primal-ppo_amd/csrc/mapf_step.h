@@ -266,8 +266,10 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         const int GW = e.W + 4, gwords = ((e.H + 4) * GW + 3) >> 2;
         const int lane = lane_id();
         const auto grid = as_lds(src.grid);
-        const auto grid32 = as_lds(reinterpret_cast<uint32_t *>(src.grid));
-        for (int k = lane; k < gwords; k += 64) grid32[k] = 0xFFFFFFFFu;
+        // cleared 16 B per lane (the grid's LDS area is 16-B aligned and padded to 16 B)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const auto grid128 = as_lds(reinterpret_cast<u32x4 *>(src.grid));
+        for (int k = lane; k < ((gwords + 3) >> 2); k += 64) grid128[k] = u32x4(0xFFFFFFFFu);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int me = (pr + 2) * GW + pc + 2;
