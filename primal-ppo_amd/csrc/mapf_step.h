@@ -272,7 +272,8 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         for (int k = lane; k < ((gwords + 3) >> 2); k += 64) grid128[k] = u32x4(0xFFFFFFFFu);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const int me = (pr + 2) * GW + pc + 2;
+        // lanes past N read around the grid's cell (0, 0) (result dropped): no branch per read
+        const int me = act ? (pr + 2) * GW + pc + 2 : 2 * GW + 2;
         if (act) grid[me] = (uint8_t)i;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -283,7 +284,10 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         // branch-free fold: interleaved with per-slot branches, each waited on its own.
         int nb[12], aj[12];
 #pragma unroll
-        for (int o = 0; o < 12; ++o) nb[o] = act ? (int)grid[me + NBR_DR[o] * GW + NBR_DC[o]] : 0xFF;
+        for (int o = 0; o < 12; ++o) {
+            const int v = (int)grid[me + NBR_DR[o] * GW + NBR_DC[o]];
+            nb[o] = act ? v : 0xFF;
+        }
 #pragma unroll
         for (int o = 0; o < 12; ++o) aj[o] = (int)shfl32((uint32_t)a, nb[o] == 0xFF ? lane : nb[o]);
 #pragma unroll
