@@ -331,11 +331,16 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const int st = ((T >> i) & 1ull) ? -3 : s0;
 
     // ---- calculateActionReward (:483-511) ----------------------------------
-    // selects, not a switch: each case's branch reloaded the env's spilled scalars
-    float rw = e.action_cost;
-    rw = st == -4 ? e.repeat_cost : rw;
-    rw = (st == -1 || st == -3) ? e.collision_cost : rw;
-    rw = st == -2 ? e.human_collision_cost : rw;
+    // selects, not a switch: each case's branch reloaded the env's spilled scalars.  The
+    // four costs are pinned in SGPRs first: otherwise the selects become a select of field
+    // ADDRESSES and one vector load from the kernel arguments, which the reward's stores
+    // then wait for with vmcnt(0).
+    float c_act = e.action_cost, c_rep = e.repeat_cost, c_col = e.collision_cost, c_hum = e.human_collision_cost;
+    asm volatile("" : "+s"(c_act), "+s"(c_rep), "+s"(c_col), "+s"(c_hum));
+    float rw = c_act;
+    rw = st == -4 ? c_rep : rw;
+    rw = (st == -1 || st == -3) ? c_col : rw;
+    rw = st == -2 ? c_hum : rw;
     const bool shadow_hit = act && st == 1 && Xr == prow(gg) && Xc == pcol(gg);
     const uint64_t shadow_mask = g.ballot(shadow_hit);
 
