@@ -10,7 +10,11 @@ getCenter (:181-183); the human's triangle (getTriPoints, :185-187); then * 255 
 astype('uint8').  The reference fills with cv2 (absent here); these rules -- a pixel is
 covered iff it lies inside or on the integer-vertex polygon, a disc iff dx^2 + dy^2 <= r^2
 -- are this build's, so parity with cv2's rasteriser is unpinned; the device kernel is
-pinned to this restatement bit-exactly.
+pinned to this restatement bit-exactly.  The geometry and the colours themselves --
+init_colors, getArrowPoints, drawStar, getRectPoints, getCenter, getTriPoints -- ARE pinned:
+tests/golden/g8_render.npz holds the reference functions' own outputs over a grid of cells,
+scales and agent counts (tests/test_render.py checks palette(), arrow_points(), star_points(),
+rect_points(), center() and tri_points() against it); only cv2's fill rule stays unpinned.
 """
 import colorsys
 import math
@@ -18,7 +22,10 @@ import math
 import numpy as np
 
 
-def _palette(n):
+def palette(n):
+    """init_colors (util.py:88-94) * 255 cast to uint8 (renderWorld :229-230): rows 0 = free
+    cell (colours[0]), 1 = obstacle (colours[-1]), 2 = human grey (colours[-2]), 3 + i = agent
+    i (colours[i + 1] = hsv(i / n, 1, 1)); n is EnvParameters.N_AGENTS in the reference."""
     pal = [(255, 255, 255), (0, 0, 0), (127, 127, 127)]
     for a in range(n):
         r, g, b = colorsys.hsv_to_rgb(a / float(n), 1.0, 1.0)
@@ -43,7 +50,10 @@ def _in_polygon(vx, vy, px, py):
     return inside | on
 
 
-def _arrow(direction, coord, scale):
+def arrow_points(direction, coord, scale):
+    """getArrowPoints (util.py:96-155) with renderWorld's tailWidth = scale / 10 and
+    headWidth = scale / 2 - 2 (:214); None for a zero direction (the reference leaves
+    `arrow` unbound there and raises)."""
     half = int(scale / 2) - 1
     th, tw, hw = half - 2, scale / 10, scale / 2 - 2
     cx, cy = coord[1] * scale + half, coord[0] * scale + half
@@ -65,7 +75,8 @@ def _arrow(direction, coord, scale):
     return np.array(pts, dtype="int64")
 
 
-def _star(coord, scale):
+def star_points(coord, scale):
+    """drawStar (util.py:157-175) with diameter = scale, numPoints = 5 (:211)."""
     half = int(scale / 2) - 1
     cx, cy = coord[1] * scale + half, coord[0] * scale + half
     outer = scale // 2
@@ -80,32 +91,50 @@ def _star(coord, scale):
     return np.array(pts, dtype="int64")
 
 
+def rect_points(coord, scale):
+    """getRectPoints (util.py:177-179): the cell's four corners, (x, y) = (col, row) * scale."""
+    x, y = coord[1] * scale, coord[0] * scale
+    return np.array([[x, y], [x + scale - 1, y], [x + scale - 1, y + scale - 1], [x, y + scale - 1]], dtype="int64")
+
+
+def center(coord, scale):
+    """getCenter (util.py:181-183): floor of the cell's origin + scale / 2."""
+    return [int(math.floor(coord[1] * scale + scale / 2)), int(math.floor(coord[0] * scale + scale / 2))]
+
+
+def tri_points(coord, scale):
+    """getTriPoints (util.py:185-187): apex at the top edge's floor(x + scale / 2)."""
+    x, y = coord[1] * scale, coord[0] * scale
+    return np.array([[int(math.floor(x + scale / 2)), y], [x + scale - 1, y + scale - 1], [x, y + scale - 1]],
+                    dtype="int64")
+
+
 def render_world(world, agents, goals, human, human_path, human_step, scale=20):
     """uint8 [H*scale, W*scale, 3]; agents / goals lists of (row, col), human (row, col),
     human_path the current path as a list of (row, col), human_step its index."""
     H, W = world.shape
     n = len(agents)
-    pal = _palette(n)
+    pal = palette(n)
     py, px = np.mgrid[0:H * scale, 0:W * scale]
     col = np.where(world[py // scale, px // scale] != 0, 1, 0)
     half = int(len(human_path) / 2)
     path = human_path[human_step + 1:half + 1] if human_step < half else human_path[human_step + 1:]
     for idx, val in enumerate(path):
         if idx == len(path) - 1:
-            pts = _star(val, scale)
+            pts = star_points(val, scale)
         else:
-            pts = _arrow(np.subtract(path[idx + 1], val), val, scale)
+            pts = arrow_points(np.subtract(path[idx + 1], val), val, scale)
             if pts is None:
                 continue
         col = np.where(_in_polygon(pts[:, 0], pts[:, 1], px, py), 2, col)
     for i, (r, c) in enumerate(agents):
         col = np.where((py // scale == r) & (px // scale == c), 3 + i, col)
-    rad, cxo = scale // 2 - 1, scale // 2
+    rad = int(math.floor(scale / 2)) - 1
     for i, (r, c) in enumerate(goals):
-        disc = (px - (c * scale + cxo)) ** 2 + (py - (r * scale + cxo)) ** 2 <= rad * rad
+        gx, gy = center((r, c), scale)
+        disc = (px - gx) ** 2 + (py - gy) ** 2 <= rad * rad
         col = np.where(disc & (py // scale == r) & (px // scale == c), 3 + i, col)
     r, c = human
-    x0, y0 = c * scale, r * scale
-    tri = np.array([[x0 + scale // 2, y0], [x0 + scale - 1, y0 + scale - 1], [x0, y0 + scale - 1]])
+    tri = tri_points((r, c), scale)
     col = np.where(_in_polygon(tri[:, 0], tri[:, 1], px, py) & (py // scale == r) & (px // scale == c), 2, col)
     return pal[col]

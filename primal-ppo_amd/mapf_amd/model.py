@@ -134,6 +134,28 @@ class Model:
             self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr)
             self.lagrange = get_lagrangian(LagrangianParameters.LAGRANGIAN_TYPE, TrainingParameters.COST_LIMIT_PER_AGENT)
             self.net_scaler = torch.amp.GradScaler(self.device.type, enabled=self.device.type == "cuda")
+            self.broadcast_weights()
+
+    def broadcast_weights(self, src=0):
+        """SURVEY.md §8(e) "weights broadcast at init": when torch.distributed is initialised with
+        more than one rank, every rank takes rank `src`'s parameters and buffers (one RCCL / gloo
+        broadcast per dtype bucket), so ranks constructed with different seeds hold one model
+        before the first all-reduced update (the reference has one global model, driver.py:50).
+        Collective: every rank must construct its global Model (or call this) in the same order.
+        Returns True if a broadcast ran."""
+        if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            return False
+        tensors = list(self.network.parameters()) + list(self.network.buffers())
+        for dtype in sorted({t.dtype for t in tensors}, key=str):
+            group = [t for t in tensors if t.dtype == dtype]
+            flat = torch.cat([t.detach().reshape(-1) for t in group])
+            dist.broadcast(flat, src)
+            off = 0
+            with torch.no_grad():
+                for t in group:      # copy_ bumps the version: the fp16 weight cache (_half) re-reads
+                    t.copy_(flat[off:off + t.numel()].view_as(t))
+                    off += t.numel()
+        return True
 
     # ------------------------------------------------------------ acting
     @torch.no_grad()

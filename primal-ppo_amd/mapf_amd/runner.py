@@ -57,22 +57,85 @@ def reference_maps(env: BatchedMapfGym, world_size=None, seed=0):
     return draw
 
 
+PERF_FIELDS = ("totalGoals", "shadowGoals", "episodeReward", "staticCollide", "humanCollide", "agentCollide",
+               "episodeCostReward", "constraintViolations")
+BATCH_FIELDS = ("observations", "vectors", "rewards", "values", "ps", "actions", "hiddenState", "returns",
+                "trainValid", "costRewards", "costValues", "costReturns")
+
+
 class OneEpPerformance:
     """util.py:56-65: the counters of ONE env's rollout (runner.py:66-99 sums them over one
     env's steps).  DeviceRunner.run() returns the mean over its B envs: driver.py:108-117
     passes one runner's object on (its loop overwrites `performance` with each result in
     turn), and Model.train feeds performance.episodeCostReward to the Lagrangian
-    (model.py:180, lagrange.py) -- a per-env quantity.  performance_per_env() has all B."""
-
-    FIELDS = ("totalGoals", "shadowGoals", "episodeReward", "staticCollide", "humanCollide", "agentCollide",
-              "episodeCostReward", "constraintViolations")
+    (model.py:180, lagrange.py) -- a per-env quantity.  performance_per_env() has all B.
+    Like the reference's class it has no public attribute but the 8 counters: driver.py
+    walks `dir(performance)` and np.nanmean()s every name not starting with '__'."""
 
     def __init__(self):
-        for f in self.FIELDS:
+        for f in PERF_FIELDS:
             setattr(self, f, 0)
 
 
-class EnvMajorRows:
+def _row_index(idx, n, device):
+    """A driver-style row index (int, slice, int array/list/tensor, bool mask) over n rows ->
+    (int64 tensor of rows in [0, n) on `device`, True if idx was a scalar)."""
+    if isinstance(idx, (int, np.integer)):
+        if not -n <= int(idx) < n:
+            raise IndexError(f"row {int(idx)} out of range for {n} rows")
+        return torch.tensor([int(idx) % n], device=device), True
+    if isinstance(idx, slice):
+        return torch.arange(*idx.indices(n), device=device), False
+    if not isinstance(idx, torch.Tensor):
+        idx = np.asarray(idx)
+        if idx.dtype == np.bool_:
+            if idx.shape != (n,):
+                raise IndexError(f"boolean index of shape {idx.shape} for {n} rows")
+            idx = np.flatnonzero(idx)
+        elif idx.size and not np.issubdtype(idx.dtype, np.integer):
+            raise IndexError(f"row indices must be integers, not {idx.dtype}")
+        idx = torch.from_numpy(idx.astype(np.int64, copy=False))
+    elif idx.dtype == torch.bool:
+        if tuple(idx.shape) != (n,):
+            raise IndexError(f"boolean index of shape {tuple(idx.shape)} for {n} rows")
+        idx = idx.nonzero().squeeze(1)
+    elif idx.is_floating_point():
+        raise IndexError(f"row indices must be integers, not {idx.dtype}")
+    idx = idx.to(device=device, dtype=torch.int64).reshape(-1)
+    if idx.numel() and (int(idx.min()) < -n or int(idx.max()) >= n):
+        raise IndexError("row index out of range")
+    return idx % n if n else idx, False
+
+
+class _DeviceRows:
+    """Row views of rollout buffers that stay on the device.  driver.py:119-121 hands a list of
+    them (one per runner result) to np.concatenate(..., axis=0): __array_function__ answers
+    with a lazy ConcatRows (runner k's rows after runner k-1's) instead of letting numpy
+    coerce the rows one by one to the host; any other numpy function, and __array__,
+    refuse -- a buffer never leaves the device behind the caller's back."""
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __array__(self, *args, **kwargs):
+        raise TypeError(f"{type(self).__name__} holds device rows; index it (rows[mb_inds]) or materialize()")
+
+    def __array_function__(self, func, types, args, kwargs):
+        if func is not np.concatenate:
+            return NotImplemented
+        seq = args[0] if args else kwargs.get("arrays")
+        axis = kwargs.get("axis", args[1] if len(args) > 1 else 0)
+        if axis != 0 or set(kwargs) - {"axis", "arrays"}:
+            return NotImplemented
+        return concat_rows(list(seq))
+
+    def __getitem__(self, idx):
+        rows, scalar = _row_index(idx, self.shape[0], self.device)
+        out = self._gather(rows)
+        return out[0] if scalar else out
+
+
+class EnvMajorRows(_DeviceRows):
     """The [B*T, ...] rows of a t-major [T, B, ...] rollout buffer in ENV-MAJOR order:
     row r = env r // T, step r % T -- the order driver.py:101-121 builds by concatenating
     the runners' results (runner k's T rows, then runner k+1's).  Rows [0, T) are env 0's
@@ -85,63 +148,96 @@ class EnvMajorRows:
         self.shape = torch.Size((B * T,) + tuple(buf.shape[2:]))
         self.dtype, self.device = buf.dtype, buf.device
 
-    def __len__(self):
-        return self.shape[0]
-
-    def __getitem__(self, idx):
-        n = self.shape[0]
-        if isinstance(idx, int):
-            if not -n <= idx < n:
-                raise IndexError(idx)
-            idx %= n
-            return self.buf[idx % self.T, idx // self.T]
-        if isinstance(idx, slice):
-            idx = torch.arange(*idx.indices(n), device=self.device)
-        else:
-            idx = torch.as_tensor(np.asarray(idx) if not isinstance(idx, torch.Tensor) else idx,
-                                  device=self.device).long()
-            if idx.numel() and (int(idx.min()) < -n or int(idx.max()) >= n):
-                raise IndexError("row index out of range")
-            idx = idx % n
-        return self.buf[idx % self.T, idx // self.T]
+    def _gather(self, rows):
+        return self.buf[rows % self.T, rows // self.T]
 
     def materialize(self):
         return self.buf.transpose(0, 1).reshape(self.shape)
 
 
-class ZeroRows:
+class ZeroRows(_DeviceRows):
     """hiddenState rows: all zeros in the reference (runner.py:47-48, never read by the
     net), handed out as expanded zero views, never materialised."""
 
     def __init__(self, n, row_shape, device):
         self.shape = torch.Size((n,) + tuple(row_shape))
-        self.dtype, self.device = torch.float32, device
+        self.dtype, self.device = torch.float32, torch.device(device)
 
-    def __len__(self):
-        return self.shape[0]
+    def _gather(self, rows):
+        return torch.zeros((), device=self.device).expand((rows.numel(),) + tuple(self.shape[1:]))
 
-    def __getitem__(self, idx):
-        k = len(range(*idx.indices(self.shape[0]))) if isinstance(idx, slice) else len(np.atleast_1d(
-            idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)))
-        return torch.zeros((), device=self.device).expand((k,) + tuple(self.shape[1:]))
+    def materialize(self):
+        return torch.zeros(self.shape, device=self.device)
+
+
+class ConcatRows(_DeviceRows):
+    """np.concatenate(parts, axis=0) of device row views, kept lazy: row r belongs to the part
+    whose row range holds it.  Indexing gathers each part's share of the rows on the device
+    and scatters it into one output in the order asked for."""
+
+    def __init__(self, parts):
+        self.parts = parts
+        self.offsets = [0]
+        for p in parts:
+            self.offsets.append(self.offsets[-1] + p.shape[0])
+        self.shape = torch.Size((self.offsets[-1],) + tuple(parts[0].shape[1:]))
+        self.dtype, self.device = parts[0].dtype, parts[0].device
+        self._bounds = torch.tensor(self.offsets[1:], device=self.device)
+
+    def _gather(self, rows):
+        part = torch.bucketize(rows, self._bounds, right=True)
+        out = torch.empty((rows.numel(),) + tuple(self.shape[1:]), dtype=self.dtype, device=self.device)
+        for k, p in enumerate(self.parts):
+            sel = (part == k).nonzero().squeeze(1)
+            if sel.numel():
+                out.index_copy_(0, sel, p._gather(rows[sel] - self.offsets[k]))
+        return out
+
+    def materialize(self):
+        return torch.cat([p.materialize() for p in self.parts], dim=0)
+
+
+def concat_rows(parts):
+    """np.concatenate(parts, axis=0) for device row views (driver.py:119-121)."""
+    flat = []
+    for p in parts:
+        if isinstance(p, ConcatRows):
+            flat.extend(p.parts)
+        elif isinstance(p, _DeviceRows):
+            flat.append(p)
+        else:
+            raise TypeError(f"np.concatenate of device rows with {type(p).__name__}: every part must stay "
+                            "on the device (DeviceRunner results only)")
+    if not flat:
+        raise ValueError("need at least one array to concatenate")
+    first = flat[0]
+    for p in flat[1:]:
+        if tuple(p.shape[1:]) != tuple(first.shape[1:]) or p.dtype != first.dtype or p.device != first.device:
+            raise ValueError(f"row shape/dtype/device mismatch in concatenate: {tuple(first.shape[1:])} "
+                             f"{first.dtype} {first.device} vs {tuple(p.shape[1:])} {p.dtype} {p.device}")
+    if len(flat) == 1:
+        return first
+    if all(isinstance(p, ZeroRows) for p in flat):
+        return ZeroRows(sum(p.shape[0] for p in flat), first.shape[1:], first.device)
+    return ConcatRows(flat)
 
 
 class BatchValues:
     """util.py:41-54: the rollout's arrays by the reference's attribute names (driver.py reads
-    them with getattr), each an EnvMajorRows view over the device buffers; mb["name"] works too."""
-
-    FIELDS = ("observations", "vectors", "rewards", "values", "ps", "actions", "hiddenState", "returns",
-              "trainValid", "costRewards", "costValues", "costReturns")
+    them with getattr over `dir(BatchValues())`), each a device row view; mb["name"] works
+    too.  BatchValues() with no arguments is the reference's empty collector (12 lists), so
+    driver.py:99-121 runs unchanged whichever of the two classes it imports: there is no
+    public attribute besides the 12 fields."""
 
     def __init__(self, **fields):
-        for k in self.FIELDS:
-            setattr(self, k, fields[k])
+        unknown = set(fields) - set(BATCH_FIELDS)
+        if unknown:
+            raise TypeError(f"unknown BatchValues fields {sorted(unknown)}")
+        for k in BATCH_FIELDS:
+            setattr(self, k, fields[k] if k in fields else list())
 
     def __getitem__(self, name):
         return getattr(self, name)
-
-    def keys(self):
-        return self.FIELDS
 
 
 class DeviceRunner:

@@ -19,6 +19,7 @@ Fixtures
              resolution, -3 overwrites, fixActions eviction, FOV edges).
   g3_search.npz  astar_4 paths and makeBfsMap outputs.
   g4_gae.npz  Runner.run GAE (runner.py:117-149) on a short rollout.
+  g8_render.npz  renderWorld's colours and shape vertices (util.py:88-187).
 """
 import copy
 import json
@@ -535,7 +536,56 @@ def g2_evict():
             keep=lambda ev: any(len(x) >= 2 for x in ev))
 
 
+def g8_render():
+    """renderWorld's geometry and colours (util.py:88-187), from the reference functions:
+    init_colors for several EnvParameters.N_AGENTS (the float colours and the uint8 they
+    become, scene * 255 -> astype('uint8'), :229-230); getArrowPoints in the four directions
+    with renderWorld's tailWidth / headWidth (:214); drawStar (diameter = scale, 5 points,
+    :211); getRectPoints, getCenter, getTriPoints -- over a grid of cells and scales (renderWorld
+    itself forces scale = 20, :199).  cv2's fill is not exercised (absent here)."""
+    out = {}
+    n_keep = alg.EnvParameters.N_AGENTS
+    try:
+        for n in (1, 2, 3, 4, 6, 7, 8, 16, 64):
+            alg.EnvParameters.N_AGENTS = n
+            util.EnvParameters.N_AGENTS = n
+            c = util.init_colors()
+            keys = [0, -1, -2] + [a + 1 for a in range(n)]
+            f = np.array([np.asarray(c[k], dtype=np.float64) for k in keys])
+            out[f"colors_f_{n}"] = f
+            out[f"colors_u8_{n}"] = (f * 255).astype(np.uint8)
+    finally:
+        alg.EnvParameters.N_AGENTS = n_keep
+        util.EnvParameters.N_AGENTS = n_keep
+    coords = np.array([(r, c) for r in (0, 1, 3, 7, 19, 39) for c in (0, 2, 5, 13, 39, 59)], dtype=np.int64)
+    scales = np.array([20, 10, 16, 7, 24, 11], dtype=np.int64)
+    dirs = np.array([(0, 1), (1, 0), (0, -1), (-1, 0)], dtype=np.int64)
+    arrows = np.zeros((len(scales), len(dirs), len(coords), 7, 2), np.int64)
+    stars = np.zeros((len(scales), len(coords), 15, 2), np.int64)
+    rects = np.zeros((len(scales), len(coords), 4, 2), np.int64)
+    tris = np.zeros((len(scales), len(coords), 3, 2), np.int64)
+    centers = np.zeros((len(scales), len(coords), 2), np.int64)
+    for si, sc in enumerate(scales):
+        sc = int(sc)
+        for ci, (r, cc) in enumerate(coords):
+            coord = (int(r), int(cc))
+            for di, d in enumerate(dirs):
+                arrows[si, di, ci] = util.getArrowPoints(direction=d, coord=coord, scale=sc, tailWidth=sc / 10,
+                                                         headWidth=sc / 2 - 2)
+            stars[si, ci] = util.drawStar(coord=coord, scale=sc, diameter=sc, numPoints=5)
+            rects[si, ci] = util.getRectPoints(coord=coord, scale=sc)
+            tris[si, ci] = util.getTriPoints(coord=coord, scale=sc)
+            centers[si, ci] = util.getCenter(coord=coord, scale=sc)
+    out.update(coords=coords, scales=scales, dirs=dirs, arrows=arrows, stars=stars, rects=rects, tris=tris,
+               centers=centers)
+    np.savez_compressed(os.path.join(OUT, "g8_render.npz"), **out)
+    print("g8_render:", {k: v.shape for k, v in out.items() if not k.startswith("colors")})
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["g8"]:
+        g8_render()
+        sys.exit(0)
     if sys.argv[1:] == ["g7"]:
         g7_warehouses()
         sys.exit(0)
@@ -565,3 +615,4 @@ if __name__ == "__main__":
     g3_search(31)
     g4_gae()
     g6_episodes()
+    g8_render()

@@ -173,53 +173,78 @@ def test_device_runner_fresh_reference_envs_each_rollout():
     assert not c[:8].any(), c[:8]
 
 
-def test_driver_loop_over_device_runner_c3():
-    """driver.py:101-134 restated over DeviceRunner's output at the c3 shape (4096 envs x 8
-    agents, 20x20, FOV 9; short T): the BatchValues attributes read with getattr, the
-    OneEpPerformance fields with np.nanmean, minibatches `inds[start:end]` of
-    `inds = np.arange(N_STEPS)` -- which select env 0's rollout first, as they select runner
-    0's in the reference -- fed to Model.train.  GAE columns vs the oracle on the whole
-    rollout; performance = the per-env mean of the per-env counters."""
-    from mapf_amd.config import TrainingParameters
+class _GuardedModel:
+    """Model.train behind driver.py:131-134: every minibatch argument must arrive as a device
+    tensor; the model's own one stats copy is the only host copy allowed (HostGuard)."""
+
+    def __init__(self, model, guard):
+        self.model, self.guard, self.obs, self.returns = model, guard, [], []
+
+    def train(self, *args):
+        for k, a in enumerate(args[:10]):
+            assert isinstance(a, torch.Tensor) and a.is_cuda, f"train argument {k} is not a device tensor"
+        self.obs.append(args[0])
+        self.returns.append(args[2])
+        with self.guard.allow():
+            return self.model.train(*args)
+
+
+@pytest.mark.parametrize("n_runners", [1, 2])
+def test_driver_block_verbatim_over_device_runners_c3(n_runners):
+    """driver.py:97-134 run unchanged (tests/driver_block.py: the attribute appends :101-107, the
+    np.nanmean of :110-117, np.concatenate(..., axis=0) of :119-121, the minibatch loop of
+    :123-134) over one and two DeviceRunner results at the c3 shape (4096 envs x 8 agents,
+    20x20, FOV 9) with the reference's rollout length T = N_STEPS = 256.  No buffer leaves the
+    device (HostGuard + peak-memory bound: one runner's observations alone are 16.3 GB), the
+    concatenation is lazy, and `inds = np.arange(N_STEPS)` trains on env 0's rollout of the
+    first runner -- as the reference trains on its first runner's rollout."""
+    from driver_block import HostGuard, ReferenceBatchValues, ReferenceOneEpPerformance, expected_minibatches, \
+        run_driver_block
+    from mapf_amd.config import TrainingParameters as TP
     from mapf_amd.model import Model
-    from mapf_amd.runner import BatchValues, DeviceRunner, OneEpPerformance
-    B, N, T = 4096, 8, 4
-    env = make_env(B, N, F=9)
+    from mapf_amd.runner import BATCH_FIELDS, PERF_FIELDS, DeviceRunner
+    B, N, T = 4096, 8, TP.N_STEPS
     model = Model(0, "cuda", global_model=True, numChannel=6, num_agents=N, fov=9)
-    runner = DeviceRunner(env, model, n_steps=T, seed=11)
-    mb, perf = runner.run()
-    # GAE on the whole rollout (B*N columns) == the oracle's numpy-f32 loop, bit-exact
-    for rew, val, last, ret in ((runner.rewards, runner.values, runner.last_v, runner.returns),
-                                (runner.cost_rewards, runner.cost_values, runner.last_cv, runner.cost_returns)):
+    runners = [DeviceRunner(make_env(B, N, F=9, offset=k * B, seed=99), model, n_steps=T, seed=11 + k)
+               for k in range(n_runners)]
+    job_results = [r.run() for r in runners]
+    torch.cuda.synchronize()
+    # GAE on runner 0's whole rollout (B*N columns) == the oracle's numpy-f32 loop, bit-exact
+    r0 = runners[0]
+    for rew, val, last, ret in ((r0.rewards, r0.values, r0.last_v, r0.returns),
+                                (r0.cost_rewards, r0.cost_values, r0.last_cv, r0.cost_returns)):
         _, want = O.gae(rew.reshape(T, -1).cpu().numpy(), val.reshape(T, -1).cpu().numpy(),
                         last.reshape(-1).cpu().numpy())
         np.testing.assert_array_equal(ret.reshape(T, -1).cpu().numpy(), want)
-    # driver.py:108-117: performance fields through np.nanmean
-    performance = OneEpPerformance()
-    for i in OneEpPerformance.FIELDS:
-        setattr(performance, i, np.nanmean(getattr(perf, i)))
-    per_env = runner.performance_per_env()
+    want_perf = {f: getattr(job_results[-1][1], f) for f in PERF_FIELDS}
+    before = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    np.random.seed(2024)
+    with HostGuard() as guard:
+        proxy = _GuardedModel(model, guard)
+        mb, performance, losses, steps, episodes = run_driver_block(
+            job_results, proxy, ReferenceBatchValues, ReferenceOneEpPerformance, TP)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - before
+    assert not guard.hits and peak < 2 << 30, (guard.hits, peak)
+    assert steps == n_runners * T and episodes == n_runners
+    for k in BATCH_FIELDS:
+        v = getattr(mb, k)
+        assert not isinstance(v, np.ndarray) and len(v) == n_runners * T * B and v.device.type == "cuda", k
+    for f in PERF_FIELDS:                    # the last result's per-env means, through two nanmeans
+        assert getattr(performance, f) == want_perf[f], f
+    per_env = runners[-1].performance_per_env()
     assert performance.episodeCostReward == np.mean(per_env["episodeCostReward"])
-    b0 = runner.cost_rewards[:, 0].double().sum().item()
-    assert abs(per_env["episodeCostReward"][0] - b0) < 1e-6 * max(1.0, abs(b0))
-    assert per_env["staticCollide"][7] == int((runner.status[:, 7] == -1).sum())
-    # driver.py:123-131 over getattr(mb, name)
-    n_rows = TrainingParameters.N_STEPS
-    inds = np.arange(n_rows)
-    rng = np.random.default_rng(0)
-    losses = []
-    for _ in range(2):
-        rng.shuffle(inds)
-        for start in range(0, n_rows, TrainingParameters.MINIBATCH_SIZE):
-            mb_inds = inds[start:start + TrainingParameters.MINIBATCH_SIZE]
-            g = {k: getattr(mb, k)[mb_inds] for k in BatchValues.FIELDS}
-            envs, steps = mb_inds // T, mb_inds % T
-            np.testing.assert_array_equal(g["observations"].cpu().numpy(),
-                                          runner.obs[steps, envs].cpu().numpy())
-            np.testing.assert_array_equal(g["returns"].cpu().numpy(), runner.returns[steps, envs].cpu().numpy())
-            assert g["hiddenState"].shape == (len(mb_inds), 2, N, 512) and not g["hiddenState"].any()
-            losses.append(model.train(g["observations"], g["vectors"], g["returns"], g["costReturns"], g["values"],
-                                      g["costValues"], g["actions"], g["ps"], g["hiddenState"], g["trainValid"],
-                                      performance.episodeCostReward))
-    assert len(losses) == 2 * (n_rows // TrainingParameters.MINIBATCH_SIZE)
+    # the minibatches: env 0's rollout of runner 0, in the shuffled order of the global numpy RNG
+    mbs = expected_minibatches(2024, TP)
+    assert len(losses) == len(mbs) == TP.N_EPOCHS * (T // TP.MINIBATCH_SIZE)
+    for obs, ret, inds in zip(proxy.obs, proxy.returns, mbs):
+        assert torch.equal(obs, r0.obs[torch.as_tensor(inds, device="cuda"), 0])
+        assert torch.equal(ret, r0.returns[torch.as_tensor(inds, device="cuda"), 0])
+    if n_runners == 2:                       # runner 1's rows follow runner 0's
+        r1 = runners[1]
+        rows = np.array([T * B, T * B + 7, 2 * T * B - 1])
+        got = mb.observations[rows]
+        assert torch.equal(got[0], r1.obs[0, 0]) and torch.equal(got[1], r1.obs[7, 0])
+        assert torch.equal(got[2], r1.obs[T - 1, B - 1])
     assert all(np.isfinite(float(np.asarray(s))) for k, s in enumerate(losses[-1]) if k != 8)

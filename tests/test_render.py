@@ -20,8 +20,8 @@ def test_oracle_frame_structure():
     path = [(9, 9), (9, 8), (8, 8), (7, 8), (8, 8), (9, 8), (9, 9)]
     f = R.render_world(world, [(0, 0), (2, 3)], [(0, 1), (5, 5)], (9, 9), path, 0)
     assert f.shape == (200, 200, 3) and f.dtype == np.uint8
-    assert (f[0:20, 0:20] == R._palette(2)[3]).all()                   # agent 0's whole cell
-    assert (f[105:115, 110:111] == R._palette(2)[4]).all()             # agent 1's goal disc at (5, 5)
+    assert (f[0:20, 0:20] == R.palette(2)[3]).all()                   # agent 0's whole cell
+    assert (f[105:115, 110:111] == R.palette(2)[4]).all()             # agent 1's goal disc at (5, 5)
     assert (f[20 * 1 + 1, 20 * 2 + 2] == 0).all()                      # a shelf cell stays black
     # the path segment path[1:4] is drawn: arrows on (9,8) and (8,8), the star on (7,8)
     star = np.all(f[140:160, 160:180] == 127, axis=-1)
@@ -31,9 +31,37 @@ def test_oracle_frame_structure():
 
 
 def test_oracle_palette_is_hsv():
-    pal = R._palette(8)
+    pal = R.palette(8)
     assert tuple(pal[3]) == (255, 0, 0) and tuple(pal[5]) == (127, 255, 0)   # hsv(1/4) * 255 truncated
     assert tuple(pal[2]) == (127, 127, 127)                                 # colours[-2] = 0.5
+
+
+def test_oracle_geometry_and_colours_match_reference_g8():
+    """The restatement's palette and shape vertices == the reference's init_colors /
+    getArrowPoints / drawStar / getRectPoints / getCenter / getTriPoints (util.py:88-187),
+    from tests/golden/g8_render.npz, over 36 cells x 6 scales x 4 directions and 9 agent
+    counts.  With the device kernel bit-exact to this restatement (GPU test below), only the
+    cv2 fill rule itself is unpinned."""
+    import colorsys
+    from golden_io import load
+    z = load("g8_render")
+    for n in (1, 2, 3, 4, 6, 7, 8, 16, 64):
+        np.testing.assert_array_equal(R.palette(n), z[f"colors_u8_{n}"], err_msg=f"palette n={n}")
+        # the float colours too (matplotlib's hsv_to_rgb vs colorsys: same float64 formula)
+        f = np.array([[1, 1, 1], [0, 0, 0], [0.5, 0.5, 0.5]] +
+                     [list(colorsys.hsv_to_rgb(a / float(n), 1.0, 1.0)) for a in range(n)])
+        np.testing.assert_array_equal(f, z[f"colors_f_{n}"])
+    for si, sc in enumerate(z["scales"]):
+        sc = int(sc)
+        for ci, (r, c) in enumerate(z["coords"]):
+            coord = (int(r), int(c))
+            for di, d in enumerate(z["dirs"]):
+                np.testing.assert_array_equal(R.arrow_points(d, coord, sc), z["arrows"][si, di, ci])
+            np.testing.assert_array_equal(R.star_points(coord, sc), z["stars"][si, ci])
+            np.testing.assert_array_equal(R.rect_points(coord, sc), z["rects"][si, ci])
+            np.testing.assert_array_equal(R.tri_points(coord, sc), z["tris"][si, ci])
+            assert R.center(coord, sc) == list(z["centers"][si, ci])
+    assert R.arrow_points((0, 0), (1, 1), 20) is None
 
 
 def test_make_gif_roundtrip(tmp_path):

@@ -55,10 +55,7 @@ def main():
                                      shared_map=not args.reference_maps), device=dev)
     new_maps = reference_maps(env, seed=rank) if args.reference_maps else None
     env.reset_seeded(new_maps(0) if new_maps else generate_warehouse(H, H))
-    model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=F)
-    if world > 1:
-        for p in model.network.parameters():
-            torch.distributed.broadcast(p.data, 0)
+    model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=F)   # broadcasts rank 0's weights
     runner = DeviceRunner(env, model, n_steps=args.steps, seed=rank, new_maps=new_maps)
     runner.run()                       # warm-up (kernels, autotuning)
     torch.cuda.synchronize()
