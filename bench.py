@@ -344,9 +344,18 @@ def main():
         return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     KT = args.kernel_launches or (max(1, min(20, K // T)) if path == "rollout" else min(K, 300))
-    KS = min(K, 300)
+    # every breakdown path is warmed up before it is timed (first launches of a path pay code
+    # object loads, instruction-cache misses and, for the split path, its first search work),
+    # and timed over at least 100 launches whatever --steps is
+    KS = min(max(K, 100), 300)
+    for _ in range(20):
+        env.step_observe(acts, obs, vec, random_policy=True)
     fused_ms = event_ms(lambda: env.step_observe(acts, obs, vec, random_policy=True), KS)
     env.flush()
+    for _ in range(20):
+        env.step_random(acts)
+        env.flush()
+        env.observe(obs, vec)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KS)]
     for k in range(KS):
         e0, e1, e2, e3 = ev[k]
@@ -361,7 +370,16 @@ def main():
     step_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(KS)]))
     search_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(KS)]))
     obs_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(KS)]))
-    roll_ms = event_ms(lambda: rollout(T), KT) if path == "rollout" else None
+    # the roofline kernel is timed over launches of --rollout-steps steps (the production launch
+    # length, the reference's N_STEPS = 256) whatever --steps is: a short timed run (one launch
+    # of K < 256 steps) pays the launch's ramp once over few steps, which `value` includes
+    TR = T if roll is not None else max(1, args.rollout_steps)
+    if path == "rollout":
+        KT = args.kernel_launches or max(3, min(20, K // T))
+        if TR != T:
+            rollout(TR)
+            torch.cuda.synchronize()
+    roll_ms = event_ms(lambda: rollout(TR), KT) if path == "rollout" else None
 
     # The same workload down each path, each with its own roofline fraction:
     #  rollout_inplace  mapf_rollout_random, every step re-writes the [B]-leading buffers
@@ -387,7 +405,7 @@ def main():
                                                     f"observe + forked search; breakdown_ms.split has them serial)")
         if env.rollout_fused:
             if roll is None:
-                paths["rollout_inplace"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
+                paths["rollout_inplace"] = entry(roll_ms / TR, bpa_f, f"HIP events, {KT} launches of {TR} steps")
                 TS = min(T, max(8, int(25e9 // (B * N * (C * F * F + 4) * 4))))   # <= ~25 GB of slots
                 sl = dict(actions=torch.zeros(TS, B, N, dtype=torch.int32, device=dev),
                           obs=torch.zeros(TS, B, N, C, F, F, device=dev), vec=torch.zeros(TS, B, N, 4, device=dev),
@@ -410,7 +428,7 @@ def main():
         if path == "rollout":
             kname = ("rollout_random_kernel" if env.rollout_kernel == 1 else "rollout_wide_kernel") + \
                 ("<true> (nontemporal stores)" if roll else "")
-            bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, T
+            bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, TR
         elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one
             kname, bpa, kms, steps_pl = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms, 1
         else:
@@ -432,7 +450,8 @@ def main():
                        "total_envs": B * world_size,
                        "parallelism": f"env-shards x{world_size}"},
             "breakdown_ms": {"rollout_launch": round(roll_ms, 4) if roll_ms else None,
-                             "rollout_per_step": round(roll_ms / T, 5) if roll_ms else None,
+                             "rollout_per_step": round(roll_ms / TR, 5) if roll_ms else None,
+                             "rollout_steps_per_launch": TR if roll_ms else None,
                              "step_observe_launch": round(fused_ms, 4),
                              "split": {"step_kernel": round(step_ms, 4), "search_kernel": round(search_ms, 4),
                                        "observe_kernel": round(obs_ms, 4)},
