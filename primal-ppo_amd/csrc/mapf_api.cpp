@@ -68,6 +68,7 @@ struct mapf_env {
     long def_due[2] = {-1, -1};            // join before the step that would make nsteps exceed this
     int def_next = 0;
     bool no_defer = false;                 // MAPF_NO_DEFER=1: join every search in its own call (A/B timing)
+    ArgRing args;                          // device-resident argument blocks of the persistent kernels
     template <class T>
     int alloc(T *&p, size_t n) {
         void *q = nullptr;
@@ -170,6 +171,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(e->maps8, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
+    rc |= e->alloc(e->args.base, ARG_SLOTS * ARG_SLOT_BYTES);
     if (rc) {
         std::string m = g_err;
         mapf_destroy(e);
@@ -221,7 +223,18 @@ int mapf_rollout_random_fused(const mapf_env *e) {
 
 // s waits for the deferred aux-stream searches: every one (all), or those due before the
 // step about to be launched
+// Deferral is off while s is captured (observe_with_search), so a pending event was recorded
+// outside any capture: a captured stream cannot wait on it (the graph would depend on work
+// outside itself) -- the caller must join it first (mapf_flush, or any call on an uncaptured
+// stream) before beginning the capture.
 static int join_deferred(mapf_env *e, hipStream_t s, bool all) {
+    if (e->def_due[0] >= 0 || e->def_due[1] >= 0) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        HIPCHK(hipStreamIsCapturing(s, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(MAPF_ESTATE, "a search deferred before this stream capture began is still pending: "
+                                     "call mapf_flush on an uncaptured stream before capturing");
+    }
     for (int k = 0; k < 2; ++k) {
         if (e->def_due[k] >= 0 && (all || e->nsteps >= e->def_due[k])) {
             HIPCHK(hipStreamWaitEvent(s, e->ev_def[k], 0));
@@ -552,8 +565,8 @@ int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_
     if (T == 0) return MAPF_OK;
     if (rollout_random_fused(e)) {
         if (int rc = flush_search(e, s)) return rc;     // the kernel searches inline from here on
-        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s))
-            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, s);
+        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->args, s))
+            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->args, s);
         HIPCHK(hipGetLastError());
         return MAPF_OK;
     }

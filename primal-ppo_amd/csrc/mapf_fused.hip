@@ -142,6 +142,11 @@ struct RolloutOut {
     int slots;
     int xcd_remap;
 };
+// the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
+struct RolloutArgs {
+    DevEnv e;
+    RolloutOut ro;
+};
 
 __host__ __device__ inline bool rollout_fusable(const DevEnv &e) {
     return e.G == 8 && e.human_mode != 2 && e.goal_mode == 1 && e.C < 7 && !e.force_agent_lanes && fused_per_wave(e) &&
@@ -158,7 +163,14 @@ __host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
 // measured faster); re-written [B]-leading buffers keep plain stores (their lines
 // stay cache-resident between steps, measured faster).
 template <bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(DevEnv e, int T, RolloutOut ro) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(
+#if MAPF_ARGS_PTR      // experiment build: arguments through a device pointer (mapf_rollout_wide.hip)
+    const RolloutArgs *__restrict__ args, int T) {
+    const DevEnv &e = args->e;
+    const RolloutOut &ro = args->ro;
+#else
+    DevEnv e, int T, RolloutOut ro) {
+#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int E = 4;                     // envs per workgroup, one per wave
     // XCD-aware env order: workgroups are dealt round-robin over the 8 XCDs, so workgroup w
@@ -218,32 +230,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
 bool rollout_random_fusable(const DevEnv &e) { return rollout_fusable(e) && rollout_lds_bytes(e) <= 64 * 1024; }
 
 bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                           int slots, hipStream_t s) {
+                           int slots, ArgRing &ring, hipStream_t s) {
     if (!rollout_random_fusable(e)) return false;
     const int grid = (e.B + 3) / 4;
     // Persistent waves: every CU should hold the same number of workgroups, or the
     // CUs holding more set the pace of every step.  The LDS request caps the
     // workgroups per CU at ceil(grid / CUs) (160 KiB of LDS per CU).
-    static int ncu = 0;
-    if (ncu == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-    }
+    const int ncu = device_cu_count();
     int occ = (grid + ncu - 1) / ncu;
     if (const char *v = std::getenv("MAPF_ROLL_OCC")) { const int x = std::atoi(v); if (x >= 1 && x <= 16) occ = x; }
     size_t lds = rollout_lds_bytes(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
-    static int remap = -1;
-    if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
+    const int remap = env_flag("MAPF_XCD_REMAP", 1) != 0;
+#if MAPF_ARGS_PTR
+    const RolloutArgs *args = push_args(ring, RolloutArgs{e, RolloutOut{actions, out, obs, vec, slots, remap}}, s);
     if (slots)
-        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T,
-                           RolloutOut{actions, out, obs, vec, slots, remap});
+        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, args, T);
     else
-        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, e, T,
-                           RolloutOut{actions, out, obs, vec, slots, remap});
+        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, args, T);
+#else
+    (void)ring;
+    const RolloutOut ro{actions, out, obs, vec, slots, remap};
+    if (slots)
+        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T, ro);
+    else
+        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, e, T, ro);
+#endif
     return true;
 }
 

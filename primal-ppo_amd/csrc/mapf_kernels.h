@@ -1,8 +1,45 @@
 // primal-ppo_amd/csrc/mapf_kernels.h -- host-side launchers of the MAPF kernels.
 #pragma once
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+
 #include "mapf_common.h"
 
 namespace mapf {
+
+// Launch-configuration queries, cached per device (a process may drive several GPUs with
+// different CU counts) and safe to call from several host threads.
+inline int device_cu_count() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    int v = dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0;
+    if (v > 0) return v;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+    return v;
+}
+
+// VGPRs per lane of a kernel (one code object per arch: the same on every device here)
+inline int kernel_vgprs(const void *fn) {
+    static std::mutex m;
+    static std::unordered_map<const void *, int> cache;
+    std::lock_guard<std::mutex> lock(m);
+    auto it = cache.find(fn);
+    if (it != cache.end()) return it->second;
+    hipFuncAttributes fa{};
+    const int v = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? fa.numRegs : 512;
+    cache.emplace(fn, v);
+    return v;
+}
+
+// an integer environment switch (A/B experiments), read at every launch
+inline int env_flag(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
 
 struct StepOut {          // device pointers (mapf_step_out)
     int8_t *status;
@@ -43,12 +80,44 @@ void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, 
 // false (nothing launched) if the configuration is not covered
 bool rollout_random_fusable(const DevEnv &e);
 bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                           int slots, hipStream_t s);
+                           int slots, struct ArgRing &ring, hipStream_t s);
 // the same for up to 64 agents / per-env maps / the BFS channel: one wave per env
 // (mapf_rollout_wide.hip); used where the pair-lane rollout does not apply
 bool rollout_wide_fusable(const DevEnv &e);
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                         int slots, hipStream_t s);
+                         int slots, struct ArgRing &ring, hipStream_t s);
+
+// Device-resident kernel argument blocks.  A persistent kernel whose arguments (DevEnv + its
+// output pointers, ~0.5 KiB) do not fit in the SGPR file kept them live from the kernarg
+// load on and spilled ~450 SGPRs to VGPR lanes (v_readlane at every use, plus dead stack
+// slots).  Read through a `const __restrict__` pointer instead, every field is an invariant
+// scalar load the register allocator re-issues where it is used.  The block is written on
+// the launch stream by a one-wave kernel that takes it by value (stream-ordered, capturable
+// in a hipGraph), into the next of ARG_SLOTS slots: launches on different streams in flight
+// at once never share a slot unless more than ARG_SLOTS are.
+constexpr size_t ARG_SLOT_BYTES = 2048, ARG_SLOTS = 16;
+struct ArgRing {
+    char *base = nullptr;     // ARG_SLOTS * ARG_SLOT_BYTES of device memory (owned by the handle)
+    unsigned next = 0;
+    template <class A>
+    A *slot() {
+        static_assert(sizeof(A) <= ARG_SLOT_BYTES, "argument block larger than a slot");
+        return reinterpret_cast<A *>(base + (size_t)(next++ % ARG_SLOTS) * ARG_SLOT_BYTES);
+    }
+};
+
+template <class A>
+__global__ __launch_bounds__(64) void store_args_kernel(A a, A *dst) {
+    if (threadIdx.x == 0) *dst = a;
+}
+
+// a's copy in the ring's next slot, written on stream s before the kernel that reads it
+template <class A>
+inline const A *push_args(ArgRing &ring, const A &a, hipStream_t s) {
+    A *slot = ring.slot<A>();
+    hipLaunchKernelGGL(store_args_kernel<A>, dim3(1), dim3(64), 0, s, a, slot);
+    return slot;
+}
 // renderWorld (util.py:189-232) on the device (mapf_render.hip): frames [n][H*S][W*S][3] u8
 struct RenderSpec {
     int scale;

@@ -42,6 +42,12 @@ struct WideOut {
     int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
 };
 
+// the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
+struct WideArgs {
+    DevEnv e;
+    WideOut ro;
+};
+
 __host__ __device__ inline size_t wide_a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // observation part of the scratch area: stream | occ | spos | sgoal | shn | shp | shpn | idg
@@ -140,9 +146,21 @@ __device__ inline void wide_plain_barrier() {
 
 // waves_per_eu(2): at most 256 VGPRs, so two waves of every SIMD stay resident (c5: 2,048
 // envs = 8 waves per CU; above 256 the launch would run in two rounds)
+// MAPF_ARGS_PTR=1 (experiment build, `make argptr`): the arguments are read through a
+// device pointer (ArgRing) instead of the kernarg segment -- 123 instead of 454 SGPR spills,
+// but every field is then re-loaded through the scalar cache where it is used, and the
+// stepper measured slower
+#if MAPF_ARGS_PTR
+#define WIDE_PARAMS const WideArgs *__restrict__ args, int T_steps
+#define WIDE_BIND const DevEnv &e = args->e; const WideOut &ro = args->ro;
+#else
+#define WIDE_PARAMS DevEnv e, int T_steps, WideOut ro
+#define WIDE_BIND
+#endif
+
 template <class T, int RW, bool NT>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(DevEnv e, int T_steps,
-                                                                                                     WideOut ro) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(WIDE_PARAMS) {
+    WIDE_BIND
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-aware env order (as the pair-lane rollout): workgroups are dealt round-robin
     // over the 8 XCDs, so each XCD owns one contiguous range of envs
@@ -264,16 +282,10 @@ template <class T, int RW>
 static bool wide_fits(const DevEnv &e) { return wide_lds_bytes<T, RW>(e) <= 64 * 1024; }
 
 template <class T, int RW>
-static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStream_t s) {
+static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing &ring, hipStream_t s) {
     // persistent waves: every CU holds the same number of workgroups (the LDS request caps
     // them at ceil(B / CUs) per CU, 160 KiB of LDS per CU), or the fuller CUs pace each step
-    static int ncu = 0;
-    if (ncu == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-    }
+    const int ncu = device_cu_count();
     const int occ = (e.B + ncu - 1) / ncu;
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     // nontemporal observation stores for slot buffers (fresh lines every step) and for a
@@ -283,13 +295,7 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
     auto kern = nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
     // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
     // (512 per lane) over the waves it must hold, 4 SIMDs per CU
-    static int vgprs[2] = {0, 0};
-    int &vg = vgprs[nt ? 1 : 0];
-    if (vg == 0) {
-        hipFuncAttributes fa{};
-        vg = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern)) == hipSuccess && fa.numRegs > 0
-                 ? fa.numRegs : 512;
-    }
+    const int vg = kernel_vgprs(reinterpret_cast<const void *>(kern));
     const int fit = 512 / ((vg + 7) & ~7);
     bool pipe = (2 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit;
     if (const char *v = std::getenv("MAPF_WIDE_PIPE")) pipe = pipe && std::atoi(v) != 0;
@@ -308,7 +314,13 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, hipStre
 #endif
     size_t lds = wide_lds_bytes<T, RW>(e, r.grid, r.overlap);
     if (cap > lds && cap <= 64 * 1024) lds = cap;
+#if MAPF_ARGS_PTR
+    const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
+    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, args, steps);
+#else
+    (void)ring;
     hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, r);
+#endif
 }
 
 // the search row type of a W-wide map; RW = 2 above 64 rows
@@ -321,15 +333,18 @@ static auto with_row_type(const DevEnv &e, F f) {
 }
 
 bool rollout_wide_fusable(const DevEnv &e) {
+    // the HP snapshot holds human.path[1..k_predict] one lane per cell (lanes 1..63)
+    if (e.use_hp && e.C >= 6 && e.k_predict > 63) return false;
     return with_row_type(e, [&](auto t, auto rw) { return wide_fits<decltype(t), decltype(rw)::value>(e); });
 }
 
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                         int slots, hipStream_t s) {
-    static int remap = -1;
-    if (remap < 0) { const char *v = std::getenv("MAPF_XCD_REMAP"); remap = v ? std::atoi(v) != 0 : 1; }
-    const WideOut ro{actions, out, obs, vec, slots, remap, 0, 0, 0};
-    with_row_type(e, [&](auto t, auto rw) { launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, s); return 0; });
+                         int slots, ArgRing &ring, hipStream_t s) {
+    const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0};
+    with_row_type(e, [&](auto t, auto rw) {
+        launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
+        return 0;
+    });
 }
 
 }  // namespace mapf

@@ -79,13 +79,18 @@ class OneEpPerformance:
 
 def _row_index(idx, n, device):
     """A driver-style row index (int, slice, int array/list/tensor, bool mask) over n rows ->
-    (int64 tensor of rows in [0, n) on `device`, True if idx was a scalar)."""
+    (int64 rows in [0, n), True if idx was a scalar).  Host indices (what driver.py passes:
+    numpy mb_inds) are checked and wrapped on the host and come back as a host array --
+    no device synchronisation; device tensors stay on the device (their bounds check reads
+    two scalars back)."""
     if isinstance(idx, (int, np.integer)):
         if not -n <= int(idx) < n:
             raise IndexError(f"row {int(idx)} out of range for {n} rows")
-        return torch.tensor([int(idx) % n], device=device), True
+        return np.array([int(idx) % n], np.int64), True
     if isinstance(idx, slice):
-        return torch.arange(*idx.indices(n), device=device), False
+        return np.arange(*idx.indices(n), dtype=np.int64), False
+    if isinstance(idx, torch.Tensor) and idx.device.type == "cpu":
+        idx = idx.numpy()
     if not isinstance(idx, torch.Tensor):
         idx = np.asarray(idx)
         if idx.dtype == np.bool_:
@@ -94,8 +99,11 @@ def _row_index(idx, n, device):
             idx = np.flatnonzero(idx)
         elif idx.size and not np.issubdtype(idx.dtype, np.integer):
             raise IndexError(f"row indices must be integers, not {idx.dtype}")
-        idx = torch.from_numpy(idx.astype(np.int64, copy=False))
-    elif idx.dtype == torch.bool:
+        idx = idx.astype(np.int64, copy=False).reshape(-1)
+        if idx.size and (idx.min() < -n or idx.max() >= n):
+            raise IndexError("row index out of range")
+        return (idx % n if n else idx), False
+    if idx.dtype == torch.bool:
         if tuple(idx.shape) != (n,):
             raise IndexError(f"boolean index of shape {tuple(idx.shape)} for {n} rows")
         idx = idx.nonzero().squeeze(1)
@@ -104,7 +112,25 @@ def _row_index(idx, n, device):
     idx = idx.to(device=device, dtype=torch.int64).reshape(-1)
     if idx.numel() and (int(idx.min()) < -n or int(idx.max()) >= n):
         raise IndexError("row index out of range")
-    return idx % n if n else idx, False
+    return (idx % n if n else idx), False
+
+
+class _IndexCache:
+    """driver.py:131-134 indexes twelve attributes with the same mb_inds: the device copy of
+    a host index array (and its (step, env) split) is made once per minibatch, not per
+    attribute.  Keyed by the array's bytes; one entry."""
+
+    def __init__(self):
+        self.key, self.val = None, None
+
+    def get(self, rows, tag, device, make):
+        key = (rows.tobytes(), tag, str(device))
+        if key != self.key:
+            self.key, self.val = key, make()
+        return self.val
+
+
+_INDEX_CACHE = _IndexCache()
 
 
 class _DeviceRows:
@@ -149,7 +175,12 @@ class EnvMajorRows(_DeviceRows):
         self.dtype, self.device = buf.dtype, buf.device
 
     def _gather(self, rows):
-        return self.buf[rows % self.T, rows // self.T]
+        T = self.T
+        if isinstance(rows, np.ndarray):       # host rows: one H2D copy of (step, env) per minibatch
+            ts, bs = _INDEX_CACHE.get(rows, ("env-major", T), self.device, lambda: tuple(
+                torch.from_numpy(np.stack([rows % T, rows // T])).to(self.device, non_blocking=True)))
+            return self.buf[ts, bs]
+        return self.buf[rows % T, rows // T]
 
     def materialize(self):
         return self.buf.transpose(0, 1).reshape(self.shape)
@@ -164,7 +195,8 @@ class ZeroRows(_DeviceRows):
         self.dtype, self.device = torch.float32, torch.device(device)
 
     def _gather(self, rows):
-        return torch.zeros((), device=self.device).expand((rows.numel(),) + tuple(self.shape[1:]))
+        k = rows.size if isinstance(rows, np.ndarray) else rows.numel()
+        return torch.zeros((), device=self.device).expand((k,) + tuple(self.shape[1:]))
 
     def materialize(self):
         return torch.zeros(self.shape, device=self.device)
@@ -185,6 +217,17 @@ class ConcatRows(_DeviceRows):
         self._bounds = torch.tensor(self.offsets[1:], device=self.device)
 
     def _gather(self, rows):
+        if isinstance(rows, np.ndarray):       # host rows: split by part on the host
+            part = np.searchsorted(np.asarray(self.offsets[1:]), rows, side="right")
+            if (part == part[:1]).all() if rows.size else True:   # one part (driver.py: runner 0's rows)
+                k = int(part[0]) if rows.size else 0
+                return self.parts[k]._gather(rows - self.offsets[k])
+            out = torch.empty((rows.size,) + tuple(self.shape[1:]), dtype=self.dtype, device=self.device)
+            for k, p in enumerate(self.parts):
+                sel = np.flatnonzero(part == k)
+                if sel.size:
+                    out[torch.from_numpy(sel).to(self.device)] = p._gather(rows[sel] - self.offsets[k])
+            return out
         part = torch.bucketize(rows, self._bounds, right=True)
         out = torch.empty((rows.numel(),) + tuple(self.shape[1:]), dtype=self.dtype, device=self.device)
         for k, p in enumerate(self.parts):

@@ -192,7 +192,7 @@ def test_g3_astar_paths_and_bfs_on_device():
             np.testing.assert_array_equal(bfs[b, 0], ref_bfs, err_msg=f"bfs map {mi} case {k}")
             if not z["ok"][k]:
                 unreachable += 1
-                assert st["human"][b, 7] == 1
+                assert st["human"][b, 7] == 2      # stays put two steps
                 continue
             path = z["path"][offs[k]:offs[k + 1]]            # goal -> start (construct_path_from_dict)
             want = np.concatenate([path[::-1], path[1:]])     # Human.getAstarPath (mapf_gym.py:33-37)
@@ -750,3 +750,45 @@ def test_vector_every_offset_on_80x80():
             d = d2 ** .5
             want[k] = [np.float32(dx[k] / d), np.float32(dy[k] / d), np.float32(d), 0.0]
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("name,B,H,n,fov,nch,steps", [("c4_split_40x40_n16", 48, 40, 16, 9, 6, 80),
+                                                      ("c5_split_80x80_n64_bfsch", 4, 80, 64, 11, 7, 40)])
+def test_split_path_back_to_back_steps_match_oracle(name, B, H, n, fov, nch, steps):
+    """The per-step split path (step launch, then observe with the step's search forked onto
+    aux streams; the humans' next paths joined only two steps later, mapf_api.cpp
+    join_deferred) driven back to back with NO host synchronisation, get_state or bfs in
+    between -- every step's outputs and observation into [T]-slot device buffers -- so each
+    deferred search really runs beside the next step.  Compared with the oracle at the end."""
+    rng = np.random.default_rng(11)
+    from mapf_amd.maps import keep_largest_component, random_map
+    maps = np.stack([keep_largest_component(random_map(rng, H, H, 0.3)) for _ in range(B)])
+    seed = 0xD0F + B
+    env = mk_env(B=B, H=H, W=H, num_agents=n, fov=fov, num_channel=nch, human_mode="random", goal_mode="random",
+                 fix_choice=1, shared_map=False, seed=seed, env_offset=3)
+    env.reset_seeded(maps)
+    assert not env.fused, "expected the split (step + observe) path"
+    dev = env.device
+    acts = torch.zeros(steps, B, n, dtype=torch.int32, device=dev)
+    obs = torch.full((steps, B, n, nch, fov, fov), float("nan"), device=dev)
+    vec = torch.full((steps, B, n, 4), float("nan"), device=dev)
+    outs = {k: torch.zeros((steps,) + tuple(v.shape), dtype=v.dtype, device=dev) for k, v in env.out.items()}
+    for t in range(steps):
+        env.step_observe(acts[t], obs[t], vec[t], random_policy=True, out={k: v[t] for k, v in outs.items()})
+    torch.cuda.synchronize()
+    acts, obs, vec, outs = acts.cpu().numpy(), obs.cpu().numpy(), vec.cpu().numpy(), host(outs)
+    cfg = O.make_config(H, H, n, fov, nch, human_mode=1, goal_mode=1, fix_choice=1, seed=seed, env_offset=3)
+    for b in range(B):
+        oe = O.OracleEnv(cfg, env_id=3 + b)
+        oe.reset_random(maps[b])
+        for t in range(steps):
+            np.testing.assert_array_equal(acts[t, b], oe.random_actions(), err_msg=f"{name} actions t={t} b={b}")
+            o = oe.step(acts[t, b])
+            for k, key in [("status", "status"), ("reward", "reward"), ("cost", "cost"), ("train_valid", "valid"),
+                           ("actions_fixed", "fixed"), ("goals_reached", "goals"), ("constraints", "constr")]:
+                np.testing.assert_array_equal(outs[k][t, b], o[key].astype(outs[k].dtype),
+                                              err_msg=f"{name} t={t} b={b} {k}")
+            oo, ov = oe.observe()
+            np.testing.assert_array_equal(obs[t, b], oo, err_msg=f"{name} t={t} b={b} obs")
+            np.testing.assert_array_equal(vec[t, b], ov, err_msg=f"{name} t={t} b={b} vec")
+    assert_no_errors(env, allow=(1, 2))

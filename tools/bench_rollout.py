@@ -14,6 +14,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
@@ -71,7 +72,7 @@ def main():
         print(json.dumps(out), flush=True)
     if args.train:
         rows = args.minibatch
-        idx = torch.arange(rows, device=dev)
+        idx = np.arange(rows)            # host indices, as driver.py:125-130's mb_inds
         sl = lambda k: mb[k][idx]
         def upd():
             return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),

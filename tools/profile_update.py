@@ -11,6 +11,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
@@ -34,7 +35,7 @@ def main():
     model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=9)
     runner = DeviceRunner(env, model, n_steps=1, seed=0)
     mb, _ = runner.run()
-    idx = torch.arange(args.rows, device=dev)
+    idx = np.arange(args.rows)         # host indices, as driver.py:125-130's mb_inds
     sl = lambda k: mb[k][idx]
 
     def upd():
