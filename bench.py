@@ -169,7 +169,8 @@ def make_maps(kind, B, H, W, rank):
 # workload's (B, N, H, W, F, C) and kernel
 PMC_REPORTS = {((4096, 8, 20, 20, 11, 6), "observe_kernel"): "r01_pmc_observe_c2.json",
                ((4096, 8, 20, 20, 11, 6), "step_observe_kernel"): "r01_pmc_step_observe_c2.json",
-               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r01_pmc_rollout_c2.json",   # [B] buffers
+               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r03_pmc_rollout_c2.json",   # [B] buffers
+               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel<true>"): "r03_pmc_rollout_c2slots.json",
                ((1024, 16, 40, 40, 9, 6), "rollout_wide_kernel"): "r02_pmc_rollout_wide_c4.json",
                ((2048, 64, 80, 80, 11, 7), "rollout_wide_kernel"): "r02_pmc_rollout_wide_c5.json"}
 
@@ -434,7 +435,7 @@ def main():
         else:
             kname, bpa, kms, steps_pl = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms, 1
         achieved = bpa * B * N * steps_pl / (kms * 1e-3) / 1e9
-        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname.split("<")[0])
+        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname.split("<")[0] + ("<true>" if roll else ""))
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),

@@ -256,8 +256,8 @@ static int human_astar(oc_env *e, oc_cell from, oc_cell to, int round_trip) {
     int *rc = (int *)malloc(sizeof(int) * 2 * cap);
     int len = oc_astar(e->map, e->H, e->W, from.r, from.c, to.r, to.c, rc, cap);
     if (len <= 0) {           /* [] or ValueError: the reference crashes next; this build's */
-        free(rc); e->errors++; /* human stays put two steps (csrc/mapf_search.h: search_one) */
-        e->hpath[0] = from; e->hpath[1] = from; e->hlen = 2; return -1;
+        free(rc); e->errors++; /* human stays put three steps (csrc/mapf_search.h: search_one) */
+        e->hpath[0] = from; e->hpath[1] = from; e->hpath[2] = from; e->hlen = 3; return -1;
     }
     int n = 0;
     for (int k = len - 1; k >= 0; --k) { e->hpath[n].r = rc[2 * k]; e->hpath[n].c = rc[2 * k + 1]; ++n; }

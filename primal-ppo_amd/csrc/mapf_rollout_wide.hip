@@ -40,6 +40,7 @@ struct WideOut {
     int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
     int overlap;        // pipelined, no BFS channel: one barrier per step (wide_overlap_bytes)
     int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
+    int prio;           // pipelined: the stepping wave's issue priority (s_setprio; MAPF_WIDE_PRIO)
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -226,6 +227,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     // within the instruction cache); unpipelined, the one wave takes both roles in the
     // order step -> BFS maps -> snapshot -> human path -> observe
     bool stepper = !pipe || role == 0, observer = !pipe || role == 1;
+    // the stepping wave bounds the pipeline and shares its SIMD with another env's observing
+    // wave, whose work waits on store issue anyway: it goes first when both are ready
+    if (pipe && stepper && ro.prio) __builtin_amdgcn_s_setprio(3);
 #ifdef MAPF_STAMPS
     // phase-cost experiment (no observations written): the stepping role alone
     if (ro.exp == 1) observer = false;
@@ -340,7 +344,8 @@ bool rollout_wide_fusable(const DevEnv &e) {
 
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, ArgRing &ring, hipStream_t s) {
-    const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0};
+    const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
+                     env_flag("MAPF_WIDE_PRIO", 0)};
     with_row_type(e, [&](auto t, auto rw) {
         launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
         return 0;

@@ -425,12 +425,15 @@ __device__ __attribute__((always_inline)) inline int search_one(const DevEnv &e,
             uint32_t *path = human_path(e, b, buf);
             if (d <= 0) {
                 // start == goal (astar_4 returns []) or unreachable (it returns a ValueError):
-                // the reference crashes right after; the human stays put for two steps.  Two,
-                // not one: a path's end is read the step after it is switched to, and at
-                // length 1 that step would already switch to the NEXT path -- whose search
-                // (mapf_api.cpp: deferred joins) may still be running beside that step.
-                if (lane == 0) { atomicAdd(&e.counters[C_UNREACHABLE], 1u); path[0] = sr_cell; path[1] = sr_cell; }
-                len = 2;
+                // the reference crashes right after; the human stays put for three steps (the
+                // shortest round trip).  Never one: a 1-cell path is left the step after it is
+                // switched to, i.e. before the search of the path after it -- deferred beside
+                // the next step (mapf_api.cpp: join_deferred) -- is guaranteed done.
+                if (lane == 0) {
+                    atomicAdd(&e.counters[C_UNREACHABLE], 1u);
+                    path[0] = sr_cell; path[1] = sr_cell; path[2] = sr_cell;
+                }
+                len = 3;
             } else {
                 // walk back from the goal on the scalar unit: parent = predecessor neighbour with
                 // the largest (manhattan-to-goal, row, col) -- astar_4's last overwrite (:58)

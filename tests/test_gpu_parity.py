@@ -192,7 +192,7 @@ def test_g3_astar_paths_and_bfs_on_device():
             np.testing.assert_array_equal(bfs[b, 0], ref_bfs, err_msg=f"bfs map {mi} case {k}")
             if not z["ok"][k]:
                 unreachable += 1
-                assert st["human"][b, 7] == 2      # stays put two steps
+                assert st["human"][b, 7] == 3      # stays put three steps
                 continue
             path = z["path"][offs[k]:offs[k + 1]]            # goal -> start (construct_path_from_dict)
             want = np.concatenate([path[::-1], path[1:]])     # Human.getAstarPath (mapf_gym.py:33-37)
