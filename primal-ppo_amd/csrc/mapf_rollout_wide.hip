@@ -40,7 +40,7 @@ struct WideOut {
     int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
     int overlap;        // pipelined, no BFS channel: one barrier per step (wide_overlap_bytes)
     int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
-    int prio;           // pipelined: the stepping wave's issue priority (s_setprio; MAPF_WIDE_PRIO)
+    int prio;           // pipelined: the stepping wave's issue priority (s_setprio; MAPF_WIDE_PRIO, default 1: c4 -1.6 %)
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -69,7 +69,7 @@ __host__ __device__ inline size_t wide_cost_bytes(const DevEnv &e) {
     return n <= 1024 ? wide_a16(n) : 0;
 }
 
-__host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide_a16((size_t)(e.H + 4) * (e.W + 4)); }
+__host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide_a16((size_t)(e.H + 4) * (e.W + 4) * 2); }
 
 // the overlapped pipeline's own areas: a second observation snapshot (spos | sgoal | shn |
 // shp | shpn) and the stepper's BFS image
@@ -202,17 +202,37 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     const StepSrc src{L.mapc, lcost, grid};   // obstacle tests, cost table, neighbour grid in LDS
     const WaveGroup g;                     // the env is the whole wave: exchanges by v_readlane
     const size_t BN = (size_t)e.B * e.N, CFF = (size_t)e.C * e.F * e.F;
-    auto step_out = [&](size_t s) {
-        StepOut o = ro.out;
-        if (o.status) o.status += s * BN;
-        if (o.reward) o.reward += s * BN;
-        if (o.shadow_goals) o.shadow_goals += s * e.B;
-        if (o.cost) o.cost += s * BN;
-        if (o.train_valid) o.train_valid += s * BN * NA;
-        if (o.actions_fixed) o.actions_fixed += s * BN;
-        if (o.goals_reached) o.goals_reached += s * BN;
-        if (o.constraints) o.constraints += s * BN;
-        if (o.reward_total) o.reward_total += s * BN;
+    // this lane's output elements as VGPR pointers (step_group<.., LANEPTR>): the nine output
+    // bases and the actions base would otherwise hold 20 SGPRs through the loop -- spilled to
+    // VGPR lanes and read back (v_readlane pairs) at every store.  Slot buffers advance them
+    // by one [B, N] slice per step.
+    const size_t lai = (size_t)b * e.N + (size_t)min(lane, e.N - 1);
+    auto vptr = [](auto *p, size_t off) {
+        uint64_t v = p ? (uint64_t)(p + off) : 0ull;
+        asm volatile("" : "+v"(v));          // opaque and lane-held: never re-derived from the base
+        return reinterpret_cast<decltype(p)>(v);
+    };
+    const StepOut &O = ro.out;
+    const uint32_t have = (O.status ? 1u : 0u) | (O.reward ? 2u : 0u) | (O.shadow_goals ? 4u : 0u) |
+                          (O.cost ? 8u : 0u) | (O.train_valid ? 16u : 0u) | (O.actions_fixed ? 32u : 0u) |
+                          (O.goals_reached ? 64u : 0u) | (O.constraints ? 128u : 0u) | (O.reward_total ? 256u : 0u);
+    const StepOut lo{vptr(O.status, lai), vptr(O.reward, lai), vptr(O.shadow_goals, (size_t)b), vptr(O.cost, lai),
+                     vptr(O.train_valid, lai * NA), vptr(O.actions_fixed, lai), vptr(O.goals_reached, lai),
+                     vptr(O.constraints, lai), vptr(O.reward_total, lai)};
+    int32_t *const lact = vptr(ro.actions, lai);
+    auto step_out = [&](size_t s) {      // slot s of every output (s = 0: the [B]-leading buffers)
+        StepOut o = lo;
+        if (s) {
+            o.status += s * BN;
+            o.reward += s * BN;
+            o.shadow_goals += s * e.B;
+            o.cost += s * BN;
+            o.train_valid += s * BN * NA;
+            o.actions_fixed += s * BN;
+            o.goals_reached += s * BN;
+            o.constraints += s * BN;
+            o.reward_total += s * BN;
+        }
         return o;
     };
     auto bfs_maps = [&](const StepInline &inl) {
@@ -238,7 +258,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
         StepInline inl;
-        if (stepper) step_group<WaveGroup, true>(e, ro.actions + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs);
+        if (stepper) step_group<WaveGroup, true, true>(e, lact + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs, have);
         WSTAMP(0);
         // A: observation t-1 done.  Nothing the observer reads from HBM was written by the step
         // (its outputs and state are not read back), so the stepper does not wait for them.
@@ -345,7 +365,7 @@ bool rollout_wide_fusable(const DevEnv &e) {
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, ArgRing &ring, hipStream_t s) {
     const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
-                     env_flag("MAPF_WIDE_PRIO", 0)};
+                     env_flag("MAPF_WIDE_PRIO", 1)};
     with_row_type(e, [&](auto t, auto rw) {
         launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
         return 0;

@@ -117,7 +117,7 @@ __device__ inline void step_regs_store(const DevEnv &e, int b, int i, const Step
 struct StepSrc {
     const uint32_t *map = nullptr;
     const float *cost = nullptr;
-    uint8_t *grid = nullptr;      // (H + 4) x (W + 4) bytes of LDS scratch, whole-wave envs only
+    uint8_t *grid = nullptr;      // (H + 4) x (W + 4) u16 of LDS scratch, whole-wave envs only
 };
 
 // One env's step on the group g (lane i of the group = agent i; G >= N).  The
@@ -129,16 +129,22 @@ struct StepSrc {
 // wave-uniform, and a readlane costs a few cycles where a bpermute costs an LDS round trip).
 // REGS: the env's state comes from and goes back to `rg` (register-resident, persistent
 // callers) instead of being loaded from HBM (it is still stored to HBM).
-template <class Grp, bool REGS = false>
+// LANEPTR (the wide rollout): `actions` and every per-agent pointer of `out` are already this
+// lane's element (shadow_goals this env's), held in VGPRs by the caller, and `have` says which
+// outputs exist (bit k = the k-th StepOut field) -- the output bases then take no SGPRs in the
+// step loop, where they were spilled to VGPR lanes and read back at every store.
+template <class Grp, bool REGS = false, bool LANEPTR = false>
 __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e, int32_t *__restrict__ actions,
                                                                 const StepOut &out, uint32_t flags, int parity, int b,
                                                                 const Grp &g, StepInline *inl, StepSrc src,
-                                                                StepRegs &rg) {
+                                                                StepRegs &rg, uint32_t have = 0) {
     const int N = e.N;
     STAMP_BEGIN();
     const int i = g.i;
     const bool act = i < N;
     const size_t ai = (size_t)b * N + i;
+    const size_t oi = LANEPTR ? 0 : ai, ob = LANEPTR ? 0 : (size_t)b;   // output element indices
+    auto has = [&](int k, const void *p) { return LANEPTR ? ((have >> k) & 1u) != 0 : p != nullptr; };
     const uint32_t env_id = e.env_offset + (uint32_t)b;
     const uint32_t clock = REGS ? rg.clock : e.clock[b];
 
@@ -197,10 +203,10 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     if (flags & 2u) {          // random policy fused in: same stream as random_actions_kernel
         if (act) {
             a = random_action(philox(env_id, P_ACT | ((uint32_t)(i >> 3) << 8), clock, 0u, e.seed), i);
-            actions[ai] = a;
+            actions[oi] = a;
         }
     } else if (act) {
-        a = actions[ai];
+        a = actions[oi];
         if (a < 0 || a >= NA) { atomicAdd(&e.counters[C_BAD_ACTION], 1u); a = 0; }
     }
     // REGS callers hold the map rows, cost table and neighbour grid in LDS: typed as such
@@ -259,13 +265,14 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         if ((cj >> a) & 1u) M |= 1ull << j;
     };
     if (REGS && src.grid) {
-        // The agents within distance 2 straight from an LDS grid of agent indices (the env
-        // is the whole wave, its lanes the agents): 12 neighbour cells per lane instead of
-        // a loop over all N agents.  Grid = (H + 4) x (W + 4) bytes, 2-cell border, 0xFF
-        // empty; positions are distinct, so a cell holds at most one agent.
-        const int GW = e.W + 4, gwords = ((e.H + 4) * GW + 3) >> 2;
+        // The agents within distance 2 straight from an LDS grid (the env is the whole wave,
+        // its lanes the agents): 12 neighbour cells per lane instead of a loop over all N
+        // agents.  Grid = (H + 4) x (W + 4) u16, 2-cell border; a cell holds its agent's
+        // index | action << 8 (0xFFFF empty) -- positions are distinct, so at most one --
+        // so one read gives a neighbour and its action, no cross-lane exchange.
+        const int GW = e.W + 4, gwords = ((e.H + 4) * GW * 2 + 3) >> 2;
         const int lane = lane_id();
-        const auto grid = as_lds(src.grid);
+        const auto grid = as_lds(reinterpret_cast<uint16_t *>(src.grid));
         // cleared 16 B per lane (the grid's LDS area is 16-B aligned and padded to 16 B)
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const auto grid128 = as_lds(reinterpret_cast<u32x4 *>(src.grid));
@@ -274,26 +281,23 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
         __builtin_amdgcn_wave_barrier();
         // lanes past N read around the grid's cell (0, 0) (result dropped): no branch per read
         const int me = act ? (pr + 2) * GW + pc + 2 : 2 * GW + 2;
-        if (act) grid[me] = (uint8_t)i;
+        if (act) grid[me] = (uint16_t)(i | (a << 8));
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // A neighbour's offset is fixed by its slot, so pair()'s tests fold into constants:
         // NKEYS[o] = the keys it contributes, NCONF[o] bits 5aj..5aj+4 = my actions colliding
-        // with its action aj (same target, or a swap).
-        // All twelve permutes issue back to back (every lane permutes), then one wait and a
-        // branch-free fold: interleaved with per-slot branches, each waited on its own.
-        int nb[12], aj[12];
+        // with its action aj (same target, or a swap).  All twelve reads issue back to back,
+        // then one wait and a branch-free fold.
+        int nb[12];
 #pragma unroll
         for (int o = 0; o < 12; ++o) {
             const int v = (int)grid[me + NBR_DR[o] * GW + NBR_DC[o]];
-            nb[o] = act ? v : 0xFF;
+            nb[o] = act ? v : 0xFFFF;
         }
 #pragma unroll
-        for (int o = 0; o < 12; ++o) aj[o] = (int)shfl32((uint32_t)a, nb[o] == 0xFF ? lane : nb[o]);
-#pragma unroll
         for (int o = 0; o < 12; ++o) {
-            const bool h = nb[o] != 0xFF;
-            const unsigned cj = h ? (NCONF[o] >> (5 * aj[o])) & 0x1Fu : 0u;
+            const bool h = nb[o] != 0xFFFF;
+            const unsigned cj = h ? (NCONF[o] >> (5 * (nb[o] >> 8))) & 0x1Fu : 0u;
             keys |= h ? NKEYS[o] : 0u;
             conf |= cj;
             M |= (uint64_t)((cj >> a) & 1u) << (nb[o] & 63);
@@ -351,28 +355,28 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const int cd0 = prow(hn) - Xr, cd1 = pcol(hn) - Xc;
     const int cd2 = cd0 * cd0 + cd1 * cd1;
     const bool cin = cd2 <= e.R * e.R;
-    if (act && out.cost) {
+    if (act && has(3, out.cost)) {
         if (REGS && src.cost) {
-            out.cost[ai] = cin ? as_lds(src.cost)[cd2] : 0.f;
+            out.cost[oi] = cin ? as_lds(src.cost)[cd2] : 0.f;
         } else {
             const float c = cin ? e.cost_lut[cd2] : 0.f;
             // REGS: the load's wait here, on this path only, so nothing is pending at the join
             if constexpr (REGS) __builtin_amdgcn_s_waitcnt(0x0F70);
-            out.cost[ai] = c;
+            out.cost[oi] = c;
         }
     }
 
     if (act) {
-        if (out.status) out.status[ai] = (int8_t)st;
-        if (out.reward) out.reward[ai] = rw;
-        if (out.train_valid) {   // getTrainValid (:535-550)
-            float *tv = out.train_valid + ai * NA;
+        if (has(0, out.status)) out.status[oi] = (int8_t)st;
+        if (has(1, out.reward)) out.reward[oi] = rw;
+        if (has(4, out.train_valid)) {   // getTrainValid (:535-550)
+            float *tv = out.train_valid + oi * NA;
 #pragma unroll
             for (int t = 0; t < NA; ++t)
                 tv[t] = (((good >> t) & 1u) || (((keys >> t) & 1u) && !((conf >> t) & 1u))) ? 1.f : 0.f;
         }
     }
-    if (i == 0 && out.shadow_goals) out.shadow_goals[b] = popc64(shadow_mask);
+    if (i == 0 && has(2, out.shadow_goals)) out.shadow_goals[ob] = popc64(shadow_mask);
     if (inl) inl->replan = false;
     if (!(flags & 1u)) return;
 
@@ -576,10 +580,10 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     if (act) {
         const int d0 = prow(hp_new) - nr, d1 = pcol(hp_new) - nc;
         const float cv = (d0 * d0 + d1 * d1 <= e.constr_d2) ? 1.f : 0.f;   // (:632-633)
-        if (out.actions_fixed) out.actions_fixed[ai] = fixed;
-        if (out.goals_reached) out.goals_reached[ai] = reached ? 1.f : 0.f;
-        if (out.constraints) out.constraints[ai] = cv;
-        if (out.reward_total) out.reward_total[ai] = reached ? rw + e.goal_reward : rw;   // runner.py:89-91
+        if (has(5, out.actions_fixed)) out.actions_fixed[oi] = fixed;
+        if (has(6, out.goals_reached)) out.goals_reached[oi] = reached ? 1.f : 0.f;
+        if (has(7, out.constraints)) out.constraints[oi] = cv;
+        if (has(8, out.reward_total)) out.reward_total[oi] = reached ? rw + e.goal_reward : rw;   // runner.py:89-91
     }
     STAMP(6);
     STAMP_END();

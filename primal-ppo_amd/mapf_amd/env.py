@@ -241,6 +241,18 @@ class BatchedMapfGym:
         [T]-leading buffers (actions [T, B, N], obs [T, B, N, C, F, F], vec [T, B, N, 4],
         out[k] [T, ...]); otherwise every step overwrites the [B]-leading buffers.
         Returns (out, obs, vec)."""
+        if not slots and actions is None and obs is None and vec is None and out is None:
+            # the default [B]-leading buffers (checked at construction): the call's arguments are
+            # built once -- a 20-step rollout takes ~300 us on the GPU, so the host's ~8 us of
+            # argument checks and ctypes wrapping per call were 2-3 % of it
+            key = (id(self.h), id(self.actions), id(self.obs), id(self.vec), id(self._stepout))
+            fast = getattr(self, "_roll_fast", None)
+            if fast is None or fast[0] != key:
+                fast = self._roll_fast = (key, _lib.lib().mapf_rollout_random, self.h, ctypes.byref(self._stepout),
+                                          _ptr(self.actions), _ptr(self.obs), _ptr(self.vec))
+            _, fn, h, so, pa, po, pv = fast
+            _lib.check(fn(h, int(T), 0, pa, so, po, pv, _stream(self.device)))
+            return self.out, self.obs, self.vec
         k = T if slots else 1
         actions = self.actions if actions is None else actions
         obs = self.obs if obs is None else obs
