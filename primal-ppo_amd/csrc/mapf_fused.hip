@@ -141,7 +141,6 @@ struct RolloutOut {
     float *obs, *vec;
     int slots;
     int xcd_remap;
-    int skew;           // experiment (MAPF_ROLL_SKEW): workgroup k of a CU starts k * skew * 64 cycles late
 };
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
 struct RolloutArgs {
@@ -199,9 +198,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     // register's load "pending" at the loop header and waits vmcnt(0) -- i.e. behind
     // all of the previous step's stores -- where the loop uses it
     __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt/lgkmcnt untouched
-    // (the k-th workgroup dispatched to a CU: blockIdx.x / 256 on 256 CUs; its waves share
-    // their SIMDs with the other workgroups' waves)
-    for (int k = ro.skew * (((int)blockIdx.x >> 8) & 3); k > 0; --k) __builtin_amdgcn_s_sleep(1);
     for (int t = 0; t < T; ++t) {
         const DevEnv &E = e;
         const RolloutOut &R = ro;
@@ -248,14 +244,14 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
     const int remap = env_flag("MAPF_XCD_REMAP", 1) != 0;
 #if MAPF_ARGS_PTR
-    const RolloutArgs *args = push_args(ring, RolloutArgs{e, RolloutOut{actions, out, obs, vec, slots, remap, env_flag("MAPF_ROLL_SKEW", 0)}}, s);
+    const RolloutArgs *args = push_args(ring, RolloutArgs{e, RolloutOut{actions, out, obs, vec, slots, remap}}, s);
     if (slots)
         hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, args, T);
     else
         hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, args, T);
 #else
     (void)ring;
-    const RolloutOut ro{actions, out, obs, vec, slots, remap, env_flag("MAPF_ROLL_SKEW", 0)};
+    const RolloutOut ro{actions, out, obs, vec, slots, remap};
     if (slots)
         hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T, ro);
     else

@@ -251,6 +251,7 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const int Xr = pr + dr(a), Xc = pc + dc(a);
     unsigned keys = 0, conf = 0;   // conf: my actions t that collide with some j's actual action
     uint64_t M = 0;                // agents j colliding with my actual action
+    unsigned hitM = 0;             // grid path: M != 0 (M is then built lazily, per scanned agent)
     // the pair test of agent j at (qr, qc) taking action aj (only pairs within distance 2 matter)
     auto pair = [&](int j, int qr, int qc, int aj) {
         const int Yr = qr + dr(aj), Yc = qc + dc(aj);
@@ -300,7 +301,7 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
             const unsigned cj = h ? (NCONF[o] >> (5 * (nb[o] >> 8))) & 0x1Fu : 0u;
             keys |= h ? NKEYS[o] : 0u;
             conf |= cj;
-            M |= (uint64_t)((cj >> a) & 1u) << (nb[o] & 63);
+            hitM |= (cj >> a) & 1u;     // M itself is built only for the scan's agents (below)
         }
     } else {
         for (int j = 0; j < N; ++j) {
@@ -321,7 +322,7 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     if ((st_mask >> a) & 1u) s0 = -1;
     else if ((hu_mask >> a) & 1u) s0 = -2;
     else if ((good >> a) & 1u) s0 = 1;
-    else if (M) { s0 = -3; cb = true; }
+    else if (M || hitM) { s0 = -3; cb = true; }
     else s0 = ((rep_mask >> a) & 1u) ? -4 : 1;
     // sequential scan: agent k is skipped if an earlier agent already set it to
     // -3; an agent taking the conflict branch sets itself and all of M_k to -3
@@ -329,7 +330,17 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     uint64_t T = 0;
     for (uint64_t rem = g.ballot(act && cb); rem; rem &= rem - 1) {
         const int k = ctz64(rem);
-        const uint64_t Mk = g.shfl64(M, k);
+        uint64_t Mk;
+        if (REGS && src.grid) {
+            // M_k = the agents whose actual action collides with k's: same target, or a swap
+            // (a symmetric relation, so every lane tests itself against k) -- built here for
+            // the few agents in the conflict branch instead of per lane over 12 grid slots
+            const int kr = __builtin_amdgcn_readlane(pr, k), kc = __builtin_amdgcn_readlane(pc, k);
+            const int kxr = __builtin_amdgcn_readlane(Xr, k), kxc = __builtin_amdgcn_readlane(Xc, k);
+            Mk = g.ballot(act && i != k && ((Xr == kxr && Xc == kxc) || (Xr == kr && Xc == kc && kxr == pr && kxc == pc)));
+        } else {
+            Mk = g.shfl64(M, k);
+        }
         if (!((T >> k) & 1ull)) T |= Mk | (1ull << k);
     }
     const int st = ((T >> i) & 1ull) ? -3 : s0;
@@ -392,8 +403,15 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const uint64_t need = g.ballot(act && (st == -1 || st == -2 || st == -3));
     if (need) {
         int assigned = (act && st == 1) ? a : -1;
-        const uint64_t qm = g.ballot(act && st < 0);
-        int q = (act && st < 0) ? popc64(qm & below(i)) : -1;
+        // Worklist agents with a good action take its min at once: a good action collides
+        // with no action of any agent (no agent within reach of its target), so it never
+        // enters another agent's conflict set U and is never evicted -- its turn in the
+        // sequential order decides nothing.  The loop walks only the others, in order (an
+        // evicted agent re-queued later may still have one: the loop keeps that case).
+        const bool wl = act && st < 0;
+        if (wl && good) assigned = __builtin_ctz(good);
+        const uint64_t qm = g.ballot(wl && !good);
+        int q = (wl && !good) ? popc64(qm & below(i)) : -1;
         int next_q = popc64(qm), head = 0, draws = 0;
         const unsigned viable_me = ~(st_mask | hu_mask) & 0x1Fu;
         while (head < next_q) {

@@ -342,10 +342,15 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint32_t need = agents_of(eballot(head && vi && (st == -1 || st == -2 || st == -3)));
     if (need) {
         const int st_j = (int)shfl32((uint32_t)st, base + j * NP);
+        const unsigned good_j = shfl32(good, base + j * NP);
         int asg_i = (vi && st == 1) ? a_i : -1;
         int asg_j = (vj && st_j == 1) ? a_j : -1;
-        const uint32_t qm = agents_of(eballot(head && vi && st < 0));
-        int q = (vi && st < 0) ? __popc(qm & ((1u << i) - 1u)) : -1;
+        // worklist agents with a good action take its min at once (it collides with nothing:
+        // it never enters U and is never evicted, so its turn decides nothing -- step_group)
+        if (vi && st < 0 && good) asg_i = __builtin_ctz(good);
+        if (vj && st_j < 0 && good_j) asg_j = __builtin_ctz(good_j);
+        const uint32_t qm = agents_of(eballot(head && vi && st < 0 && !good));
+        int q = (vi && st < 0 && !good) ? __popc(qm & ((1u << i) - 1u)) : -1;
         int next_q = __popc(qm), hd = 0, draws = 0;
         const unsigned viable_i = ~(st_mask | hu_mask) & 0x1Fu;
         while (hd < next_q) {
