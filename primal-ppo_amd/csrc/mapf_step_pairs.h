@@ -182,6 +182,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     const uint64_t emask = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << base);
     auto eballot = [&](bool p) -> uint64_t { return (__ballot(p) & emask) >> base; };   // bit (k*NP + m)
     auto agents_of = [&](uint64_t m) -> uint32_t {   // stride-NP row-0 bits -> compact agent mask
+        if constexpr (NP == 8) {     // gather bit 8k -> k in three shift-or folds (not eight extracts)
+            m &= 0x0101010101010101ull;
+            m |= m >> 7;
+            m |= m >> 14;
+            m |= m >> 28;
+            return (uint32_t)m & 0xFFu;
+        }
         uint32_t a = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) a |= (uint32_t)((m >> (k * NP)) & 1ull) << k;
@@ -297,14 +304,13 @@ __device__ __forceinline__ void step_pairs_env(const DevEnv &e, int32_t *__restr
     }
     const int st = ((T >> i) & 1u) ? -3 : s0;
 
-    float rw;
-    switch (st) {
-        case -1: rw = e.collision_cost; break;
-        case -2: rw = e.human_collision_cost; break;
-        case -3: rw = e.collision_cost; break;
-        case -4: rw = e.repeat_cost; break;
-        default: rw = e.action_cost; break;
-    }
+    // selects, not a switch (each case's branch reloaded spilled scalars: step_group)
+    float c_act = e.action_cost, c_rep = e.repeat_cost, c_col = e.collision_cost, c_hum = e.human_collision_cost;
+    asm volatile("" : "+s"(c_act), "+s"(c_rep), "+s"(c_col), "+s"(c_hum));
+    float rw = c_act;
+    rw = st == -4 ? c_rep : rw;
+    rw = (st == -1 || st == -3) ? c_col : rw;
+    rw = st == -2 ? c_hum : rw;
     const int Xr = ri + dr(a_i), Xc = ci + dc(a_i);
     const uint32_t shadow = agents_of(eballot(head && vi && st == 1 && Xr == prow(gi) && Xc == pcol(gi)));
     float cost = 0.f;
