@@ -74,9 +74,12 @@ __host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide
 // the overlapped pipeline's own areas: a second observation snapshot (spos | sgoal | shn |
 // shp | shpn) and the stepper's BFS image
 __host__ __device__ inline size_t wide_snap_bytes(const DevEnv &e) { return wide_a16((size_t)(2 * e.N + 2 + e.k_predict) * 4); }
+// overlapped form: a ring of WIDE_SNAPS snapshots behind two LDS counters (16 B), so the
+// stepper may run up to WIDE_SNAPS - 1 steps ahead of the observer
+constexpr int WIDE_SNAPS = 4;
 template <class T, int RW>
 __host__ __device__ inline size_t wide_overlap_bytes(const DevEnv &e) {
-    return wide_snap_bytes(e) + srch::wave_lds<T, RW>(e.H, e.W);
+    return 16 + WIDE_SNAPS * wide_snap_bytes(e) + srch::wave_lds<T, RW>(e.H, e.W);
 }
 
 // nibble table (256 B) | map rows | cost table | [neighbour grid] | scratch | [snapshot 1 | BFS image]
@@ -114,6 +117,20 @@ __device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, int gmode, cha
     return L;
 }
 
+// the overlapped form's LDS counters: volatile ds_read / ds_write, wave-uniform
+__device__ inline uint32_t wide_counter(const uint32_t *c) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)*reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(const_cast<uint32_t *>(c))));
+}
+__device__ inline void wide_wait_ge(const uint32_t *c, uint32_t v) {
+    while (wide_counter(c) < v) __builtin_amdgcn_s_sleep(1);
+}
+// publish: every earlier LDS write of the wave lands before the counter moves
+__device__ inline void wide_publish(uint32_t *c, uint32_t v) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
+    if (lane_id() == 0) *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(c)) = v;
+}
+
 __device__ inline void wide_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -130,10 +147,13 @@ __device__ inline void wide_sync() {
 // releases its global stores before B; otherwise neither wave waits on memory at a
 // barrier, so the observer's stores and the stepper's outputs keep draining across them.
 // Overlapped (no BFS channel, so the observation reads no BFS map): the stepper searches in
-// its own BFS image and writes snapshot t into copy t & 1, so one barrier per step suffices,
-//     stepper  | human path t-1 | step t | BFS maps t | snapshot t | B | human path t | ...
-//     observer |        observe t-1                               | B | observe t    | ...
-// and a step costs max(stepper, observer) instead of their sum over the A..B segment.
+// its own BFS image and publishes snapshot t into ring slot t % WIDE_SNAPS through an LDS
+// counter; the observer waits for that counter, observes, and counts its observations, which
+// the stepper checks only before reusing a slot -- no barrier:
+//     stepper  | step t | BFS maps t | snapshot t, published | human path t | step t+1 ...
+//     observer | (t published?) | observe t, counted | (t+1 published?) | observe t+1 ...
+// so per step the slower wave's MEAN sets the pace, not the mean of the per-step maximum of
+// two noisy chains (a barrier per step made each wait for the other's slow steps).
 __device__ inline void wide_release_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
@@ -177,17 +197,27 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     uint8_t *grid;
     ObsLds L = wide_layout(e, smem, ro.grid, scratch, lcost, grid);
     const bool ovl = pipe && ro.overlap;
-    ObsLds L1 = L;                                     // snapshot copy 1 (overlapped form)
     char *bimg = scratch;                              // where the stepper's BFS maps search
+    uint32_t *ctr = nullptr;                           // overlapped: [0] snapshots published, [1] observed
+    uint32_t *snap0 = nullptr;                         //             the snapshot ring
     if (ovl) {
         char *x = scratch + wide_scratch_bytes<T, RW>(e);
-        L1.spos = reinterpret_cast<uint32_t *>(x);
-        L1.sgoal = L1.spos + e.N;
-        L1.shn = L1.sgoal + e.N;
-        L1.shp = L1.shn + 1;
-        L1.shpn = reinterpret_cast<int32_t *>(L1.shp + e.k_predict);
-        bimg = x + wide_snap_bytes(e);
+        ctr = reinterpret_cast<uint32_t *>(x);
+        snap0 = reinterpret_cast<uint32_t *>(x + 16);
+        bimg = x + 16 + WIDE_SNAPS * wide_snap_bytes(e);
+        if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
     }
+    auto snap_of = [&](int t) {                        // this step's snapshot
+        ObsLds S = L;
+        if (ovl) {
+            S.spos = snap0 + (size_t)(t & (WIDE_SNAPS - 1)) * (wide_snap_bytes(e) >> 2);
+            S.sgoal = S.spos + e.N;
+            S.shn = S.sgoal + e.N;
+            S.shp = S.shn + 1;
+            S.shpn = reinterpret_cast<int32_t *>(S.shp + e.k_predict);
+        }
+        return S;
+    };
     obs_lut_init(const_cast<float4 *>(L.lut));
     const uint32_t *mb = env_map(e, b);
     for (int k = (int)threadIdx.x; k < L.rowsz; k += (int)blockDim.x) L.mapc[k] = mb[k];
@@ -250,9 +280,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     // the stepping wave bounds the pipeline and shares its SIMD with another env's observing
     // wave, whose work waits on store issue anyway: it goes first when both are ready
     if (pipe && stepper && ro.prio) __builtin_amdgcn_s_setprio(3);
+    bool observing = true;                 // overlapped form: some wave consumes the snapshots
 #ifdef MAPF_STAMPS
     // phase-cost experiment (no observations written): the stepping role alone
-    if (ro.exp == 1) observer = false;
+    if (ro.exp == 1) observer = observing = false;
 #endif
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
@@ -263,9 +294,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         // A: observation t-1 done.  Nothing the observer reads from HBM was written by the step
         // (its outputs and state are not read back), so the stepper does not wait for them.
         if (pipe && !ovl) wide_plain_barrier();
-        const ObsLds &Lt = (ovl && (t & 1)) ? L1 : L;   // this step's snapshot
+        const ObsLds Lt = snap_of(t);
         if (stepper) {
             bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
+            // the slot's previous snapshot (step t - WIDE_SNAPS) has been observed
+            if (ovl && observing && t >= WIDE_SNAPS) wide_wait_ge(ctr + 1, (uint32_t)(t - WIDE_SNAPS + 1));
             // snapshot of step t for the observation, all from the registers: cells, goals,
             // the human's next cell and path cells [1..K] (HP channel)
             if (lane < e.N) { Lt.spos[lane] = rs.pp; Lt.sgoal[lane] = rs.gg; }
@@ -276,11 +309,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
                 const int len = rs.hcur ? rs.hl1 : rs.hl0;
                 Lt.shpn[0] = hp_ch ? max(0, min(e.k_predict, len - 1)) : 0;
             }
+            if (ovl) wide_publish(ctr, (uint32_t)(t + 1));
         }
         WSTAMP(1);
         // B: snapshot t in LDS; the stepper releases only when it rebuilt BFS maps (the
         // observation's BFS channel reads them from HBM)
-        if (pipe) { if (stepper && inl.bmask && !ovl) wide_release_barrier(); else wide_plain_barrier(); }
+        if (pipe && !ovl) { if (stepper && inl.bmask) wide_release_barrier(); else wide_plain_barrier(); }
         // the human's next path, into the other buffer (registers only: the observer may be
         // using the scratch by now)
         if (stepper && inl.replan) {
@@ -291,10 +325,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         WSTAMP(2);
         if (observer) {
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
+            if (ovl) wide_wait_ge(ctr, (uint32_t)(t + 1));   // snapshot t published
             wide_sync();
             const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
+            if (ovl) wide_publish(ctr + 1, (uint32_t)(t + 1));   // ... and observed
         }
         WSTAMP(3);
     }

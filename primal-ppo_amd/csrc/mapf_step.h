@@ -192,7 +192,9 @@ __device__ __attribute__((always_inline)) inline void step_group(const DevEnv &e
     const uint32_t hn_new = hpath2[(hs2 + 1 < hL2 ? hs2 + 1 : hL2 - 1) + vz];
     // and the observation's predicted cells human.path[1..K] (getObservations :293-297), in
     // the same round: read after the step's output stores they would wait for those stores
-    if constexpr (REGS) rg.hq = (i >= 1 && i <= e.k_predict && i < hL2) ? hpath2[i] : NO_CELL;
+    // (only with the HP channel: an unused load still holds its register, and the next step's
+    // reload of it would wait vmcnt behind every store issued meanwhile)
+    if constexpr (REGS) rg.hq = (e.use_hp && e.C >= 6 && i >= 1 && i <= e.k_predict && i < hL2) ? hpath2[i] : NO_CELL;
 
     // ---- state -----------------------------------------------------------
     const uint32_t pp = REGS ? rg.pp : (act ? e.pos[ai] : 0xFFFFFFFFu);
