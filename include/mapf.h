@@ -210,7 +210,12 @@ int mapf_rollout_random_fused(const mapf_env *env);
 
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the
  * humans' next paths) on its own; mapf_observe otherwise runs it inside the
- * observation launch.  Any later call that needs it flushes implicitly. */
+ * observation launch.  Any later call that needs it flushes implicitly.
+ * Also joins, on `stream`, the searches that wide maps (the split path) defer onto a
+ * second stream: call it on an uncaptured stream before beginning a hipGraph capture
+ * of a handle that stepped outside the capture -- a call inside the capture that would
+ * have to wait for such a search fails with MAPF_ESTATE instead (a graph cannot depend
+ * on work recorded before its capture began). */
 int mapf_flush(mapf_env *env, void *stream);
 
 /* Uniform random policy (Philox, counter = env clock): DEVICE int32 [B][N]. */

@@ -416,7 +416,18 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
                 asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dp), "v"(v4f{f.x, f.y, f.z, f.w}) : "memory");
 #endif
             } else {
+#if defined(MAPF_INPLACE_STORE) && MAPF_INPLACE_STORE == 1      // store-policy experiment: sc1
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dp), "v"(v4f{f.x, f.y, f.z, f.w}) : "memory");
+#elif defined(MAPF_INPLACE_STORE) && MAPF_INPLACE_STORE == 2    // store-policy experiment: nt sc1
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dp), "v"(v4f{f.x, f.y, f.z, f.w}) : "memory");
+#elif defined(MAPF_INPLACE_STORE) && MAPF_INPLACE_STORE == 3    // store-policy experiment: sc0 sc1
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dp), "v"(v4f{f.x, f.y, f.z, f.w}) : "memory");
+#else
                 *dp = f;
+#endif
             }
             swp += 8;
             dp += 64;
