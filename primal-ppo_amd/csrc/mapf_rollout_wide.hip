@@ -25,6 +25,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#define MAPF_WIDE_TU   // mapf_diag.h: no block-timeline stamps here (the WSTAMP rows use that region)
+
 #include "mapf_observe.h"
 #include "mapf_search.h"
 #include "mapf_step.h"
@@ -41,6 +43,11 @@ struct WideOut {
     int overlap;        // pipelined, no BFS channel: one barrier per step (wide_overlap_bytes)
     int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
     int prio;           // pipelined: the stepping wave's issue priority (s_setprio; MAPF_WIDE_PRIO, default 1: c4 -1.6 %)
+    int wpe;            // waves per env: 2 pipelined (stepper + observer), 1 one wave takes both roles
+    int epw;            // envs per workgroup (all the envs of one CU, wide_envs_per_group)
+    int pair;           // epw > 1: wave w is env w % epw's role w / epw (1), else env w / wpe's role w % wpe (0)
+    int slack;          // epw > 1: a pacing wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
+    int env_lds;        // epw > 1: LDS bytes per env (a multiple of 16); the pacing counters follow the envs
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -131,6 +138,21 @@ __device__ inline void wide_publish(uint32_t *c, uint32_t v) {
     if (lane_id() == 0) *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(c)) = v;
 }
 
+// pacing (envs per workgroup > 1): wait until every env of the group has counted v steps
+__device__ inline void wide_wait_min(const uint32_t *p, int n, uint32_t v) {
+    const int l = lane_id();
+    for (;;) {
+        uint32_t x = l < n ? *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(
+                                 as_lds(const_cast<uint32_t *>(p + l)))
+                           : 0xFFFFFFFFu;
+        x = min(x, (uint32_t)__shfl_xor((int)x, 1));
+        x = min(x, (uint32_t)__shfl_xor((int)x, 2));
+        x = min(x, (uint32_t)__shfl_xor((int)x, 4));
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) >= v) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 __device__ inline void wide_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -180,22 +202,31 @@ __device__ inline void wide_plain_barrier() {
 #endif
 
 template <class T, int RW, bool NT>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(WIDE_PARAMS) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(WIDE_PARAMS) {
     WIDE_BIND
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-aware env order (as the pair-lane rollout): workgroups are dealt round-robin
     // over the 8 XCDs, so each XCD owns one contiguous range of envs
     const int nb = (int)gridDim.x;
-    const int b = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
-                                                  : (int)blockIdx.x;
-    if (b >= e.B) return;
+    const int wg = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
+                                                   : (int)blockIdx.x;
+    // envs per workgroup: all the envs of one CU in one group (the host checks B % epw == 0),
+    // so a pacing wave sees how far the group's other envs are
+    const int EPW = ro.epw, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+    const int k = ro.pair ? wv % EPW : wv / ro.wpe;    // this wave's env in the group
+    const int role = ro.pair ? wv / EPW : wv % ro.wpe; // pipelined: 0 steps, 1 observes
+    const int b = wg * EPW + k;
+    if (wg * EPW >= e.B) return;
     const int lane = lane_id();
-    const bool pipe = blockDim.x == 128;
-    const int role = (int)(threadIdx.x >> 6);          // pipelined: 0 steps, 1 observes
+    const bool pipe = ro.wpe == 2;
+    const int lt = role * 64 + lane, nthr = ro.wpe * 64;   // thread index within the env's waves
+    char *esm = smem + (size_t)k * ro.env_lds;
+    uint32_t *prog = reinterpret_cast<uint32_t *>(smem + (size_t)EPW * ro.env_lds);   // [EPW] steps observed
+    const bool pacing = EPW > 1 && ro.slack >= 0;
     char *scratch;
     float *lcost;
     uint8_t *grid;
-    ObsLds L = wide_layout(e, smem, ro.grid, scratch, lcost, grid);
+    ObsLds L = wide_layout(e, esm, ro.grid, scratch, lcost, grid);
     const bool ovl = pipe && ro.overlap;
     char *bimg = scratch;                              // where the stepper's BFS maps search
     uint32_t *ctr = nullptr;                           // overlapped: [0] snapshots published, [1] observed
@@ -205,7 +236,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         ctr = reinterpret_cast<uint32_t *>(x);
         snap0 = reinterpret_cast<uint32_t *>(x + 16);
         bimg = x + 16 + WIDE_SNAPS * wide_snap_bytes(e);
-        if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+        if (lt < 2) ctr[lt] = 0u;
     }
     auto snap_of = [&](int t) {                        // this step's snapshot
         ObsLds S = L;
@@ -218,11 +249,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         }
         return S;
     };
-    obs_lut_init(const_cast<float4 *>(L.lut));
+    if (lt < 16)
+        const_cast<float4 *>(L.lut)[lt] = make_float4((float)(lt & 1), (float)((lt >> 1) & 1), (float)((lt >> 2) & 1), (float)(lt >> 3));
+    if (EPW > 1 && (int)threadIdx.x < EPW) prog[threadIdx.x] = 0u;
     const uint32_t *mb = env_map(e, b);
-    for (int k = (int)threadIdx.x; k < L.rowsz; k += (int)blockDim.x) L.mapc[k] = mb[k];
+    for (int q = lt; q < L.rowsz; q += nthr) L.mapc[q] = mb[q];
     if (lcost)
-        for (int k = (int)threadIdx.x; k <= e.R * e.R; k += (int)blockDim.x) lcost[k] = e.cost_lut[k];
+        for (int q = lt; q <= e.R * e.R; q += nthr) lcost[q] = e.cost_lut[q];
     __syncthreads();
     StepRegs rs;                           // the stepping wave keeps the env's state in registers
     step_regs_load(e, b, lane, rs);
@@ -288,6 +321,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
+        if (pacing && !pipe && t > ro.slack) wide_wait_min(prog, EPW, (uint32_t)(t - ro.slack));
         StepInline inl;
         if (stepper) step_group<WaveGroup, true, true>(e, lact + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs, have);
         WSTAMP(0);
@@ -326,16 +360,30 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
         if (observer) {
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
             if (ovl) wide_wait_ge(ctr, (uint32_t)(t + 1));   // snapshot t published
+            if (pacing && pipe && t > ro.slack) wide_wait_min(prog, EPW, (uint32_t)(t - ro.slack));
             wide_sync();
             const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
             if (ovl) wide_publish(ctr + 1, (uint32_t)(t + 1));   // ... and observed
+            if (EPW > 1) wide_publish(prog + k, (uint32_t)(t + 1));
         }
         WSTAMP(3);
     }
     if (stepper) step_regs_store(e, b, lane, rs);
-    WSTAMP_END(b);
+    WSTAMP_END(b, role);
+}
+
+// the device's LDS limit per workgroup (160 KiB on gfx950), read once
+static int wide_max_group_lds() {
+    static const int v = [] {
+        int dev = 0, x = 64 * 1024;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+            x = 64 * 1024;
+        return x;
+    }();
+    return v;
 }
 
 template <class T, int RW>
@@ -373,13 +421,36 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     if (const char *v = std::getenv("MAPF_WIDE_EXP")) r.exp = std::atoi(v);
 #endif
     size_t lds = wide_lds_bytes<T, RW>(e, r.grid, r.overlap);
-    if (cap > lds && cap <= 64 * 1024) lds = cap;
+    r.wpe = pipe ? 2 : 1;
+    // one wave per env (c5): all the envs of a CU in one workgroup (<= 8 waves:
+    // launch_bounds(512) keeps the 256-VGPR budget), each env's LDS at its own offset, then
+    // the pacing counters; every wave runs at most `slack` steps ahead of its group's
+    // slowest env.  Unpaced, the younger wave of every SIMD (the CU's last-dispatched four
+    // envs) ran 8 % slower than the older one through the whole launch and the launch
+    // waited for it (tools/stamps_wide.py, "by dispatch rank in CU"): c5 85.5-85.9 -> 79.8
+    // us per step, slack 1 (2: 80.0-80.7, 4: 80.9-81.3, 8: 82.4-83.1, groups unpaced 86.8).
+    // The pipelined form (c4) measured no gain from groups (its CUs share out the same
+    // throughput either way: balanced envs all ran at the slow env's pace) and 4-6 % slower,
+    // so it keeps one env per workgroup.  MAPF_WIDE_EPW overrides; the per-step barriers of
+    // the non-overlapped pipeline would couple the envs, so never there.
+    r.env_lds = (int)wide_a16(lds);
+    r.epw = 1;
+    int epw = pipe ? 1 : occ;
+    if (const char *v = std::getenv("MAPF_WIDE_EPW")) epw = std::atoi(v);
+    if (epw > 1 && e.B % epw == 0 && epw * r.wpe <= 8 && (!pipe || r.overlap) &&
+        (size_t)epw * r.env_lds + 32 <= (size_t)wide_max_group_lds())
+        r.epw = epw;
+    r.pair = env_flag("MAPF_WIDE_PAIR", 0);
+    r.slack = env_flag("MAPF_WIDE_SLACK", 1);
+    if (r.epw > 1) lds = (size_t)wide_max_group_lds();   // the whole CU: one group per CU
+    else if (cap > lds && cap <= 64 * 1024) lds = cap;
+    const dim3 grid_dim(e.B / r.epw), block_dim(64 * r.wpe * r.epw);
 #if MAPF_ARGS_PTR
     const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
-    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, args, steps);
+    hipLaunchKernelGGL(kern, grid_dim, block_dim, lds, s, args, steps);
 #else
     (void)ring;
-    hipLaunchKernelGGL(kern, dim3(e.B), dim3(pipe ? 128 : 64), lds, s, e, steps, r);
+    hipLaunchKernelGGL(kern, grid_dim, block_dim, lds, s, e, steps, r);
 #endif
 }
 
@@ -401,7 +472,7 @@ bool rollout_wide_fusable(const DevEnv &e) {
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, ArgRing &ring, hipStream_t s) {
     const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
-                     env_flag("MAPF_WIDE_PRIO", 1)};
+                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0};
     with_row_type(e, [&](auto t, auto rw) {
         launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
         return 0;

@@ -350,6 +350,22 @@ def test_rollout_wide_one_wave_form_matches_oracle(name, grid, monkeypatch):
     run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
 
 
+@pytest.mark.parametrize("name,pipe,epw,pair,slack", [
+    ("c4_40x40_n16_f9_looping", 1, 4, 0, 4), ("c4_40x40_n16_f9_looping", 1, 4, 1, 0),
+    ("dense_12x12_n16_f9_dahp", 1, 2, 0, -1), ("dense_12x12_n16_f9_dahp", 0, 8, 0, 4),
+    ("c5_80x80_n64_f11_bfsch", 0, 3, 0, 1)])
+def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack, monkeypatch):
+    """Several envs per workgroup (all the envs of a CU at full size), each at its own LDS
+    offset, their pacing waves kept within `slack` steps of the group's slowest env: the
+    same trajectories and observations as the oracle, in both wave-to-env orders."""
+    monkeypatch.setenv("MAPF_WIDE_PIPE", str(pipe))
+    monkeypatch.setenv("MAPF_WIDE_EPW", str(epw))
+    monkeypatch.setenv("MAPF_WIDE_PAIR", str(pair))
+    monkeypatch.setenv("MAPF_WIDE_SLACK", str(slack))
+    case = FUSED_CASES.get(name) or RANDOM_CASES[name]
+    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
+
+
 def run_random_case(name, case, path, expect_rollout_kernel=None):
     B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
     rng = np.random.default_rng(5)

@@ -61,3 +61,85 @@ if len(rows):
     for k, nm in enumerate(PHASES):
         print(f"  {nm:24s} {rows[:, k].mean():9.0f} {np.percentile(rows[:, k], 90):9.0f}")
     print(f"  {'total':24s} {rows.sum(1).mean():9.0f}")
+
+# where the slow envs are: each wave's start / end on the realtime counter and its CU
+# (slot 6 = HW_ID | XCC_ID << 32), grouped by XCD and by CU
+raw = env.timeline(min(2 * B, 8192))
+rows_all = [("first wave", np.arange(B))]
+if (raw[B:2 * B, 7] == 1).any():
+    rows_all.append(("observing wave", np.arange(B, 2 * B)))
+t0 = raw[:2 * B][raw[:2 * B, 7] == 1, 4].min()
+for who, idx in rows_all:
+    r = raw[idx]
+    ok = r[:, 7] == 1
+    r, idx = r[ok], idx[ok]
+    st = (r[:, 4] - t0) / 100.0
+    en = (r[:, 5] - t0) / 100.0
+    hw = r[:, 6].astype(np.uint64)
+    xcc = (hw >> np.uint64(32)).astype(np.int64)
+    h = (hw & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    simd = (h >> 4) & 3
+    cu = (h >> 8) & 15
+    sh = (h >> 12) & 1
+    se = (h >> 13) & 7
+    cukey = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    tot = (r[:, :4].sum(1)) / 100.0 / T
+    print(f" {who}: start us mean {st.mean():.2f} max {st.max():.2f}; end us mean {en.mean():.1f} "
+          f"p50 {np.percentile(en, 50):.1f} p99 {np.percentile(en, 99):.1f} max {en.max():.1f}")
+    xs = sorted(set(xcc.tolist()))
+    print("  per XCD: " + "  ".join(f"{x}:{tot[xcc == x].mean():.2f}/{tot[xcc == x].max():.2f}" for x in xs))
+    # the realtime counters of different XCDs are not aligned: wall per XCD from its own first start
+    print("  per XCD wall us/step: " + "  ".join(
+        f"{x}:{(r[xcc == x, 5].max() - r[xcc == x, 4].min()) / 100.0 / T:.2f}" for x in xs))
+    print("  per SIMD: " + "  ".join(f"{k}:{tot[simd == k].mean():.2f}" for k in range(4) if (simd == k).any()))
+    u, inv, cnt = np.unique(cukey, return_inverse=True, return_counts=True)
+    cu_mean = np.bincount(inv, tot) / cnt
+    print(f"  {len(u)} CUs, waves per CU {np.bincount(cnt).nonzero()[0].tolist()}; per-CU mean total "
+          f"min {cu_mean.min():.2f} p50 {np.median(cu_mean):.2f} max {cu_mean.max():.2f}; "
+          f"within-CU spread mean {np.mean([tot[inv == k].max() - tot[inv == k].min() for k in range(len(u))]):.2f}")
+    wslot = h & 15
+    print("  per wave slot: " + "  ".join(f"{k}:{tot[wslot == k].mean():.2f}({(wslot == k).sum()})"
+                                          for k in range(16) if (wslot == k).any()))
+    # dispatch order within the CU (workgroup id; with the XCD remap env b runs as
+    # workgroup (b % (B/8)) * 8 + b // (B/8))
+    bb = idx % B
+    wg = (bb % (B // 8)) * 8 + bb // (B // 8) if B % 8 == 0 else bb
+    rank = np.zeros(len(tot), np.int64)
+    for k in range(len(u)):
+        m = np.nonzero(inv == k)[0]
+        rank[m[np.argsort(wg[m])]] = np.arange(len(m))
+    print("  by dispatch rank in CU: " + "  ".join(f"{k}:{tot[rank == k].mean():.2f}" for k in range(rank.max() + 1)))
+    print("  XCD x wave slot: " + "  ".join(
+        f"{x}/{k}:{tot[(xcc == x) & (wslot == k)].mean():.2f}({((xcc == x) & (wslot == k)).sum()})"
+        for x in xs for k in range(4) if ((xcc == x) & (wslot == k)).any()))
+    print("  XCD x rank: " + "  ".join(
+        f"{x}/{k}:{tot[(xcc == x) & (rank == k)].mean():.2f}" for x in xs for k in range(rank.max() + 1)))
+    slow = np.argsort(tot)[-8:]
+    print("  slowest: " + "  ".join(f"b{idx[k] % B}:{tot[k]:.2f}(x{xcc[k]} cu{cukey[k] % 256} s{simd[k]})" for k in slow))
+
+# SIMD sharing: which roles share each SIMD (two waves per SIMD), and each role's mean total by
+# the role of the other wave on its SIMD and by its own wave slot
+if len(rows_all) == 2:
+    recs = []
+    for role, (who, idx) in enumerate(rows_all):
+        r = raw[idx]
+        ok = r[:, 7] == 1
+        r = r[ok]
+        hw = r[:, 6].astype(np.uint64)
+        xcc = (hw >> np.uint64(32)).astype(np.int64)
+        h = (hw & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        key = ((((xcc * 8 + ((h >> 13) & 7)) * 2 + ((h >> 12) & 1)) * 16 + ((h >> 8) & 15)) * 4 + ((h >> 4) & 3))
+        tot = r[:, :4].sum(1) / 100.0 / T
+        for q in range(len(r)):
+            recs.append((int(key[q]), role, int(h[q] & 15), float(tot[q])))
+    by = {}
+    for k_, role, slot, tt in recs:
+        by.setdefault(k_, []).append((role, slot, tt))
+    comp = {}
+    for k_, lst in by.items():
+        for i, (role, slot, tt) in enumerate(lst):
+            others = "".join(sorted("SO"[o[0]] for j, o in enumerate(lst) if j != i))
+            comp.setdefault(("SO"[role], others, slot), []).append(tt)
+    print(" SIMD sharing (own role | other roles on the SIMD | own slot): mean total, count")
+    for kk in sorted(comp):
+        print(f"  {kk[0]} | {kk[1] or '-':3s} | slot {kk[2]}: {np.mean(comp[kk]):.2f} ({len(comp[kk])})")
