@@ -61,7 +61,19 @@ __device__ inline uint64_t stamp_rt() {   // constant-rate 100 MHz counter
     for (int _k = 0; _k < 6; ++_k) e.prof[PROF_TL + _row * 8 + _k] = _w_d[_k]; \
     e.prof[PROF_TL + _row * 8 + 6] = (uint64_t)_h | ((uint64_t)_x << 32); \
     e.prof[PROF_TL + _row * 8 + 7] = 1; } } while (0)
+// pair-lane rollout kernel: each env wave's start / end (realtime) and HW_ID | XCC_ID << 32 in
+// prof[(RSTAMP_ROW0 + b) * 8 + 4..6], slot 7 = 1 (rows above the step kernels' per-wave rows)
+constexpr size_t RSTAMP_ROW0 = 32768;
+#define RSTAMP_BEGIN() const uint64_t _r_start = stamp_rt()
+#define RSTAMP_END(b) do { if ((threadIdx.x & 63) == 0 && (size_t)(b) < RSTAMP_ROW0) { \
+    uint32_t _h, _x; const uint64_t _r_end = stamp_rt(); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_h)); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_x)); \
+    unsigned long long *_p = e.prof + (RSTAMP_ROW0 + (size_t)(b)) * 8; \
+    _p[4] = _r_start; _p[5] = _r_end; _p[6] = (uint64_t)_h | ((uint64_t)_x << 32); _p[7] = 1; } } while (0)
 #else
+#define RSTAMP_BEGIN() do { } while (0)
+#define RSTAMP_END(b) do { } while (0)
 #define WSTAMP_BEGIN() do { } while (0)
 #define WSTAMP(k) do { } while (0)
 #define WSTAMP_END(b, r) do { } while (0)

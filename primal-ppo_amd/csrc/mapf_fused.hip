@@ -141,6 +141,8 @@ struct RolloutOut {
     float *obs, *vec;
     int slots;
     int xcd_remap;
+    int sub_lds;        // SUBS > 1: LDS bytes of one 4-env quarter (the pacing counters follow the quarters)
+    int slack;          // SUBS > 1: a wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
 };
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
 struct RolloutArgs {
@@ -162,8 +164,10 @@ __host__ __device__ inline size_t rollout_lds_bytes(const DevEnv &e) {
 // NT: nontemporal observation stores -- for slot buffers (fresh HBM lines every step,
 // measured faster); re-written [B]-leading buffers keep plain stores (their lines
 // stay cache-resident between steps, measured faster).
-template <bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(
+// SUBS 4-env quarters per workgroup: SUBS = 4 puts all 16 waves of a CU in one workgroup, so
+// each can see how far the others are (pacing, below)
+template <bool NT, int SUBS>
+__global__ __launch_bounds__(256 * SUBS) __attribute__((amdgpu_waves_per_eu(4))) void rollout_random_kernel(
 #if MAPF_ARGS_PTR      // experiment build: arguments through a device pointer (mapf_rollout_wide.hip)
     const RolloutArgs *__restrict__ args, int T) {
     const DevEnv &e = args->e;
@@ -178,19 +182,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     // envs, and the output lines that several envs share (status: 16 envs per 128-B line)
     // are completed in one XCD's L2 instead of leaving it as partial lines from several.
     const int nb = (int)gridDim.x;
-    const int blk = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
-                                                    : (int)blockIdx.x;
+    const int wg = (ro.xcd_remap && (nb & 7) == 0) ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3)
+                                                   : (int)blockIdx.x;
+    const int sub = SUBS > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;   // this wave's quarter
+    const int qt = (int)(threadIdx.x & 255);           // thread index within the quarter
+    const int blk = wg * SUBS + sub;                   // the quarter's 4-env block
     const int b0 = blk * E;
     const int nenv = min(E, e.B - b0);
-    const int le = (int)(threadIdx.x >> 6);
-    ObsLds L = obs_layout(e, E, smem, true);
-    float4 *lut = reinterpret_cast<float4 *>(smem + rollout_obs_lds(e) - 256);
-    obs_lut_init(lut);
+    const int le = qt >> 6;
+    char *qsm = smem + (SUBS > 1 ? (size_t)sub * ro.sub_lds : 0);
+    uint32_t *prog = reinterpret_cast<uint32_t *>(smem + (size_t)SUBS * ro.sub_lds);   // [4 * SUBS] steps done
+    const int gw = sub * E + le;                       // the wave's index in the workgroup
+    ObsLds L = obs_layout(e, E, qsm, true);
+    float4 *lut = reinterpret_cast<float4 *>(qsm + rollout_obs_lds(e) - 256);
+    if (qt < 16) lut[qt] = make_float4((float)(qt & 1), (float)((qt >> 1) & 1), (float)((qt >> 2) & 1), (float)(qt >> 3));
+    // envs past B never count: they start at the top
+    if (SUBS > 1 && (int)threadIdx.x < 4 * SUBS) prog[threadIdx.x] = wg * SUBS * E + (int)threadIdx.x < e.B ? 0u : 0xFFFFFFFFu;
     __syncthreads();
     L.lut = lut;
     const size_t swl = srch::wave_lds<uint32_t, 1>(e.H, e.W);
-    char *slds = smem + rollout_obs_lds(e) + (size_t)le * swl;
-    uint32_t *lpath = reinterpret_cast<uint32_t *>(smem + rollout_obs_lds(e) + 4 * swl) + (size_t)le * e.Lmax;
+    char *slds = qsm + rollout_obs_lds(e) + (size_t)le * swl;
+    uint32_t *lpath = reinterpret_cast<uint32_t *>(qsm + rollout_obs_lds(e) + 4 * swl) + (size_t)le * e.Lmax;
     const uint32_t mreg = obs_map_word(e, b0, nenv, (int)(threadIdx.x & 63));
     EnvRegs rs{};
     if (le < nenv) env_regs_load<8>(e, b0 + le, rs, lpath);
@@ -198,9 +210,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     // register's load "pending" at the loop header and waits vmcnt(0) -- i.e. behind
     // all of the previous step's stores -- where the loop uses it
     __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt/lgkmcnt untouched
+    RSTAMP_BEGIN();
+    const bool pacing = SUBS > 1 && ro.slack >= 0 && le < nenv;
     for (int t = 0; t < T; ++t) {
         const DevEnv &E = e;
         const RolloutOut &R = ro;
+        if (pacing && t > R.slack) wait_group_min(prog, 4 * SUBS, (uint32_t)(t - R.slack));
         const size_t BN = (size_t)E.B * E.N;
         const size_t s = R.slots ? (size_t)t : 0;
         StepOut o = R.out;
@@ -214,17 +229,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
         if (o.constraints) o.constraints += s * BN;
         if (o.reward_total) o.reward_total += s * BN;
         PairsDeferred dfr;
-        step_pairs_env<8, true, true, true>(E, R.actions + s * BN, o, 3u, 0, blk * 256 + (int)threadIdx.x,
+        step_pairs_env<8, true, true, true>(E, R.actions + s * BN, o, 3u, 0, blk * 256 + qt,
                                             L, b0, RegMap{mreg, true}, dfr, &rs);
         if (le < nenv) {
             const ObsGroup g = obs_wave_init(E, L, le, mreg);
             obs_emit<false, NT>(E, L, R.obs + s * BN * E.C * E.F * E.F, R.vec + s * BN * 4, g, b0, false);
             step_pairs_search_inline(E, dfr, slds, L.mapc + (size_t)le * L.rowsz, rs);
+            if (pacing) publish_count(prog + gw, (uint32_t)(t + 1));
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     if (le < nenv) env_regs_store<8>(e, b0 + le, rs);
+    if (le < nenv) RSTAMP_END(b0 + le);
 }
 
 bool rollout_random_fusable(const DevEnv &e) { return rollout_fusable(e) && rollout_lds_bytes(e) <= 64 * 1024; }
@@ -242,21 +259,39 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     size_t lds = rollout_lds_bytes(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
+    // Slot buffers at four workgroups per CU (c2): one workgroup of all 16 waves instead,
+    // each wave paced within `slack` steps of the slowest (RolloutOut::slack).  Unpaced,
+    // each SIMD's four waves ran at 12.3 / 14.4 / 16.3 / 18.3 us per step by wave slot
+    // (issue goes to the oldest) and the launch waited for the youngest; paced, all run
+    // at 16.9 and the launch takes 17.5-17.7 us per step instead of 20.3
+    // (tools/stamps_pairs.py, tools/ab_env.sh).  The in-place buffer stays in the
+    // Infinity Cache and its CUs share out the same throughput either way: paced 14.5-14.7
+    // against 13.8-13.9 (every wave then runs at the pace the youngest ran), grouped but
+    // unpaced 13.8-13.9 -- so it keeps four workgroups.  MAPF_ROLL_GROUP=0/1 overrides.
+    const size_t sub = (rollout_lds_bytes(e) + 15) & ~(size_t)15;
+    const int gsel = env_flag("MAPF_ROLL_GROUP", -1);
+    const bool group = occ == 4 && grid % 4 == 0 && 4 * sub + 64 <= (size_t)device_max_group_lds() &&
+                       (gsel < 0 ? slots != 0 : gsel != 0);
     const int remap = env_flag("MAPF_XCD_REMAP", 1) != 0;
+    const RolloutOut ro{actions, out, obs, vec, slots, remap, (int)sub, env_flag("MAPF_ROLL_SLACK", 1)};
+    auto launch = [&](auto kern, int subs) {
+        const dim3 gd(grid / subs), bd(256 * subs);
+        const size_t l = subs > 1 ? (size_t)device_max_group_lds() : lds;   // subs > 1: the whole CU
 #if MAPF_ARGS_PTR
-    const RolloutArgs *args = push_args(ring, RolloutArgs{e, RolloutOut{actions, out, obs, vec, slots, remap}}, s);
-    if (slots)
-        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, args, T);
-    else
-        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, args, T);
+        const RolloutArgs *args = push_args(ring, RolloutArgs{e, ro}, s);
+        hipLaunchKernelGGL(kern, gd, bd, l, s, args, T);
 #else
-    (void)ring;
-    const RolloutOut ro{actions, out, obs, vec, slots, remap};
-    if (slots)
-        hipLaunchKernelGGL(rollout_random_kernel<true>, dim3(grid), dim3(256), lds, s, e, T, ro);
-    else
-        hipLaunchKernelGGL(rollout_random_kernel<false>, dim3(grid), dim3(256), lds, s, e, T, ro);
+        hipLaunchKernelGGL(kern, gd, bd, l, s, e, T, ro);
 #endif
+    };
+    (void)ring;
+    if (group) {
+        if (slots) launch(rollout_random_kernel<true, 4>, 4);
+        else launch(rollout_random_kernel<false, 4>, 4);
+    } else {
+        if (slots) launch(rollout_random_kernel<true, 1>, 1);
+        else launch(rollout_random_kernel<false, 1>, 1);
+    }
     return true;
 }
 

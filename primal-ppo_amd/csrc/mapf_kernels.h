@@ -22,6 +22,18 @@ inline int device_cu_count() {
     return v;
 }
 
+// LDS bytes one workgroup may request (160 KiB on gfx950)
+inline int device_max_group_lds() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 64 * 1024;
+    int v = dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0;
+    if (v > 0) return v;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0) v = 64 * 1024;
+    if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+    return v;
+}
+
 // VGPRs per lane of a kernel (one code object per arch: the same on every device here)
 inline int kernel_vgprs(const void *fn) {
     static std::mutex m;

@@ -124,33 +124,9 @@ __device__ inline ObsLds wide_layout(const DevEnv &e, char *smem, int gmode, cha
     return L;
 }
 
-// the overlapped form's LDS counters: volatile ds_read / ds_write, wave-uniform
-__device__ inline uint32_t wide_counter(const uint32_t *c) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)*reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(const_cast<uint32_t *>(c))));
-}
+// the overlapped form's LDS counters (mapf_group.h: lds_count, publish_count)
 __device__ inline void wide_wait_ge(const uint32_t *c, uint32_t v) {
-    while (wide_counter(c) < v) __builtin_amdgcn_s_sleep(1);
-}
-// publish: every earlier LDS write of the wave lands before the counter moves
-__device__ inline void wide_publish(uint32_t *c, uint32_t v) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
-    if (lane_id() == 0) *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(c)) = v;
-}
-
-// pacing (envs per workgroup > 1): wait until every env of the group has counted v steps
-__device__ inline void wide_wait_min(const uint32_t *p, int n, uint32_t v) {
-    const int l = lane_id();
-    for (;;) {
-        uint32_t x = l < n ? *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(
-                                 as_lds(const_cast<uint32_t *>(p + l)))
-                           : 0xFFFFFFFFu;
-        x = min(x, (uint32_t)__shfl_xor((int)x, 1));
-        x = min(x, (uint32_t)__shfl_xor((int)x, 2));
-        x = min(x, (uint32_t)__shfl_xor((int)x, 4));
-        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) >= v) return;
-        __builtin_amdgcn_s_sleep(1);
-    }
+    while (lds_count(c) < v) __builtin_amdgcn_s_sleep(1);
 }
 
 __device__ inline void wide_sync() {
@@ -321,7 +297,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
-        if (pacing && !pipe && t > ro.slack) wide_wait_min(prog, EPW, (uint32_t)(t - ro.slack));
+        if (pacing && !pipe && t > ro.slack) wait_group_min(prog, EPW, (uint32_t)(t - ro.slack));
         StepInline inl;
         if (stepper) step_group<WaveGroup, true, true>(e, lact + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs, have);
         WSTAMP(0);
@@ -343,7 +319,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
                 const int len = rs.hcur ? rs.hl1 : rs.hl0;
                 Lt.shpn[0] = hp_ch ? max(0, min(e.k_predict, len - 1)) : 0;
             }
-            if (ovl) wide_publish(ctr, (uint32_t)(t + 1));
+            if (ovl) publish_count(ctr, (uint32_t)(t + 1));
         }
         WSTAMP(1);
         // B: snapshot t in LDS; the stepper releases only when it rebuilt BFS maps (the
@@ -360,30 +336,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
         if (observer) {
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
             if (ovl) wide_wait_ge(ctr, (uint32_t)(t + 1));   // snapshot t published
-            if (pacing && pipe && t > ro.slack) wide_wait_min(prog, EPW, (uint32_t)(t - ro.slack));
+            if (pacing && pipe && t > ro.slack) wait_group_min(prog, EPW, (uint32_t)(t - ro.slack));
             wide_sync();
             const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
-            if (ovl) wide_publish(ctr + 1, (uint32_t)(t + 1));   // ... and observed
-            if (EPW > 1) wide_publish(prog + k, (uint32_t)(t + 1));
+            if (ovl) publish_count(ctr + 1, (uint32_t)(t + 1));   // ... and observed
+            if (EPW > 1) publish_count(prog + k, (uint32_t)(t + 1));
         }
         WSTAMP(3);
     }
     if (stepper) step_regs_store(e, b, lane, rs);
     WSTAMP_END(b, role);
-}
-
-// the device's LDS limit per workgroup (160 KiB on gfx950), read once
-static int wide_max_group_lds() {
-    static const int v = [] {
-        int dev = 0, x = 64 * 1024;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
-            x = 64 * 1024;
-        return x;
-    }();
-    return v;
 }
 
 template <class T, int RW>
@@ -438,11 +402,11 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     int epw = pipe ? 1 : occ;
     if (const char *v = std::getenv("MAPF_WIDE_EPW")) epw = std::atoi(v);
     if (epw > 1 && e.B % epw == 0 && epw * r.wpe <= 8 && (!pipe || r.overlap) &&
-        (size_t)epw * r.env_lds + 32 <= (size_t)wide_max_group_lds())
+        (size_t)epw * r.env_lds + 32 <= (size_t)device_max_group_lds())
         r.epw = epw;
     r.pair = env_flag("MAPF_WIDE_PAIR", 0);
     r.slack = env_flag("MAPF_WIDE_SLACK", 1);
-    if (r.epw > 1) lds = (size_t)wide_max_group_lds();   // the whole CU: one group per CU
+    if (r.epw > 1) lds = (size_t)device_max_group_lds();   // the whole CU: one group per CU
     else if (cap > lds && cap <= 64 * 1024) lds = cap;
     const dim3 grid_dim(e.B / r.epw), block_dim(64 * r.wpe * r.epw);
 #if MAPF_ARGS_PTR

@@ -276,6 +276,24 @@ def test_rollout_random_matches_oracle(name):
     run_random_case(name, case, "rollout", expect_rollout_kernel=kind)
 
 
+GROUP_CASES = {
+    "g_n8_20x20_f11": dict(B=64, H=20, W=20, n=8, fov=11, nch=6, steps=60, map="wh"),
+    "g_n6_16x16_f9_dahp_ragged": dict(B=45, H=16, W=16, n=6, fov=9, nch=6, steps=60, map="wh", da=1, hp=1),
+}
+
+
+@pytest.mark.parametrize("name,slack", [("g_n8_20x20_f11", 1), ("g_n8_20x20_f11", 0), ("g_n8_20x20_f11", -1),
+                                        ("g_n6_16x16_f9_dahp_ragged", 1), ("g_n6_16x16_f9_dahp_ragged", 3)])
+def test_rollout_random_cu_groups_match_oracle(name, slack, monkeypatch):
+    """The pair-lane rollout with all 16 waves of a CU in one workgroup (four 4-env quarters
+    at their own LDS offsets, the waves paced within `slack` steps of the group's slowest;
+    ragged B: the envs past B never count) -- every slot bit-exact vs the oracle."""
+    monkeypatch.setenv("MAPF_ROLL_OCC", "4")
+    monkeypatch.setenv("MAPF_ROLL_GROUP", "1")
+    monkeypatch.setenv("MAPF_ROLL_SLACK", str(slack))
+    run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1)
+
+
 # the one-wave-per-env kernel's other search row layouts (u32 rows on two lane slots, u64 on
 # two, 128-bit rows on one) and the BFS channel on a non-square map
 WIDE_SHAPES = {
