@@ -208,6 +208,9 @@ struct ObsGroup {
     uint32_t *stream;            // bit 0 = float 0 of env le0's observation
     const uint32_t *mapc;        // map rows: the shared map, or per-env maps at (le - le0) * rowsz
     bool wave;
+#ifdef MAPF_STAMPS
+    int diag = 0;                // stamps-build experiments: 2 no float stores, 3 stores only (no bit-stream)
+#endif
 };
 
 __device__ inline void obs_sync(const ObsGroup &g) {
@@ -252,7 +255,12 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
 
     // ---- phase 1: worldWithAgents as a padded bitmap per env + agent index grid ----
     const int HW = e.H * e.W;
-    for (int k = tid; k < K; k += nt) {
+#ifdef MAPF_STAMPS
+    const int KB = G.diag == 3 ? 0 : K;       // agents whose bits phases 1-3 build
+#else
+    const int KB = K;
+#endif
+    for (int k = tid; k < KB; k += nt) {
         const int le = G.le0 + k / N;
         const int r = prow(L.spos[kw + k]), c = pcol(L.spos[kw + k]);
         const int rr = r + e.P, cc = c + e.P;
@@ -265,7 +273,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         // the BFS channel's bfsMap windows: every load of the workgroup issued here
         // at once (one HBM latency, not one per FOV-row task), as aligned dwords
         const int WD = obs_bfs_wd(e);
-        for (int idx = tid; idx < K * F * WD; idx += nt) {
+        for (int idx = tid; idx < KB * F * WD; idx += nt) {
             const int task = idx / WD, w = idx - task * WD;
             const int k = task / F, y = task - k * F;
             const int rr = min(max(prow(L.spos[kw + k]) - half + y, 0), e.H - 1);
@@ -273,14 +281,14 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
             const int16_t *bm = e.bfs + ((size_t)b0 * N + k) * bcells;
             L.bfsw[kw * F * WD + idx] = *reinterpret_cast<const uint32_t *>(bm + bfs_at(e.W, rr, col));   // col even
         }
-        for (int k = tid; k < K; k += nt)
+        for (int k = tid; k < KB; k += nt)
             L.bfsown[kw + k] = e.bfs[((size_t)b0 * N + k) * bcells + bfs_at(e.W, prow(L.spos[kw + k]), pcol(L.spos[kw + k]))];
     }
     obs_sync(G);
 
     // ---- phase 2: (agent, FOV row) ----
     const int R2 = e.R * e.R;
-    for (int task = tid; task < K * F; task += nt) {
+    for (int task = tid; task < KB * F; task += nt) {
         const int k = task / F, y = task - k * F;
         const int le = G.le0 + k / N;
         const int pr = prow(L.spos[kw + k]), pc = pcol(L.spos[kw + k]);
@@ -355,7 +363,7 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     }
 
     // ---- phase 3: per agent: own goal (ch2), human next position (ch4), HP cells (ch5), vector ----
-    for (int k = tid; k < K; k += nt) {
+    for (int k = tid; k < KB; k += nt) {
         const int le = G.le0 + k / N;
         const int pr = prow(L.spos[kw + k]), pc = pcol(L.spos[kw + k]);
         const int tr = pr - half, tc = pc - half;
@@ -385,6 +393,9 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     }
     obs_sync(G);
     TL_STAMP(4);
+#ifdef MAPF_STAMPS
+    if (G.diag == 2) return;
+#endif
 
     // ---- phase 4: bit-stream -> float stores ----
     const size_t total = (size_t)K * CFF;

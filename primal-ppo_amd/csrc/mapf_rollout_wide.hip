@@ -338,7 +338,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
             if (ovl) wide_wait_ge(ctr, (uint32_t)(t + 1));   // snapshot t published
             if (pacing && pipe && t > ro.slack) wait_group_min(prog, EPW, (uint32_t)(t - ro.slack));
             wide_sync();
+#ifdef MAPF_STAMPS
+            const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true, ro.exp};   // exp 2 / 3: mapf_observe.h
+#else
             const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
+#endif
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
             if (ovl) publish_count(ctr + 1, (uint32_t)(t + 1));   // ... and observed
@@ -363,7 +367,9 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     // nontemporal observation stores for slot buffers (fresh lines every step) and for a
     // re-written [B] buffer too large to stay resident in the 256 MiB Infinity Cache (c5:
     // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4)
-    const bool nt = ro.slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20);
+    bool nt = ro.slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20);
+    // MAPF_WIDE_NT=0/1 overrides (c4 in place, nt sc1: 6.27 -> 7.03 us per step)
+    if (const char *v = std::getenv("MAPF_WIDE_NT")) nt = std::atoi(v) != 0;
     auto kern = nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
     // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
     // (512 per lane) over the waves it must hold, 4 SIMDs per CU
