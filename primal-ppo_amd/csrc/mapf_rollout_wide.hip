@@ -178,8 +178,7 @@ __device__ inline void wide_plain_barrier() {
 #endif
 
 template <class T, int RW, bool NT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(WIDE_PARAMS) {
-    WIDE_BIND
+__device__ __attribute__((always_inline)) inline void rollout_wide_body(const DevEnv &e, int T_steps, const WideOut &ro) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-aware env order (as the pair-lane rollout): workgroups are dealt round-robin
     // over the 8 XCDs, so each XCD owns one contiguous range of envs
@@ -190,11 +189,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
     // so a pacing wave sees how far the group's other envs are
     const int EPW = ro.epw, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
     const int k = ro.pair ? wv % EPW : wv / ro.wpe;    // this wave's env in the group
-    const int role = ro.pair ? wv / EPW : wv % ro.wpe; // pipelined: 0 steps, 1 observes
+    const int role = ro.pair ? wv / EPW : wv % ro.wpe; // pipelined: 0 steps, 1.. observe
     const int b = wg * EPW + k;
     if (wg * EPW >= e.B) return;
     const int lane = lane_id();
-    const bool pipe = ro.wpe == 2;
+    const bool pipe = ro.wpe >= 2;
+    // observing waves per env (pipelined): observer o (role 1 + o) observes the steps t with
+    // t % nobs == o
+    const int nobs = pipe ? ro.wpe - 1 : 1, obs_o = pipe ? max(role - 1, 0) : 0;
     const int lt = role * 64 + lane, nthr = ro.wpe * 64;   // thread index within the env's waves
     char *esm = smem + (size_t)k * ro.env_lds;
     uint32_t *prog = reinterpret_cast<uint32_t *>(smem + (size_t)EPW * ro.env_lds);   // [EPW] steps observed
@@ -205,14 +207,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
     ObsLds L = wide_layout(e, esm, ro.grid, scratch, lcost, grid);
     const bool ovl = pipe && ro.overlap;
     char *bimg = scratch;                              // where the stepper's BFS maps search
-    uint32_t *ctr = nullptr;                           // overlapped: [0] snapshots published, [1] observed
-    uint32_t *snap0 = nullptr;                         //             the snapshot ring
+    // overlapped: ctr [0] snapshots published, [1 + o] steps observer o has observed
+    uint32_t *ctr = nullptr;
+    uint32_t *snap0 = nullptr;                         // overlapped: the snapshot ring
     if (ovl) {
         char *x = scratch + wide_scratch_bytes<T, RW>(e);
         ctr = reinterpret_cast<uint32_t *>(x);
         snap0 = reinterpret_cast<uint32_t *>(x + 16);
         bimg = x + 16 + WIDE_SNAPS * wide_snap_bytes(e);
-        if (lt < 2) ctr[lt] = 0u;
+        if (lt < 4) ctr[lt] = 0u;
+        if (obs_o > 0) {                               // observers past the first: their own scratch
+            const ptrdiff_t d = (bimg + srch::wave_lds<T, RW>(e.H, e.W) +
+                                 (size_t)(obs_o - 1) * wide_scratch_bytes<T, RW>(e)) - scratch;
+            L.stream = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(L.stream) + d);
+            L.occ = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(L.occ) + d);
+            L.idg = L.idg + d;
+        }
     }
     auto snap_of = [&](int t) {                        // this step's snapshot
         ObsLds S = L;
@@ -285,7 +295,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
     // one loop for both forms (every function inlined once: the kernel's code stays
     // within the instruction cache); unpipelined, the one wave takes both roles in the
     // order step -> BFS maps -> snapshot -> human path -> observe
-    bool stepper = !pipe || role == 0, observer = !pipe || role == 1;
+    bool stepper = !pipe || role == 0, observer = !pipe || role >= 1;
     // the stepping wave bounds the pipeline and shares its SIMD with another env's observing
     // wave, whose work waits on store issue anyway: it goes first when both are ready
     if (pipe && stepper && ro.prio) __builtin_amdgcn_s_setprio(3);
@@ -308,7 +318,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
         if (stepper) {
             bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
             // the slot's previous snapshot (step t - WIDE_SNAPS) has been observed
-            if (ovl && observing && t >= WIDE_SNAPS) wide_wait_ge(ctr + 1, (uint32_t)(t - WIDE_SNAPS + 1));
+            if (ovl && observing && t >= WIDE_SNAPS) {
+                const int tt = t - WIDE_SNAPS;             // its observer's (tt / nobs + 1)-th step
+                wide_wait_ge(ctr + 1 + tt % nobs, (uint32_t)(tt / nobs + 1));
+            }
             // snapshot of step t for the observation, all from the registers: cells, goals,
             // the human's next cell and path cells [1..K] (HP channel)
             if (lane < e.N) { Lt.spos[lane] = rs.pp; Lt.sgoal[lane] = rs.gg; }
@@ -333,7 +346,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
             else rs.hl0 = len;
         }
         WSTAMP(2);
-        if (observer) {
+        if (observer && (nobs == 1 || t % nobs == obs_o)) {
             for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;   // stream then occ
             if (ovl) wide_wait_ge(ctr, (uint32_t)(t + 1));   // snapshot t published
             if (pacing && pipe && t > ro.slack) wait_group_min(prog, EPW, (uint32_t)(t - ro.slack));
@@ -345,13 +358,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void r
 #endif
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
-            if (ovl) publish_count(ctr + 1, (uint32_t)(t + 1));   // ... and observed
-            if (EPW > 1) publish_count(prog + k, (uint32_t)(t + 1));
+            if (ovl) publish_count(ctr + 1 + obs_o, (uint32_t)(t / nobs + 1));   // ... and observed
+            if (pacing) publish_count(prog + k, (uint32_t)(t + 1));
         }
         WSTAMP(3);
     }
     if (stepper) step_regs_store(e, b, lane, rs);
     WSTAMP_END(b, role);
+}
+
+template <class T, int RW, bool NT>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void rollout_wide_kernel(WIDE_PARAMS) {
+    WIDE_BIND
+    rollout_wide_body<T, RW, NT>(e, T_steps, ro);
+}
+
+// Three waves per env (c4): the stepper and two observers taking alternate steps.  With one
+// observer c4 was bounded by it (5.75 us per step against the stepper's 4.45: one wave per
+// SIMD issuing each step's 31 KiB of stores).  Three waves per SIMD need <= 168 VGPRs:
+// the arguments come through a device pointer (ArgRing), which also frees the ~450 SGPRs the
+// by-value arguments spilled to VGPR lanes (152 VGPRs, 129 SGPR spills, no scratch).
+template <class T, int RW, bool NT>
+__global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void rollout_wide3_kernel(
+    const WideArgs *__restrict__ args, int T_steps) {
+    rollout_wide_body<T, RW, NT>(args->e, T_steps, args->ro);
 }
 
 template <class T, int RW>
@@ -371,6 +401,7 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     // MAPF_WIDE_NT=0/1 overrides (c4 in place, nt sc1: 6.27 -> 7.03 us per step)
     if (const char *v = std::getenv("MAPF_WIDE_NT")) nt = std::atoi(v) != 0;
     auto kern = nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
+    auto kern3 = nt ? rollout_wide3_kernel<T, RW, true> : rollout_wide3_kernel<T, RW, false>;
     // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
     // (512 per lane) over the waves it must hold, 4 SIMDs per CU
     const int vg = kernel_vgprs(reinterpret_cast<const void *>(kern));
@@ -392,6 +423,20 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
 #endif
     size_t lds = wide_lds_bytes<T, RW>(e, r.grid, r.overlap);
     r.wpe = pipe ? 2 : 1;
+    // a second observer (overlapped form) where three waves per env fit on the chip at once,
+    // its scratch fits the CU's LDS share, and all the envs of a CU fit one workgroup (<= 12
+    // waves): three-wave workgroups dealt to a CU one by one did not always land 3 + 3 + 3 + 3
+    // on its SIMDs -- a SIMD asked for a fourth wave (4 x 152 VGPRs > 512) and part of the grid
+    // ran in a second round (c4: 6.2 or 8.3 us per step by launch); one workgroup per CU is
+    // spread evenly
+    const int fit3 = 512 / ((kernel_vgprs(reinterpret_cast<const void *>(kern3)) + 7) & ~7);
+    const size_t lds3 = wide_a16(lds + wide_scratch_bytes<T, RW>(e));
+    if (r.overlap && (3 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit3 && lds3 <= (occ > 1 ? cap : (size_t)64 * 1024) &&
+        e.B % occ == 0 && 3 * occ <= 12 && (size_t)occ * lds3 + 32 <= (size_t)device_max_group_lds() &&
+        env_flag("MAPF_WIDE_OBS", 2) >= 2) {
+        r.wpe = 3;
+        lds = lds3;
+    }
     // one wave per env (c5): all the envs of a CU in one workgroup (<= 8 waves:
     // launch_bounds(512) keeps the 256-VGPR budget), each env's LDS at its own offset, then
     // the pacing counters; every wave runs at most `slack` steps ahead of its group's
@@ -405,16 +450,22 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     // the non-overlapped pipeline would couple the envs, so never there.
     r.env_lds = (int)wide_a16(lds);
     r.epw = 1;
-    int epw = pipe ? 1 : occ;
+    int epw = pipe ? (r.wpe == 3 ? occ : 1) : occ;
     if (const char *v = std::getenv("MAPF_WIDE_EPW")) epw = std::atoi(v);
-    if (epw > 1 && e.B % epw == 0 && epw * r.wpe <= 8 && (!pipe || r.overlap) &&
+    if (epw > 1 && e.B % epw == 0 && epw * r.wpe <= (r.wpe == 3 ? 12 : 8) && (!pipe || r.overlap) &&
         (size_t)epw * r.env_lds + 32 <= (size_t)device_max_group_lds())
         r.epw = epw;
     r.pair = env_flag("MAPF_WIDE_PAIR", 0);
-    r.slack = env_flag("MAPF_WIDE_SLACK", 1);
+    // pacing counters count observations: with two observers per env, not in order (no pacing)
+    r.slack = r.wpe == 3 ? -1 : env_flag("MAPF_WIDE_SLACK", 1);
     if (r.epw > 1) lds = (size_t)device_max_group_lds();   // the whole CU: one group per CU
     else if (cap > lds && cap <= 64 * 1024) lds = cap;
     const dim3 grid_dim(e.B / r.epw), block_dim(64 * r.wpe * r.epw);
+    if (r.wpe == 3) {
+        const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
+        hipLaunchKernelGGL(kern3, grid_dim, block_dim, lds, s, args, steps);
+        return;
+    }
 #if MAPF_ARGS_PTR
     const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
     hipLaunchKernelGGL(kern, grid_dim, block_dim, lds, s, args, steps);
