@@ -427,7 +427,10 @@ def main():
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
         if path == "rollout":
-            kname = ("rollout_random_kernel" if env.rollout_kernel == 1 else "rollout_wide_kernel") + \
+            # the wide rollout without the BFS channel runs three waves per env where they fit
+            # (rollout_wide3_kernel, mapf_rollout_wide.hip) -- every preset config does
+            wide = "rollout_wide3_kernel" if C < 7 else "rollout_wide_kernel"
+            kname = ("rollout_random_kernel" if env.rollout_kernel == 1 else wide) + \
                 ("<true> (nontemporal stores)" if roll else "")
             bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, TR
         elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one

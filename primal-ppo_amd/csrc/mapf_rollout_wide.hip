@@ -48,6 +48,7 @@ struct WideOut {
     int pair;           // epw > 1: wave w is env w % epw's role w / epw (1), else env w / wpe's role w % wpe (0)
     int slack;          // epw > 1: a pacing wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
     int env_lds;        // epw > 1: LDS bytes per env (a multiple of 16); the pacing counters follow the envs
+    int bfsobs;         // three-wave form: the observers search the BFS maps (MAPF_WIDE_BFSOBS, default 1)
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -80,7 +81,8 @@ __host__ __device__ inline size_t wide_grid_bytes(const DevEnv &e) { return wide
 
 // the overlapped pipeline's own areas: a second observation snapshot (spos | sgoal | shn |
 // shp | shpn) and the stepper's BFS image
-__host__ __device__ inline size_t wide_snap_bytes(const DevEnv &e) { return wide_a16((size_t)(2 * e.N + 2 + e.k_predict) * 4); }
+// (+ 2 words after shpn: the agents whose BFS maps the step rebuilds, when the observers search them)
+__host__ __device__ inline size_t wide_snap_bytes(const DevEnv &e) { return wide_a16((size_t)(2 * e.N + 4 + e.k_predict) * 4); }
 // overlapped form: a ring of WIDE_SNAPS snapshots behind two LDS counters (16 B), so the
 // stepper may run up to WIDE_SNAPS - 1 steps ahead of the observer
 constexpr int WIDE_SNAPS = 4;
@@ -304,6 +306,12 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
     // phase-cost experiment (no observations written): the stepping role alone
     if (ro.exp == 1) observer = observing = false;
 #endif
+    // Three-wave form: the BFS maps of the agents whose goal changed (nothing in the loop reads
+    // them without the BFS channel) are searched by the observer of that step, after its
+    // observation, instead of on the stepper's chain (c4: 0.59 of its 4.63 us per step).  Step
+    // t's maps are written after step t - 1's (ctr[3]: steps whose maps are done), so an agent's
+    // later map wins; an observer that searched drains its stores before it counts.
+    const bool bfs_obs = ovl && nobs >= 2 && observing && ro.bfsobs;
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
@@ -316,7 +324,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
         if (pipe && !ovl) wide_plain_barrier();
         const ObsLds Lt = snap_of(t);
         if (stepper) {
-            bfs_maps(inl);                               // agent.bfsMap of the agents whose goal changed
+            if (!bfs_obs) bfs_maps(inl);                 // agent.bfsMap of the agents whose goal changed
             // the slot's previous snapshot (step t - WIDE_SNAPS) has been observed
             if (ovl && observing && t >= WIDE_SNAPS) {
                 const int tt = t - WIDE_SNAPS;             // its observer's (tt / nobs + 1)-th step
@@ -331,6 +339,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
                 Lt.shn[0] = rs.hn;
                 const int len = rs.hcur ? rs.hl1 : rs.hl0;
                 Lt.shpn[0] = hp_ch ? max(0, min(e.k_predict, len - 1)) : 0;
+                if (bfs_obs) {
+                    reinterpret_cast<uint32_t *>(Lt.shpn)[1] = (uint32_t)inl.bmask;
+                    reinterpret_cast<uint32_t *>(Lt.shpn)[2] = (uint32_t)(inl.bmask >> 32);
+                }
             }
             if (ovl) publish_count(ctr, (uint32_t)(t + 1));
         }
@@ -358,8 +370,26 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
 #endif
             obs_emit<true, NT>(e, Lt, ro.obs + s * BN * CFF, ro.vec + s * BN * 4, G, b, false);
             wide_sync();
+            uint64_t bm = 0;
+            uint32_t mygoal = 0;
+            if (bfs_obs) {                               // out of the snapshot before its slot is freed
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(Lt.shpn) + 1;
+                bm = (uint64_t)lds_count(w) | ((uint64_t)lds_count(w + 1) << 32);
+                mygoal = Lt.sgoal[min(lane, e.N - 1)];
+            }
             if (ovl) publish_count(ctr + 1 + obs_o, (uint32_t)(t / nobs + 1));   // ... and observed
             if (pacing) publish_count(prog + k, (uint32_t)(t + 1));
+            if (bfs_obs) {
+                wide_wait_ge(ctr + 3, (uint32_t)t);      // step t - 1's maps written
+                for (uint64_t m = bm; m; m &= m - 1ull) {
+                    const int l = ctz64(m);
+                    const uint32_t gl = (uint32_t)__builtin_amdgcn_readlane((int)mygoal, l);
+                    srch::search_one<T, RW>(e, false, b, (uint32_t)b * (uint32_t)e.N + (uint32_t)l, gl, NO_CELL, 0,
+                                            reinterpret_cast<char *>(L.stream), L.mapc);
+                }
+                if (bm) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the maps land before step t + 1's
+                publish_count(ctr + 3, (uint32_t)(t + 1));
+            }
         }
         WSTAMP(3);
     }
@@ -493,7 +523,7 @@ bool rollout_wide_fusable(const DevEnv &e) {
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, ArgRing &ring, hipStream_t s) {
     const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
-                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0};
+                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0, env_flag("MAPF_WIDE_BFSOBS", 1)};
     with_row_type(e, [&](auto t, auto rw) {
         launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
         return 0;

@@ -384,13 +384,16 @@ def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack, monk
     run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
 
 
-@pytest.mark.parametrize("name,nobs", [("c4_40x40_n16_f9_looping", 1), ("dense_12x12_n16_f9_dahp", 1),
-                                       ("w_n12_70x30_f9", 1), ("w_n10_96x60_f7_looping", 2)])
-def test_rollout_wide_observer_count_matches_oracle(name, nobs, monkeypatch):
+@pytest.mark.parametrize("name,nobs,bfsobs", [("c4_40x40_n16_f9_looping", 1, 1), ("dense_12x12_n16_f9_dahp", 1, 1),
+                                              ("w_n12_70x30_f9", 1, 1), ("w_n10_96x60_f7_looping", 2, 1),
+                                              ("dense_12x12_n16_f9_dahp", 2, 0), ("c4_40x40_n16_f9_looping", 2, 0)])
+def test_rollout_wide_observer_count_matches_oracle(name, nobs, bfsobs, monkeypatch):
     """The overlapped two-wave form (MAPF_WIDE_OBS=1: one stepping, one observing wave) and the
-    three-wave form (2: two observers taking alternate steps, the default where it fits) --
-    every slot bit-exact vs the oracle."""
+    three-wave form (2: two observers taking alternate steps, the default where it fits), with
+    the BFS maps searched by the observers (the default) or by the stepper -- every slot and
+    the BFS maps bit-exact vs the oracle."""
     monkeypatch.setenv("MAPF_WIDE_OBS", str(nobs))
+    monkeypatch.setenv("MAPF_WIDE_BFSOBS", str(bfsobs))
     case = FUSED_CASES.get(name) or RANDOM_CASES.get(name) or WIDE_SHAPES[name]
     run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
 
