@@ -36,12 +36,14 @@ env.rollout_random(T)
 b.record()
 torch.cuda.synchronize()
 ms = a.elapsed_time(b)
-tl = env.timeline(min(2 * B, 8192)).astype(np.float64)
+tl = env.timeline(min(3 * B, 8192)).astype(np.float64)
 assert (tl[:B, 7] == 1).all(), "no stamps: MAPF_LIB is not the stamps build"
 names = ["step", "bfs + snapshot", "human path", "observe"]
 print(f"{cfg}: launch {ms * 1e3 / T:.2f} us/step (stamps build)")
-# rows B.. hold the observing waves of the pipelined form
-for who, rows in (("first wave (steps)", tl[:B]), ("observing wave", tl[B:2 * B][tl[B:2 * B, 7] == 1])):
+# rows B.. hold the observing waves of the pipelined form (2B..: the second observer of the
+# three-wave form)
+for who, rows in (("first wave (steps)", tl[:B]), ("observing wave", tl[B:2 * B][tl[B:2 * B, 7] == 1]),
+                  ("second observing wave", tl[2 * B:3 * B][tl[2 * B:3 * B, 7] == 1])):
     if not len(rows):
         continue
     us = rows[:, :4] / 100.0 / T          # s_memrealtime ticks at 100 MHz -> us per step
@@ -64,11 +66,13 @@ if len(rows):
 
 # where the slow envs are: each wave's start / end on the realtime counter and its CU
 # (slot 6 = HW_ID | XCC_ID << 32), grouped by XCD and by CU
-raw = env.timeline(min(2 * B, 8192))
+raw = env.timeline(min(3 * B, 8192))
 rows_all = [("first wave", np.arange(B))]
 if (raw[B:2 * B, 7] == 1).any():
     rows_all.append(("observing wave", np.arange(B, 2 * B)))
-t0 = raw[:2 * B][raw[:2 * B, 7] == 1, 4].min()
+if len(raw) >= 3 * B and (raw[2 * B:3 * B, 7] == 1).any():
+    rows_all.append(("second observing wave", np.arange(2 * B, 3 * B)))
+t0 = raw[:3 * B][raw[:3 * B, 7] == 1, 4].min()
 for who, idx in rows_all:
     r = raw[idx]
     ok = r[:, 7] == 1
@@ -119,7 +123,7 @@ for who, idx in rows_all:
 
 # SIMD sharing: which roles share each SIMD (two waves per SIMD), and each role's mean total by
 # the role of the other wave on its SIMD and by its own wave slot
-if len(rows_all) == 2:
+if len(rows_all) >= 2:
     recs = []
     for role, (who, idx) in enumerate(rows_all):
         r = raw[idx]
@@ -131,7 +135,7 @@ if len(rows_all) == 2:
         key = ((((xcc * 8 + ((h >> 13) & 7)) * 2 + ((h >> 12) & 1)) * 16 + ((h >> 8) & 15)) * 4 + ((h >> 4) & 3))
         tot = r[:, :4].sum(1) / 100.0 / T
         for q in range(len(r)):
-            recs.append((int(key[q]), role, int(h[q] & 15), float(tot[q])))
+            recs.append((int(key[q]), min(role, 1), int(h[q] & 15), float(tot[q])))
     by = {}
     for k_, role, slot, tt in recs:
         by.setdefault(k_, []).append((role, slot, tt))
