@@ -469,7 +469,13 @@ def main():
                          "traffic": round(traffic * steps_pl, 3) if traffic is not None else None,
                          "traffic_unit": "MB/launch (PMC)", "steps_per_launch": steps_pl,
                          "algorithmic_mb": round(bpa * B * N * steps_pl / 1e6, 3), "bytes_per_agent_step": bpa,
-                         "agents_per_step": B * N},
+                         "agents_per_step": B * N,
+                         "residency": ("the re-written [B] observation buffer (%.0f MB) stays in the 256 MiB Infinity "
+                                       "Cache: the PMC EA traffic equals the algorithmic bytes, but it is absorbed "
+                                       "on-die, so this rate can exceed the HBM peak -- the HBM-bound form of the same "
+                                       "work is paths.rollout_slots (fresh lines every step)"
+                                       % (B * N * C * F * F * 4 / 1e6))
+                         if path == "rollout" and not roll and B * N * C * F * F * 4 < 128e6 else "HBM"},
             "device_counters": [int(x) for x in counters[:8]],
         }
         if paths:

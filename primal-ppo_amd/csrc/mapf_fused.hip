@@ -143,6 +143,8 @@ struct RolloutOut {
     int xcd_remap;
     int sub_lds;        // SUBS > 1: LDS bytes of one 4-env quarter (the pacing counters follow the quarters)
     int slack;          // SUBS > 1: a wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
+    int fair;           // SUBS > 1, > 0: a wave more than `fair` steps ahead of the group's slowest env issues at
+                        // priority 0, the others at 2 (no waiting) -- experiment, MAPF_ROLL_FAIR
 };
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
 struct RolloutArgs {
@@ -212,10 +214,15 @@ __global__ __launch_bounds__(256 * SUBS) __attribute__((amdgpu_waves_per_eu(4)))
     __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt/lgkmcnt untouched
     RSTAMP_BEGIN();
     const bool pacing = SUBS > 1 && ro.slack >= 0 && le < nenv;
+    const bool fair = SUBS > 1 && ro.fair > 0 && le < nenv;
     for (int t = 0; t < T; ++t) {
         const DevEnv &E = e;
         const RolloutOut &R = ro;
         if (pacing && t > R.slack) wait_group_min(prog, 4 * SUBS, (uint32_t)(t - R.slack));
+        if (fair) {
+            if ((uint32_t)t > group_min(prog, 4 * SUBS) + (uint32_t)R.fair) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         const size_t BN = (size_t)E.B * E.N;
         const size_t s = R.slots ? (size_t)t : 0;
         StepOut o = R.out;
@@ -235,7 +242,7 @@ __global__ __launch_bounds__(256 * SUBS) __attribute__((amdgpu_waves_per_eu(4)))
             const ObsGroup g = obs_wave_init(E, L, le, mreg);
             obs_emit<false, NT>(E, L, R.obs + s * BN * E.C * E.F * E.F, R.vec + s * BN * 4, g, b0, false);
             step_pairs_search_inline(E, dfr, slds, L.mapc + (size_t)le * L.rowsz, rs);
-            if (pacing) publish_count(prog + gw, (uint32_t)(t + 1));
+            if (pacing || fair) publish_count(prog + gw, (uint32_t)(t + 1));
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -270,10 +277,16 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     // unpaced 13.8-13.9 -- so it keeps four workgroups.  MAPF_ROLL_GROUP=0/1 overrides.
     const size_t sub = (rollout_lds_bytes(e) + 15) & ~(size_t)15;
     const int gsel = env_flag("MAPF_ROLL_GROUP", -1);
+    // In place (c2): the same one workgroup per CU, but issue priority by progress instead of
+    // waits: a wave more than 4 steps ahead of the group's slowest env drops to priority 0, the
+    // rest run at 2 -- no wave ever idles, and the youngest wave of a SIMD no longer trails
+    // (13.9-14.0 -> 11.9-12.0 us per step; MAPF_ROLL_FAIR, 0: four workgroups, unpaced).
+    const int fair = env_flag("MAPF_ROLL_FAIR", slots ? 0 : 4);
     const bool group = occ == 4 && grid % 4 == 0 && 4 * sub + 64 <= (size_t)device_max_group_lds() &&
-                       (gsel < 0 ? slots != 0 : gsel != 0);
+                       (gsel < 0 ? slots != 0 || fair > 0 : gsel != 0);
     const int remap = env_flag("MAPF_XCD_REMAP", 1) != 0;
-    const RolloutOut ro{actions, out, obs, vec, slots, remap, (int)sub, env_flag("MAPF_ROLL_SLACK", 1)};
+    const RolloutOut ro{actions, out, obs, vec, slots, remap, (int)sub,
+                        fair > 0 ? -1 : env_flag("MAPF_ROLL_SLACK", 1), fair};
     auto launch = [&](auto kern, int subs) {
         const dim3 gd(grid / subs), bd(256 * subs);
         const size_t l = subs > 1 ? (size_t)device_max_group_lds() : lds;   // subs > 1: the whole CU

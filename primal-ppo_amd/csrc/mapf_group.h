@@ -109,6 +109,15 @@ __device__ inline void publish_count(uint32_t *c, uint32_t v) {
     __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
     if (lane_id() == 0) *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(as_lds(c)) = v;
 }
+// the smallest of the n (<= 64) counters p[0..n), wave-uniform
+__device__ inline uint32_t group_min(const uint32_t *p, int n) {
+    const int l = lane_id();
+    uint32_t x = l < n ? *reinterpret_cast<volatile __attribute__((address_space(3))) uint32_t *>(
+                             as_lds(const_cast<uint32_t *>(p + l)))
+                       : 0xFFFFFFFFu;
+    for (int o = 1; o < n; o <<= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
 // pacing: wait until each of the n (<= 64) counters p[0..n) has reached v
 __device__ inline void wait_group_min(const uint32_t *p, int n, uint32_t v) {
     const int l = lane_id();

@@ -49,6 +49,8 @@ struct WideOut {
     int slack;          // epw > 1: a pacing wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
     int env_lds;        // epw > 1: LDS bytes per env (a multiple of 16); the pacing counters follow the envs
     int bfsobs;         // three-wave form: the observers search the BFS maps (MAPF_WIDE_BFSOBS, default 1)
+    int fair;           // one-wave form, epw > 1, > 0: a wave more than `fair` steps ahead of its group's slowest
+                        // env issues at priority 0, the others at 2, instead of waiting (MAPF_WIDE_FAIR)
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -203,6 +205,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
     char *esm = smem + (size_t)k * ro.env_lds;
     uint32_t *prog = reinterpret_cast<uint32_t *>(smem + (size_t)EPW * ro.env_lds);   // [EPW] steps observed
     const bool pacing = EPW > 1 && ro.slack >= 0;
+    const bool fairw = EPW > 1 && ro.fair > 0 && !(ro.wpe >= 2);
     char *scratch;
     float *lcost;
     uint8_t *grid;
@@ -316,6 +319,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
         if (pacing && !pipe && t > ro.slack) wait_group_min(prog, EPW, (uint32_t)(t - ro.slack));
+        if (fairw) {
+            if ((uint32_t)t > group_min(prog, EPW) + (uint32_t)ro.fair) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         StepInline inl;
         if (stepper) step_group<WaveGroup, true, true>(e, lact + s * BN, step_out(s), 3u, 0, b, g, &inl, src, rs, have);
         WSTAMP(0);
@@ -378,7 +385,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
                 mygoal = Lt.sgoal[min(lane, e.N - 1)];
             }
             if (ovl) publish_count(ctr + 1 + obs_o, (uint32_t)(t / nobs + 1));   // ... and observed
-            if (pacing) publish_count(prog + k, (uint32_t)(t + 1));
+            if (pacing || fairw) publish_count(prog + k, (uint32_t)(t + 1));
             if (bfs_obs) {
                 wide_wait_ge(ctr + 3, (uint32_t)t);      // step t - 1's maps written
                 for (uint64_t m = bm; m; m &= m - 1ull) {
@@ -487,7 +494,8 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
         r.epw = epw;
     r.pair = env_flag("MAPF_WIDE_PAIR", 0);
     // pacing counters count observations: with two observers per env, not in order (no pacing)
-    r.slack = r.wpe == 3 ? -1 : env_flag("MAPF_WIDE_SLACK", 1);
+    r.fair = r.wpe == 1 ? env_flag("MAPF_WIDE_FAIR", 0) : 0;
+    r.slack = (r.wpe == 3 || r.fair > 0) ? -1 : env_flag("MAPF_WIDE_SLACK", 1);
     if (r.epw > 1) lds = (size_t)device_max_group_lds();   // the whole CU: one group per CU
     else if (cap > lds && cap <= 64 * 1024) lds = cap;
     const dim3 grid_dim(e.B / r.epw), block_dim(64 * r.wpe * r.epw);
@@ -523,7 +531,7 @@ bool rollout_wide_fusable(const DevEnv &e) {
 void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                          int slots, ArgRing &ring, hipStream_t s) {
     const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
-                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0, env_flag("MAPF_WIDE_BFSOBS", 1)};
+                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0, env_flag("MAPF_WIDE_BFSOBS", 1), 0};
     with_row_type(e, [&](auto t, auto rw) {
         launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
         return 0;

@@ -294,6 +294,16 @@ def test_rollout_random_cu_groups_match_oracle(name, slack, monkeypatch):
     run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1)
 
 
+@pytest.mark.parametrize("name,fair", [("g_n8_20x20_f11", 4), ("g_n6_16x16_f9_dahp_ragged", 1)])
+def test_rollout_random_fair_priority_matches_oracle(name, fair, monkeypatch):
+    """The pair-lane rollout with all 16 waves of a CU in one workgroup and issue priority by
+    progress (a wave more than `fair` steps ahead of the group's slowest env drops to priority
+    0; ragged B: the envs past B never count) -- every slot bit-exact vs the oracle."""
+    monkeypatch.setenv("MAPF_ROLL_OCC", "4")
+    monkeypatch.setenv("MAPF_ROLL_FAIR", str(fair))
+    run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1)
+
+
 # the one-wave-per-env kernel's other search row layouts (u32 rows on two lane slots, u64 on
 # two, 128-bit rows on one) and the BFS channel on a non-square map
 WIDE_SHAPES = {
@@ -371,7 +381,7 @@ def test_rollout_wide_one_wave_form_matches_oracle(name, grid, monkeypatch):
 @pytest.mark.parametrize("name,pipe,epw,pair,slack", [
     ("c4_40x40_n16_f9_looping", 1, 4, 0, 4), ("c4_40x40_n16_f9_looping", 1, 4, 1, 0),
     ("dense_12x12_n16_f9_dahp", 1, 2, 0, -1), ("dense_12x12_n16_f9_dahp", 0, 8, 0, 4),
-    ("c5_80x80_n64_f11_bfsch", 0, 3, 0, 1)])
+    ("c5_80x80_n64_f11_bfsch", 0, 3, 0, 1), ("dense_12x12_n16_f9_dahp", 0, 4, 0, -3)])
 def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack, monkeypatch):
     """Several envs per workgroup (all the envs of a CU at full size), each at its own LDS
     offset, their pacing waves kept within `slack` steps of the group's slowest env: the
@@ -379,7 +389,9 @@ def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack, monk
     monkeypatch.setenv("MAPF_WIDE_PIPE", str(pipe))
     monkeypatch.setenv("MAPF_WIDE_EPW", str(epw))
     monkeypatch.setenv("MAPF_WIDE_PAIR", str(pair))
-    monkeypatch.setenv("MAPF_WIDE_SLACK", str(slack))
+    monkeypatch.setenv("MAPF_WIDE_SLACK", str(max(slack, -1)))
+    if slack < -1:      # issue priority by progress instead of waits (MAPF_WIDE_FAIR = -slack - 1)
+        monkeypatch.setenv("MAPF_WIDE_FAIR", str(-slack - 1))
     case = FUSED_CASES.get(name) or RANDOM_CASES[name]
     run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
 
