@@ -169,7 +169,7 @@ def make_maps(kind, B, H, W, rank):
 # workload's (B, N, H, W, F, C) and kernel
 PMC_REPORTS = {((4096, 8, 20, 20, 11, 6), "observe_kernel"): "r01_pmc_observe_c2.json",
                ((4096, 8, 20, 20, 11, 6), "step_observe_kernel"): "r01_pmc_step_observe_c2.json",
-               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r03b_pmc_rollout_c2.json",   # [B] buffers
+               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r03c_pmc_rollout_c2.json",   # [B] buffers
                ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel<true>"): "r03_pmc_rollout_c2slots.json",
                ((1024, 16, 40, 40, 9, 6), "rollout_wide_kernel"): "r03_pmc_rollout_wide_c4.json",
                ((1024, 16, 40, 40, 9, 6), "rollout_wide3_kernel"): "r03b_pmc_rollout_wide3_c4.json",
