@@ -9,9 +9,12 @@ Paths (--path):
   rollout (default)  mapf_rollout_random: a random-policy rollout of T steps per
                      launch (T = --rollout-steps, default 256 = the reference's
                      N_STEPS, alg_parameters.py:68); each wave owns one env and
-                     loops step -> observe -> its own search work.  Every step's
-                     actions, outputs and observation are written (to the same
-                     [B]-leading buffers; --slots: to [T]-slot rollout buffers).
+                     loops step -> observe -> its own search work.  Step t's
+                     actions, outputs and observation are written to slot t of
+                     [T]-leading rollout buffers -- the runner's per-rollout arrays
+                     (runner.py:104-115), a fresh HBM line for every store;
+                     --inplace: every step re-writes the same [B]-leading buffers
+                     (the per-step API's; at c2 they stay in the Infinity Cache).
   fused              one mapf_step_observe_random launch per step (the path a
                      policy-in-the-loop rollout uses), hipGraph replays of 24 steps
   split              mapf_step_random + mapf_observe, two launches per step
@@ -166,20 +169,20 @@ def make_maps(kind, B, H, W, rank):
 
 
 # committed rocprofv3 --pmc passes (WRITE_SIZE + FETCH_SIZE, tools/pmc_report.py), by the
-# workload's (B, N, H, W, F, C) and kernel
-PMC_REPORTS = {((4096, 8, 20, 20, 11, 6), "observe_kernel"): "r01_pmc_observe_c2.json",
-               ((4096, 8, 20, 20, 11, 6), "step_observe_kernel"): "r01_pmc_step_observe_c2.json",
-               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel"): "r03c_pmc_rollout_c2.json",   # [B] buffers
-               ((4096, 8, 20, 20, 11, 6), "rollout_random_kernel<true>"): "r03_pmc_rollout_c2slots.json",
-               ((1024, 16, 40, 40, 9, 6), "rollout_wide_kernel"): "r03_pmc_rollout_wide_c4.json",
-               ((1024, 16, 40, 40, 9, 6), "rollout_wide3_kernel"): "r03b_pmc_rollout_wide3_c4.json",
-               ((2048, 64, 80, 80, 11, 7), "rollout_wide_kernel"): "r03b_pmc_rollout_wide_c5.json"}
+# workload's (B, N, H, W, F, C), the kernel instantiation (mapf_rollout_plan) and slot buffers
+C2, C4, C5 = (4096, 8, 20, 20, 11, 6), (1024, 16, 40, 40, 9, 6), (2048, 64, 80, 80, 11, 7)
+PMC_REPORTS = {(C2, "observe_kernel", False): "r01_pmc_observe_c2.json",
+               (C2, "step_observe_kernel", False): "r01_pmc_step_observe_c2.json",
+               (C2, "rollout_random_kernel<false,4>", False): "r03c_pmc_rollout_c2.json",
+               (C2, "rollout_random_kernel<true,4>", True): "r03_pmc_rollout_c2slots.json",
+               (C4, "rollout_wide3_kernel<u64,1,false>", False): "r03b_pmc_rollout_wide3_c4.json",
+               (C5, "rollout_wide_kernel<Row2,2,true>", False): "r03b_pmc_rollout_wide_c5.json"}
 
 
-def pmc_traffic_per_step(B, N, H, W, F, C, kernel):
+def pmc_traffic_per_step(B, N, H, W, F, C, kernel, slots=False):
     """HBM bytes per lockstep step of `kernel` (MB) from the committed PMC report of this
     workload (per launch / steps per launch) -- null where none is committed."""
-    path = os.path.join(ROOT, "profiles", PMC_REPORTS.get(((B, N, H, W, F, C), kernel), "-"))
+    path = os.path.join(ROOT, "profiles", PMC_REPORTS.get(((B, N, H, W, F, C), kernel, bool(slots)), "-"))
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -204,8 +207,14 @@ def main():
     ap.add_argument("--path", default="rollout", choices=["rollout", "fused", "split"])
     ap.add_argument("--split", action="store_true", help="= --path split")
     ap.add_argument("--rollout-steps", type=int, default=256, help="steps per mapf_rollout_random launch")
-    ap.add_argument("--slots", action="store_true",
-                    help="rollout path: write step t to slot t of [T]-leading rollout buffers")
+    ap.add_argument("--inplace", action="store_true",
+                    help="rollout path: every step re-writes the same [B]-leading buffers instead of slot t of "
+                         "[T]-leading rollout buffers (the default, runner.py:104-115)")
+    ap.add_argument("--slots", action="store_true", help=argparse.SUPPRESS)   # the default since round 4
+    ap.add_argument("--slot-gb", type=float, default=40.0,
+                    help="cap on the slot buffers (GB): launches of fewer steps where 256 slots would exceed it")
+    ap.add_argument("--tune", default="",
+                    help="launch forms, mapf_tuning fields of include/mapf.h as k=v[,k=v...] (identical results)")
     ap.add_argument("--graph-steps", type=int, default=24,
                     help="fused/split paths: steps per captured hipGraph, a multiple of 3; 0 = direct")
     ap.add_argument("--kernel-launches", type=int, default=None,
@@ -252,20 +261,23 @@ def main():
     world, shared = make_maps(preset["maps"], B, H, W, rank)
     env = BatchedMapfGym(make_config(B, H, W, num_agents=N, fov=F, num_channel=C, human_mode="random",
                                      goal_mode="random", fix_choice=1, seed=1234, env_offset=rank * B,
-                                     shared_map=shared), device=dev)
+                                     shared_map=shared), device=dev, tuning=args.tune)
     env.reset_seeded(world)
     path = args.path
     if path == "rollout" and not env.rollout_fused:
         path = "fused"                       # the one-launch rollout does not cover this config
     obs, vec, acts = env.obs, env.vec, env.actions
     K = args.steps
-    T = max(1, min(args.rollout_steps, K))
+    slot_bytes = B * N * ((C * F * F + 4) * 4 + 4 + 45) + B * 4          # one step's slot of every buffer
+    TS = max(1, min(args.rollout_steps, int(args.slot_gb * 1e9 // slot_bytes)))
+    slotted = path == "rollout" and not args.inplace
+    T = max(1, min(args.rollout_steps, K, TS if slotted else K))
 
     roll = None
-    if path == "rollout" and args.slots:    # [T]-slot rollout buffers (runner.py's per-rollout arrays)
-        roll = dict(actions=torch.zeros(T, B, N, dtype=torch.int32, device=dev),
-                    obs=torch.zeros(T, B, N, C, F, F, device=dev), vec=torch.zeros(T, B, N, 4, device=dev),
-                    out={k: torch.zeros((T,) + tuple(v.shape), dtype=v.dtype, device=dev)
+    if slotted:    # [T]-slot rollout buffers (runner.py's per-rollout arrays): TS slots, launches of T <= TS steps
+        roll = dict(actions=torch.zeros(TS, B, N, dtype=torch.int32, device=dev),
+                    obs=torch.zeros(TS, B, N, C, F, F, device=dev), vec=torch.zeros(TS, B, N, 4, device=dev),
+                    out={k: torch.zeros((TS,) + tuple(v.shape), dtype=v.dtype, device=dev)
                          for k, v in env.out.items()})
 
     def rollout(n):
@@ -375,7 +387,7 @@ def main():
     # the roofline kernel is timed over launches of --rollout-steps steps (the production launch
     # length, the reference's N_STEPS = 256) whatever --steps is: a short timed run (one launch
     # of K < 256 steps) pays the launch's ramp once over few steps, which `value` includes
-    TR = T if roll is not None else max(1, args.rollout_steps)
+    TR = TS if roll is not None else max(1, args.rollout_steps)
     if path == "rollout":
         KT = args.kernel_launches or max(3, min(20, K // T))
         if TR != T:
@@ -405,41 +417,55 @@ def main():
         else:   # mapf_step_observe = step launch, then observe with the step's search forked beside it
             paths["split"] = entry(fused_ms, bpa_f, f"HIP events around {KS} mapf_step_observe calls (step, "
                                                     f"observe + forked search; breakdown_ms.split has them serial)")
+        def entry_inplace(ms_step, bpa, note):
+            e = entry(ms_step, bpa, note)
+            if B * N * C * F * F * 4 < 128e6:
+                # re-written in place, the buffer stays in the 256 MiB Infinity Cache (the PMC EA writes
+                # equal the algorithmic bytes but are absorbed on-die): no HBM roofline applies
+                e["frac"] = None
+                e["bound"] = ("infinity_cache: the %.0f MB [B] buffer is re-written every step and stays resident; "
+                              "the HBM-bound form of the same work is rollout_slots" % (B * N * C * F * F * 4 / 1e6))
+            return e
         if env.rollout_fused:
             if roll is None:
-                paths["rollout_inplace"] = entry(roll_ms / TR, bpa_f, f"HIP events, {KT} launches of {TR} steps")
-                TS = min(T, max(8, int(25e9 // (B * N * (C * F * F + 4) * 4))))   # <= ~25 GB of slots
-                sl = dict(actions=torch.zeros(TS, B, N, dtype=torch.int32, device=dev),
-                          obs=torch.zeros(TS, B, N, C, F, F, device=dev), vec=torch.zeros(TS, B, N, 4, device=dev),
-                          out={k: torch.zeros((TS,) + tuple(v.shape), dtype=v.dtype, device=dev)
+                paths["rollout_inplace"] = entry_inplace(roll_ms / TR, bpa_f, f"HIP events, {KT} launches of {TR} steps")
+                TS2 = min(TS, max(8, int(25e9 // slot_bytes)))   # <= ~25 GB of slots
+                sl = dict(actions=torch.zeros(TS2, B, N, dtype=torch.int32, device=dev),
+                          obs=torch.zeros(TS2, B, N, C, F, F, device=dev), vec=torch.zeros(TS2, B, N, 4, device=dev),
+                          out={k: torch.zeros((TS2,) + tuple(v.shape), dtype=v.dtype, device=dev)
                                for k, v in env.out.items()})
-                run_sl = lambda: env.rollout_random(TS, slots=True, **sl)   # noqa: E731
+                run_sl = lambda: env.rollout_random(TS2, slots=True, **sl)   # noqa: E731
                 run_sl()
                 ms = event_ms(run_sl, max(2, min(8, KT)))
-                paths["rollout_slots"] = entry(ms / TS, bpa_f, f"HIP events, {max(2, min(8, KT))} launches of "
-                                                               f"{TS} steps, {TS} slots")
+                paths["rollout_slots"] = entry(ms / TS2, bpa_f, f"HIP events, {max(2, min(8, KT))} launches of "
+                                                                f"{TS2} steps, {TS2} slots")
                 del sl
                 torch.cuda.empty_cache()
             else:
-                paths["rollout_slots"] = entry(roll_ms / T, bpa_f, f"HIP events, {KT} launches of {T} steps")
+                paths["rollout_slots"] = entry(roll_ms / TR, bpa_f, f"HIP events, {KT} launches of {TR} steps")
+                run_ip = lambda: env.rollout_random(args.rollout_steps)   # noqa: E731
+                run_ip()
+                ms = event_ms(run_ip, max(3, min(8, KT)))
+                paths["rollout_inplace"] = entry_inplace(ms / args.rollout_steps, bpa_f,
+                                                         f"HIP events, {max(3, min(8, KT))} launches of "
+                                                         f"{args.rollout_steps} steps")
     counters = env.counters()
 
     if rank == 0:
         total_agent_steps = world_size * B * N * K
         value = total_agent_steps / elapsed
         if path == "rollout":
-            # the wide rollout without the BFS channel runs three waves per env where they fit
-            # (rollout_wide3_kernel, mapf_rollout_wide.hip) -- every preset config does
-            wide = "rollout_wide3_kernel" if C < 7 else "rollout_wide_kernel"
-            kname = ("rollout_random_kernel" if env.rollout_kernel == 1 else wide) + \
-                ("<true> (nontemporal stores)" if roll else "")
+            # the template instantiation the library launched (mapf_rollout_plan), e.g.
+            # rollout_random_kernel<true,4> at c2 (slot buffers, the 16 waves of a CU in one workgroup)
+            kname = env.rollout_kernel_name(slots=roll is not None)
             bpa, kms, steps_pl = fused_bytes_per_agent(C, F, H, W, N), roll_ms, TR
         elif path == "split" or not env.fused:   # two launches per step: the observe kernel is the roofline one
             kname, bpa, kms, steps_pl = "observe_kernel", observe_bytes_per_agent(C, F, H, W, N), obs_ms, 1
         else:
             kname, bpa, kms, steps_pl = "step_observe_kernel", fused_bytes_per_agent(C, F, H, W, N), fused_ms, 1
         achieved = bpa * B * N * steps_pl / (kms * 1e-3) / 1e9
-        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname.split("<")[0] + ("<true>" if roll else ""))
+        traffic = pmc_traffic_per_step(B, N, H, W, F, C, kname, slots=roll is not None)
+        ic_resident = path == "rollout" and roll is None and B * N * C * F * F * 4 < 128e6
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world_size,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -450,8 +476,10 @@ def main():
                                    f"{C} channels, random policy, env.step+observe",
                        "num_envs_per_gpu": B, "num_agents": N, "grid": [H, W], "fov": F, "channels": C,
                        "human": "Human (random goals, device A*)", "goals": "lifelong, random", "keep_bfs": True,
-                       "path": path + (f" (T={T} steps per launch{', slot buffers' if roll else ''})"
+                       "path": path + (f" (T={T} steps per launch, " + (f"[{TS}]-slot rollout buffers" if roll
+                                                                         else "[B] buffers re-written in place") + ")"
                                        if path == "rollout" else ""),
+                       "kernel_form": env.rollout_plan(slots=roll is not None) if path == "rollout" else None,
                        "total_envs": B * world_size,
                        "parallelism": f"env-shards x{world_size}"},
             "breakdown_ms": {"rollout_launch": round(roll_ms, 4) if roll_ms else None,
@@ -464,18 +492,18 @@ def main():
                                        + (f"{KT} rollout launches, " if path == "rollout" else "") + f"{KS} of each "
                                        f"per-step path; split: search flushed alone); value timed over the {path} "
                                        f"path" + (f" with hipGraph replays of {G} steps" if graph else "")},
-            "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "roofline": {"kernel": kname, "bound": "infinity_cache" if ic_resident else "hbm",
+                         "achieved": round(achieved, 1),
+                         "peak": None if ic_resident else HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": None if ic_resident else round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic * steps_pl, 3) if traffic is not None else None,
                          "traffic_unit": "MB/launch (PMC)", "steps_per_launch": steps_pl,
                          "algorithmic_mb": round(bpa * B * N * steps_pl / 1e6, 3), "bytes_per_agent_step": bpa,
                          "agents_per_step": B * N,
-                         "residency": ("the re-written [B] observation buffer (%.0f MB) stays in the 256 MiB Infinity "
-                                       "Cache: the PMC EA traffic equals the algorithmic bytes, but it is absorbed "
-                                       "on-die, so this rate can exceed the HBM peak -- the HBM-bound form of the same "
-                                       "work is paths.rollout_slots (fresh lines every step)"
-                                       % (B * N * C * F * F * 4 / 1e6))
-                         if path == "rollout" and not roll and B * N * C * F * F * 4 < 128e6 else "HBM"},
+                         "residency": ("--inplace: the re-written [B] observation buffer (%.0f MB) stays in the 256 MiB "
+                                       "Infinity Cache, so no HBM roofline applies (the HBM-bound form of the same work "
+                                       "is the default slot-buffer path)" % (B * N * C * F * F * 4 / 1e6))
+                         if ic_resident else "HBM: every store a fresh line" if roll is not None else "HBM"},
             "device_counters": [int(x) for x in counters[:8]],
         }
         if paths:

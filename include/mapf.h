@@ -208,6 +208,50 @@ int mapf_rollout_random(mapf_env *env, int32_t T, int32_t slots, int32_t *action
  * fits 64 KiB: up to 64 agents, per-env maps, the BFS channel (c4, c5). */
 int mapf_rollout_random_fused(const mapf_env *env);
 
+/* Launch tuning of one handle: which form of a kernel the launches take (the measured choices
+ * of DESIGN.md §4 / §9).  The reference has no counterpart (its env is Python); these fields
+ * only pick between forms that produce identical results.  mapf_create sets the defaults
+ * (mapf_tuning_default); nothing is read from the process environment.  A field at its
+ * default means "the measured choice for this configuration", which may depend on B, N, the
+ * map size, slots and the device (CU count, LDS size, the kernels' VGPR counts). */
+typedef struct mapf_tuning {
+    /* pair-lane rollout (mapf_rollout_random_fused == 1: N in 5..8, shared map) */
+    int32_t roll_occ;        /* workgroups per CU the LDS request admits: 0 = ceil(grid / CUs), 1..16      */
+    int32_t roll_group;      /* the 16 waves of a CU in one workgroup: -1 auto (slots, or roll_fair > 0), 0, 1 */
+    int32_t roll_fair;       /* grouped, issue priority by progress: -1 auto (4 in place, 0 slots), 0 off, n */
+    int32_t roll_slack;      /* grouped, roll_fair 0: waves paced within n steps of the slowest (< 0 off)  */
+    /* one-wave-per-env rollout (mapf_rollout_random_fused == 2: up to 64 agents, per-env maps, C = 7) */
+    int32_t wide_nt;         /* nontemporal observation stores: -1 auto (slots, or a [B] buffer > 128 MB), 0, 1 */
+    int32_t wide_pipe;       /* 1 auto: a stepping and observing waves per env where they fit; 0 one wave   */
+    int32_t wide_grid;       /* 1 auto: the step's LDS neighbour grid where it fits; 0 the agent loop       */
+    int32_t wide_overlap;    /* 1 auto: pipelined through LDS counters (no BFS channel); 0 per-step barriers */
+    int32_t wide_obs;        /* observing waves per env in the overlapped form: 2 (auto, where they fit) or 1 */
+    int32_t wide_epw;        /* envs per workgroup: 0 auto (all the envs of a CU where the form allows), n    */
+    int32_t wide_pair;       /* epw > 1: 0 wave w is env w / wpe's role w % wpe, 1 env w % epw's role w / epw */
+    int32_t wide_slack;      /* one wave per env, epw > 1: paced within n steps of the group's slowest (< 0 off) */
+    int32_t wide_fair;       /* one wave per env, epw > 1: issue priority by progress instead of waits (0 off) */
+    int32_t wide_prio;       /* pipelined: the stepping wave issues at priority 3 (0 off)                   */
+    int32_t wide_bfsobs;     /* three-wave form: the observers search the rebuilt BFS maps (0: the stepper)  */
+    int32_t xcd_remap;       /* persistent kernels: XCD-aware env order (0 off)                            */
+    /* per-step launches */
+    int32_t obs_envs;        /* envs per observe workgroup: 0 auto (64 / N for N <= 8, else 1), 1..64      */
+    int32_t step_block;      /* threads per step workgroup: 64, 128 or 256                                 */
+    int32_t search_blocks;   /* workgroups of an observe launch that run search work: 1..1024              */
+    int32_t band_blocks;     /* zero-band workgroups of the fused step+observe launch: 0..4096             */
+    int32_t agent_lanes;     /* 1: the agent-per-lane step kernel even for N <= 8 (no pair-lane kernels)    */
+    int32_t serial_search;   /* 1: wide maps search, then observe, on one stream                           */
+    int32_t no_defer;        /* 1: a forked search is joined inside its own call                           */
+    int32_t diag_exp;        /* -DMAPF_STAMPS builds only: phase experiment (0 = none)                     */
+} mapf_tuning;
+void mapf_tuning_default(mapf_tuning *t);
+int mapf_get_tuning(const mapf_env *env, mapf_tuning *t);
+/* Validates every field (MAPF_EINVAL, nothing changed, on a bad one); takes effect at the next launch. */
+int mapf_set_tuning(mapf_env *env, const mapf_tuning *t);
+/* The kernel mapf_rollout_random would launch now for `slots`, as text into buf (n bytes, NUL-terminated),
+ * e.g. "rollout_wide3_kernel<u64,1,false> wpe=3 epw=4 grid=1 overlap=1 slack=-1 fair=0".  Returns
+ * mapf_rollout_random_fused's kind (0: per-step launches, text "step_observe") or a negative error. */
+int mapf_rollout_plan(const mapf_env *env, int32_t slots, char *buf, int32_t n);
+
 /* Launch the search work a committed step left pending (agent.bfsMap updates, the
  * humans' next paths) on its own; mapf_observe otherwise runs it inside the
  * observation launch.  Any later call that needs it flushes implicitly.

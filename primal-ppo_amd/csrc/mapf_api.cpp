@@ -56,7 +56,6 @@ struct mapf_env {
     // one API call, so the caller's stream -- and a hipGraph capture of it -- sees one
     // sequence); created on first use
     hipStream_t aux = nullptr, aux2 = nullptr;   // aux: BFS maps the observation reads; aux2: deferred work
-    bool serial_search = false;   // MAPF_SERIAL_SEARCH=1: search, then observe, one stream (A/B timing)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
     // Deferred joins.  A human's next path is read no earlier than two steps after its
     // step queued it (mapf_fused.hip), and agent BFS maps only by the BFS channel
@@ -67,7 +66,7 @@ struct mapf_env {
     hipEvent_t ev_def[2] = {nullptr, nullptr};
     long def_due[2] = {-1, -1};            // join before the step that would make nsteps exceed this
     int def_next = 0;
-    bool no_defer = false;                 // MAPF_NO_DEFER=1: join every search in its own call (A/B timing)
+    mapf_tuning tune;                      // launch forms (mapf_set_tuning); never the process environment
     ArgRing args;                          // device-resident argument blocks of the persistent kernels
     template <class T>
     int alloc(T *&p, size_t n) {
@@ -80,7 +79,83 @@ struct mapf_env {
     }
 };
 
+// the per-step launches' tuning fields live in DevEnv (the kernels read them)
+static void apply_tuning(DevEnv &d, const mapf_tuning &t) {
+    // envs per observe_kernel workgroup: 64/N fills a wave's lanes for N <= 8; above that one
+    // env per workgroup measured fastest (c4, 16 agents: 12.4 us vs 14.2 us at 4 envs, tools/sweep_c45.sh)
+    d.obs_envs = t.obs_envs > 0 ? t.obs_envs : (d.N > 8 ? 1 : 64 / d.N);
+    if (d.obs_envs > d.B) d.obs_envs = d.B;
+    d.step_block = t.step_block;
+    d.search_blocks = t.search_blocks;
+    d.band_blocks = t.band_blocks;   // zero-band workgroups: slower than the waves' table-driven stores (0)
+    d.force_agent_lanes = t.agent_lanes;
+}
+
 extern "C" {
+
+void mapf_tuning_default(mapf_tuning *t) {
+    if (!t) return;
+    *t = mapf_tuning{};
+    t->roll_occ = 0;
+    t->roll_group = -1;
+    t->roll_fair = -1;
+    t->roll_slack = 1;
+    t->wide_nt = -1;
+    t->wide_pipe = 1;
+    t->wide_grid = 1;
+    t->wide_overlap = 1;
+    t->wide_obs = 2;
+    t->wide_epw = 0;
+    t->wide_pair = 0;
+    t->wide_slack = 1;
+    t->wide_fair = 0;
+    t->wide_prio = 1;
+    t->wide_bfsobs = 1;
+    t->xcd_remap = 1;
+    t->obs_envs = 0;
+    t->step_block = 256;
+    t->search_blocks = 64;
+    t->band_blocks = 0;
+    t->agent_lanes = 0;
+    t->serial_search = 0;
+    t->no_defer = 0;
+    t->diag_exp = 0;
+}
+
+int mapf_get_tuning(const mapf_env *e, mapf_tuning *t) {
+    if (!e || !t) return fail(MAPF_EINVAL, "null argument");
+    *t = e->tune;
+    return MAPF_OK;
+}
+
+int mapf_set_tuning(mapf_env *e, const mapf_tuning *t) {
+    if (!e || !t) return fail(MAPF_EINVAL, "null argument");
+    auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
+    auto flag = [&](int v) { return in(v, 0, 1); };
+    if (!in(t->roll_occ, 0, 16)) return fail(MAPF_EINVAL, "roll_occ must be in 0..16");
+    if (!in(t->roll_group, -1, 1)) return fail(MAPF_EINVAL, "roll_group must be -1, 0 or 1");
+    if (!in(t->roll_fair, -1, 1 << 20)) return fail(MAPF_EINVAL, "roll_fair must be >= -1");
+    if (!in(t->roll_slack, -1, 1 << 20)) return fail(MAPF_EINVAL, "roll_slack must be >= -1");
+    if (!in(t->wide_nt, -1, 1)) return fail(MAPF_EINVAL, "wide_nt must be -1, 0 or 1");
+    if (!flag(t->wide_pipe) || !flag(t->wide_grid) || !flag(t->wide_overlap) || !flag(t->wide_pair) ||
+        !flag(t->wide_prio) || !flag(t->wide_bfsobs) || !flag(t->xcd_remap) || !flag(t->agent_lanes) ||
+        !flag(t->serial_search) || !flag(t->no_defer))
+        return fail(MAPF_EINVAL, "wide_pipe/grid/overlap/pair/prio/bfsobs, xcd_remap, agent_lanes, serial_search, "
+                                 "no_defer must be 0 or 1");
+    if (!in(t->wide_obs, 1, 2)) return fail(MAPF_EINVAL, "wide_obs must be 1 or 2");
+    if (!in(t->wide_epw, 0, 12)) return fail(MAPF_EINVAL, "wide_epw must be in 0..12");
+    if (!in(t->wide_slack, -1, 1 << 20)) return fail(MAPF_EINVAL, "wide_slack must be >= -1");
+    if (!in(t->wide_fair, 0, 1 << 20)) return fail(MAPF_EINVAL, "wide_fair must be >= 0");
+    if (!in(t->obs_envs, 0, 64)) return fail(MAPF_EINVAL, "obs_envs must be in 0..64");
+    if (t->step_block != 64 && t->step_block != 128 && t->step_block != 256)
+        return fail(MAPF_EINVAL, "step_block must be 64, 128 or 256");
+    if (!in(t->search_blocks, 1, 1024)) return fail(MAPF_EINVAL, "search_blocks must be in 1..1024");
+    if (!in(t->band_blocks, 0, 4096)) return fail(MAPF_EINVAL, "band_blocks must be in 0..4096");
+    if (!in(t->diag_exp, 0, 3)) return fail(MAPF_EINVAL, "diag_exp must be in 0..3");
+    e->tune = *t;
+    apply_tuning(e->d, e->tune);
+    return MAPF_OK;
+}
 
 const char *mapf_last_error(void) { return g_err.c_str(); }
 int mapf_abi_version(void) { return MAPF_ABI_VERSION; }
@@ -124,18 +199,8 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     d.seed = c.seed;
     // envs per observe_kernel workgroup: 64/N fills a wave's lanes for N <= 8; above that one
     // env per workgroup measured fastest (c4, 16 agents: 12.4 us vs 14.2 us at 4 envs, tools/sweep_c45.sh)
-    d.obs_envs = d.N > 8 ? 1 : 64 / d.N;
-    d.step_block = 256;
-    d.search_blocks = 64;
-    d.band_blocks = 0;       // zero-band workgroups (MAPF_BAND_BLOCKS): slower than the waves' table-driven stores
-    if (const char *v = std::getenv("MAPF_BAND_BLOCKS")) { int x = std::atoi(v); if (x >= 0 && x <= 4096) d.band_blocks = x; }
-    if (const char *v = std::getenv("MAPF_SEARCH_BLOCKS")) { int x = std::atoi(v); if (x >= 1 && x <= 1024) d.search_blocks = x; }
-    if (const char *v = std::getenv("MAPF_OBS_ENVS")) { int x = std::atoi(v); if (x >= 1 && x <= 64) d.obs_envs = x; }
-    if (const char *v = std::getenv("MAPF_STEP_BLOCK")) { int x = std::atoi(v); if (x == 64 || x == 128 || x == 256) d.step_block = x; }
-    if (const char *v = std::getenv("MAPF_AGENT_LANES")) d.force_agent_lanes = std::atoi(v) != 0;
-    if (const char *v = std::getenv("MAPF_SERIAL_SEARCH")) e->serial_search = std::atoi(v) != 0;
-    if (const char *v = std::getenv("MAPF_NO_DEFER")) e->no_defer = std::atoi(v) != 0;
-    if (d.obs_envs > d.B) d.obs_envs = d.B;
+    mapf_tuning_default(&e->tune);
+    apply_tuning(d, e->tune);
 
     // fp64 lookup table, computed exactly like the reference (numpy sqrt)
     const double R = (double)c.penalty_radius;
@@ -171,7 +236,7 @@ int mapf_create(const mapf_config *cfg, int device, mapf_env **out) {
     rc |= e->alloc(smask, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(e->maps8, nmaps * (size_t)d.H * d.W);
     rc |= e->alloc(cl, cost_lut.size());
-    rc |= e->alloc(e->args.base, ARG_SLOTS * ARG_SLOT_BYTES);
+    rc |= e->alloc(e->args.base, (ARG_SLOTS + ARG_CAPTURE_SLOTS) * ARG_SLOT_BYTES);
     if (rc) {
         std::string m = g_err;
         mapf_destroy(e);
@@ -219,6 +284,15 @@ static bool rollout_random_fused(const mapf_env *e) {
 int mapf_rollout_random_fused(const mapf_env *e) {
     if (!e) return 0;
     return rollout_random_fusable(e->d) ? 1 : (rollout_wide_fusable(e->d) ? 2 : 0);
+}
+int mapf_rollout_plan(const mapf_env *e, int32_t slots, char *buf, int32_t n) {
+    if (!e || !buf || n < 1) return fail(MAPF_EINVAL, "null argument");
+    if (hipSetDevice(e->device) != hipSuccess) return fail(MAPF_EDEVICE, "hipSetDevice failed");
+    const int kind = mapf_rollout_random_fused(e);
+    if (kind == 1) describe_rollout_random(e->d, slots ? 1 : 0, e->tune, buf, (size_t)n);
+    else if (kind == 2) describe_rollout_wide(e->d, slots ? 1 : 0, e->tune, buf, (size_t)n);
+    else std::snprintf(buf, (size_t)n, "step_observe");
+    return kind;
 }
 
 // s waits for the deferred aux-stream searches: every one (all), or those due before the
@@ -451,7 +525,7 @@ static int observe_with_search(mapf_env *e, float *obs, float *vec, hipStream_t 
     }
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
-    const bool defer = !e->no_defer && cap == hipStreamCaptureStatusNone;
+    const bool defer = !e->tune.no_defer && cap == hipStreamCaptureStatusNone;
     const bool bfsch = e->d.C >= 7 && e->d.keep_bfs;
     const int parity = e->pending;
     e->pending = -1;
@@ -490,7 +564,7 @@ int mapf_observe(mapf_env *e, float *obs, float *vec, void *stream) {
     int nsearch = 0, parity = 0;
     if (e->pending >= 0) {
         if (!observe_hosts_search(e->d) || e->d.C >= 7) {   // wide grids / BFS channel: search beside the launch
-            if (!e->serial_search) return observe_with_search(e, obs, vec, s);
+            if (!e->tune.serial_search) return observe_with_search(e, obs, vec, s);
             if (int rc = flush_search(e, s)) return rc;
         } else {                       // search work rides in the observe launch
             nsearch = e->d.search_blocks;
@@ -565,8 +639,10 @@ int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_
     if (T == 0) return MAPF_OK;
     if (rollout_random_fused(e)) {
         if (int rc = flush_search(e, s)) return rc;     // the kernel searches inline from here on
-        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->args, s))
-            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->args, s);
+        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s) &&
+            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s) != MAPF_OK)
+            return fail(MAPF_ESTATE, "every argument slot for captured persistent launches of this handle is taken "
+                                     "(16 per handle, ArgRing)");
         HIPCHK(hipGetLastError());
         return MAPF_OK;
     }

@@ -23,7 +23,7 @@
 // cells, mapf_gym.py:33-38) and agents' BFS maps (read only by mapf_bfs and
 // the BFS channel, which is not fused).  The step of this launch reads none of
 // what they write (the path buffer it walks is the other one).
-#include <cstdlib>
+#include <cstdio>
 
 #include "mapf_step_pairs.h"
 #include "mapf_search.h"
@@ -144,7 +144,7 @@ struct RolloutOut {
     int sub_lds;        // SUBS > 1: LDS bytes of one 4-env quarter (the pacing counters follow the quarters)
     int slack;          // SUBS > 1: a wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
     int fair;           // SUBS > 1, > 0: a wave more than `fair` steps ahead of the group's slowest env issues at
-                        // priority 0, the others at 2 (no waiting) -- experiment, MAPF_ROLL_FAIR
+                        // priority 0, the others at 2 (no waiting; mapf_tuning.roll_fair)
 };
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
 struct RolloutArgs {
@@ -253,8 +253,15 @@ __global__ __launch_bounds__(256 * SUBS) __attribute__((amdgpu_waves_per_eu(4)))
 
 bool rollout_random_fusable(const DevEnv &e) { return rollout_fusable(e) && rollout_lds_bytes(e) <= 64 * 1024; }
 
-bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                           int slots, ArgRing &ring, hipStream_t s) {
+// The pair-lane rollout's launch form for this handle's tuning (mapf.h: mapf_tuning).
+struct RolloutPlan {
+    int subs = 1;        // 4-env quarters per workgroup (4: the 16 waves of a CU in one workgroup)
+    int grid = 0;        // workgroups
+    size_t lds = 0;      // dynamic LDS request
+    int sub_lds = 0, slack = -1, fair = 0, remap = 1;
+};
+
+static bool plan_rollout_random(const DevEnv &e, int slots, const mapf_tuning &tu, RolloutPlan &p) {
     if (!rollout_random_fusable(e)) return false;
     const int grid = (e.B + 3) / 4;
     // Persistent waves: every CU should hold the same number of workgroups, or the
@@ -262,7 +269,7 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     // workgroups per CU at ceil(grid / CUs) (160 KiB of LDS per CU).
     const int ncu = device_cu_count();
     int occ = (grid + ncu - 1) / ncu;
-    if (const char *v = std::getenv("MAPF_ROLL_OCC")) { const int x = std::atoi(v); if (x >= 1 && x <= 16) occ = x; }
+    if (tu.roll_occ >= 1 && tu.roll_occ <= 16) occ = tu.roll_occ;
     size_t lds = rollout_lds_bytes(e);
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     if (occ >= 3 && cap > lds && cap <= 64 * 1024) lds = cap;
@@ -271,39 +278,58 @@ bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepO
     // each SIMD's four waves ran at 12.3 / 14.4 / 16.3 / 18.3 us per step by wave slot
     // (issue goes to the oldest) and the launch waited for the youngest; paced, all run
     // at 16.9 and the launch takes 17.5-17.7 us per step instead of 20.3
-    // (tools/stamps_pairs.py, tools/ab_env.sh).  The in-place buffer stays in the
-    // Infinity Cache and its CUs share out the same throughput either way: paced 14.5-14.7
-    // against 13.8-13.9 (every wave then runs at the pace the youngest ran), grouped but
-    // unpaced 13.8-13.9 -- so it keeps four workgroups.  MAPF_ROLL_GROUP=0/1 overrides.
-    const size_t sub = (rollout_lds_bytes(e) + 15) & ~(size_t)15;
-    const int gsel = env_flag("MAPF_ROLL_GROUP", -1);
+    // (tools/stamps_pairs.py, tools/ab_env.sh).
     // In place (c2): the same one workgroup per CU, but issue priority by progress instead of
     // waits: a wave more than 4 steps ahead of the group's slowest env drops to priority 0, the
     // rest run at 2 -- no wave ever idles, and the youngest wave of a SIMD no longer trails
-    // (13.9-14.0 -> 11.9-12.0 us per step; MAPF_ROLL_FAIR, 0: four workgroups, unpaced).
-    const int fair = env_flag("MAPF_ROLL_FAIR", slots ? 0 : 4);
+    // (13.9-14.0 -> 11.9-12.0 us per step; roll_fair 0 with roll_group 0: four workgroups, unpaced).
+    const size_t sub = (rollout_lds_bytes(e) + 15) & ~(size_t)15;
+    const int fair = tu.roll_fair >= 0 ? tu.roll_fair : (slots ? 0 : 4);
     const bool group = occ == 4 && grid % 4 == 0 && 4 * sub + 64 <= (size_t)device_max_group_lds() &&
-                       (gsel < 0 ? slots != 0 || fair > 0 : gsel != 0);
-    const int remap = env_flag("MAPF_XCD_REMAP", 1) != 0;
-    const RolloutOut ro{actions, out, obs, vec, slots, remap, (int)sub,
-                        fair > 0 ? -1 : env_flag("MAPF_ROLL_SLACK", 1), fair};
-    auto launch = [&](auto kern, int subs) {
-        const dim3 gd(grid / subs), bd(256 * subs);
-        const size_t l = subs > 1 ? (size_t)device_max_group_lds() : lds;   // subs > 1: the whole CU
+                       (tu.roll_group < 0 ? slots != 0 || fair > 0 : tu.roll_group != 0);
+    p.subs = group ? 4 : 1;
+    p.grid = grid / p.subs;
+    p.lds = group ? (size_t)device_max_group_lds() : lds;   // grouped: the whole CU
+    p.sub_lds = (int)sub;
+    p.fair = fair;
+    p.slack = fair > 0 ? -1 : tu.roll_slack;
+    p.remap = tu.xcd_remap != 0;
+    return true;
+}
+
+void describe_rollout_random(const DevEnv &e, int slots, const mapf_tuning &tu, char *buf, size_t n) {
+    RolloutPlan p;
+    if (!plan_rollout_random(e, slots, tu, p)) {
+        std::snprintf(buf, n, "none");
+        return;
+    }
+    std::snprintf(buf, n, "rollout_random_kernel<%s,%d> grid=%d block=%d lds=%zu fair=%d slack=%d remap=%d",
+                  slots ? "true" : "false", p.subs, p.grid, 256 * p.subs, p.lds, p.subs > 1 ? p.fair : 0,
+                  p.subs > 1 ? p.slack : -1, p.remap);
+}
+
+bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                           int slots, const mapf_tuning &tu, ArgRing &ring, hipStream_t s) {
+    RolloutPlan p;
+    if (!plan_rollout_random(e, slots, tu, p)) return false;
+    const RolloutOut ro{actions, out, obs, vec, slots, p.remap, p.sub_lds, p.slack, p.fair};
+    auto launch = [&](auto kern) {
+        const dim3 gd(p.grid), bd(256 * p.subs);
 #if MAPF_ARGS_PTR
         const RolloutArgs *args = push_args(ring, RolloutArgs{e, ro}, s);
-        hipLaunchKernelGGL(kern, gd, bd, l, s, args, T);
+        if (!args) return;
+        hipLaunchKernelGGL(kern, gd, bd, p.lds, s, args, T);
 #else
-        hipLaunchKernelGGL(kern, gd, bd, l, s, e, T, ro);
+        hipLaunchKernelGGL(kern, gd, bd, p.lds, s, e, T, ro);
 #endif
     };
     (void)ring;
-    if (group) {
-        if (slots) launch(rollout_random_kernel<true, 4>, 4);
-        else launch(rollout_random_kernel<false, 4>, 4);
+    if (p.subs == 4) {
+        if (slots) launch(rollout_random_kernel<true, 4>);
+        else launch(rollout_random_kernel<false, 4>);
     } else {
-        if (slots) launch(rollout_random_kernel<true, 1>, 1);
-        else launch(rollout_random_kernel<false, 1>, 1);
+        if (slots) launch(rollout_random_kernel<true, 1>);
+        else launch(rollout_random_kernel<false, 1>);
     }
     return true;
 }

@@ -5,6 +5,7 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "mapf.h"
 #include "mapf_common.h"
 
 namespace mapf {
@@ -47,12 +48,6 @@ inline int kernel_vgprs(const void *fn) {
     return v;
 }
 
-// an integer environment switch (A/B experiments), read at every launch
-inline int env_flag(const char *name, int dflt) {
-    const char *v = std::getenv(name);
-    return v ? std::atoi(v) : dflt;
-}
-
 struct StepOut {          // device pointers (mapf_step_out)
     int8_t *status;
     float *reward;
@@ -90,30 +85,43 @@ void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, 
                          float *obs, float *vec, int nsearch, int sslot, hipStream_t s);
 // T committed random-policy steps + observations in one launch (mapf_fused.hip);
 // false (nothing launched) if the configuration is not covered
+// (the kernel's form from the handle's tuning, mapf.h: mapf_tuning); describe_* write the
+// form launch_* would take as text (mapf_rollout_plan)
 bool rollout_random_fusable(const DevEnv &e);
 bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                           int slots, struct ArgRing &ring, hipStream_t s);
+                           int slots, const mapf_tuning &tu, struct ArgRing &ring, hipStream_t s);
+void describe_rollout_random(const DevEnv &e, int slots, const mapf_tuning &tu, char *buf, size_t n);
 // the same for up to 64 agents / per-env maps / the BFS channel: one wave per env
-// (mapf_rollout_wide.hip); used where the pair-lane rollout does not apply
+// (mapf_rollout_wide.hip); used where the pair-lane rollout does not apply.  Returns MAPF_OK or
+// MAPF_ESTATE (a captured launch found no free argument slot, ArgRing).
 bool rollout_wide_fusable(const DevEnv &e);
-void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                         int slots, struct ArgRing &ring, hipStream_t s);
+int launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                        int slots, const mapf_tuning &tu, struct ArgRing &ring, hipStream_t s);
+void describe_rollout_wide(const DevEnv &e, int slots, const mapf_tuning &tu, char *buf, size_t n);
 
 // Device-resident kernel argument blocks.  A persistent kernel whose arguments (DevEnv + its
 // output pointers, ~0.5 KiB) do not fit in the SGPR file kept them live from the kernarg
 // load on and spilled ~450 SGPRs to VGPR lanes (v_readlane at every use, plus dead stack
 // slots).  Read through a `const __restrict__` pointer instead, every field is an invariant
 // scalar load the register allocator re-issues where it is used.  The block is written on
-// the launch stream by a one-wave kernel that takes it by value (stream-ordered, capturable
-// in a hipGraph), into the next of ARG_SLOTS slots: launches on different streams in flight
-// at once never share a slot unless more than ARG_SLOTS are.
-constexpr size_t ARG_SLOT_BYTES = 2048, ARG_SLOTS = 16;
+// the launch stream by a one-wave kernel that takes it by value (stream-ordered), into the
+// next of ARG_SLOTS ring slots: launches on different streams in flight at once never share a
+// slot unless more than ARG_SLOTS are.  A launch recorded into a hipGraph keeps its slot's
+// address for every replay, so captured launches never take a ring slot (a later direct
+// launch would overwrite it between replays): each gets one of ARG_CAPTURE_SLOTS slots of its
+// own for the life of the handle, and a capture past them fails (MAPF_ESTATE).
+constexpr size_t ARG_SLOT_BYTES = 2048, ARG_SLOTS = 16, ARG_CAPTURE_SLOTS = 16;
 struct ArgRing {
-    char *base = nullptr;     // ARG_SLOTS * ARG_SLOT_BYTES of device memory (owned by the handle)
-    unsigned next = 0;
+    char *base = nullptr;     // (ARG_SLOTS + ARG_CAPTURE_SLOTS) * ARG_SLOT_BYTES of device memory (the handle's)
+    unsigned next = 0;        // ring position
+    unsigned captured = 0;    // capture slots handed out
     template <class A>
-    A *slot() {
+    A *slot(bool capturing) {
         static_assert(sizeof(A) <= ARG_SLOT_BYTES, "argument block larger than a slot");
+        if (capturing) {
+            if (captured >= ARG_CAPTURE_SLOTS) return nullptr;
+            return reinterpret_cast<A *>(base + (ARG_SLOTS + captured++) * ARG_SLOT_BYTES);
+        }
         return reinterpret_cast<A *>(base + (size_t)(next++ % ARG_SLOTS) * ARG_SLOT_BYTES);
     }
 };
@@ -123,10 +131,14 @@ __global__ __launch_bounds__(64) void store_args_kernel(A a, A *dst) {
     if (threadIdx.x == 0) *dst = a;
 }
 
-// a's copy in the ring's next slot, written on stream s before the kernel that reads it
+// a's copy in the ring's next slot (a capture slot while s is being captured), written on
+// stream s before the kernel that reads it; nullptr when no capture slot is left
 template <class A>
 inline const A *push_args(ArgRing &ring, const A &a, hipStream_t s) {
-    A *slot = ring.slot<A>();
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
+    A *slot = ring.slot<A>(cap != hipStreamCaptureStatusNone);
+    if (!slot) return nullptr;
     hipLaunchKernelGGL(store_args_kernel<A>, dim3(1), dim3(64), 0, s, a, slot);
     return slot;
 }

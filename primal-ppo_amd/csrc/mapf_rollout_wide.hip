@@ -22,7 +22,7 @@
 // reads back, stay in HBM (a wave's own stores are visible to its later loads).  LDS per wave:
 // the nibble table, the env's padded map rows, and one scratch area shared by the
 // observation (bit-stream, occupancy, agent grid) and the search (BFS image).
-#include <cstdlib>
+#include <cstdio>
 #include <type_traits>
 
 #define MAPF_WIDE_TU   // mapf_diag.h: no block-timeline stamps here (the WSTAMP rows use that region)
@@ -41,16 +41,16 @@ struct WideOut {
     int xcd_remap;
     int grid;           // the step's neighbour grid: 0 none (agent loop), 1 own LDS, 2 over the scratch
     int overlap;        // pipelined, no BFS channel: one barrier per step (wide_overlap_bytes)
-    int exp;            // diagnostic (stamps) builds only, MAPF_WIDE_EXP=1: no observation
-    int prio;           // pipelined: the stepping wave's issue priority (s_setprio; MAPF_WIDE_PRIO, default 1: c4 -1.6 %)
+    int exp;            // diagnostic (stamps) builds only (mapf_tuning.diag_exp), 1: no observation
+    int prio;           // pipelined: the stepping wave's issue priority (s_setprio; mapf_tuning.wide_prio, default 1: c4 -1.6 %)
     int wpe;            // waves per env: 2 pipelined (stepper + observer), 1 one wave takes both roles
     int epw;            // envs per workgroup (all the envs of one CU, wide_envs_per_group)
     int pair;           // epw > 1: wave w is env w % epw's role w / epw (1), else env w / wpe's role w % wpe (0)
     int slack;          // epw > 1: a pacing wave runs at most `slack` steps ahead of its group's slowest env (< 0: off)
     int env_lds;        // epw > 1: LDS bytes per env (a multiple of 16); the pacing counters follow the envs
-    int bfsobs;         // three-wave form: the observers search the BFS maps (MAPF_WIDE_BFSOBS, default 1)
+    int bfsobs;         // three-wave form: the observers search the BFS maps (mapf_tuning.wide_bfsobs, default 1)
     int fair;           // one-wave form, epw > 1, > 0: a wave more than `fair` steps ahead of its group's slowest
-                        // env issues at priority 0, the others at 2, instead of waiting (MAPF_WIDE_FAIR)
+                        // env issues at priority 0, the others at 2, instead of waiting (mapf_tuning.wide_fair)
 };
 
 // the kernel's arguments, read from device memory (ArgRing, mapf_kernels.h)
@@ -424,8 +424,17 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void r
 template <class T, int RW>
 static bool wide_fits(const DevEnv &e) { return wide_lds_bytes<T, RW>(e) <= 64 * 1024; }
 
+// The launch form for this handle's tuning (mapf.h: mapf_tuning; the measured defaults below)
+struct WidePlan {
+    bool nt = false;     // nontemporal observation stores
+    WideOut r{};         // the form fields (no pointers)
+    size_t lds = 0;
+    int grid = 0, block = 0;
+};
+
 template <class T, int RW>
-static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing &ring, hipStream_t s) {
+static WidePlan plan_wide_t(const DevEnv &e, int slots, const mapf_tuning &tu) {
+    WidePlan p;
     // persistent waves: every CU holds the same number of workgroups (the LDS request caps
     // them at ceil(B / CUs) per CU, 160 KiB of LDS per CU), or the fuller CUs pace each step
     const int ncu = device_cu_count();
@@ -433,30 +442,33 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     const size_t cap = ((size_t)160 * 1024 / (size_t)occ) & ~(size_t)255;
     // nontemporal observation stores for slot buffers (fresh lines every step) and for a
     // re-written [B] buffer too large to stay resident in the 256 MiB Infinity Cache (c5:
-    // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4)
-    bool nt = ro.slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20);
-    // MAPF_WIDE_NT=0/1 overrides (c4 in place, nt sc1: 6.27 -> 7.03 us per step)
-    if (const char *v = std::getenv("MAPF_WIDE_NT")) nt = std::atoi(v) != 0;
-    auto kern = nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
-    auto kern3 = nt ? rollout_wide3_kernel<T, RW, true> : rollout_wide3_kernel<T, RW, false>;
+    // 446 MB, measured 94 vs 124 us per step); smaller ones keep plain stores (c2, c4;
+    // c4 in place, nt sc1: 6.27 -> 7.03 us per step)
+    p.nt = tu.wide_nt >= 0 ? tu.wide_nt != 0 : (slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20));
+    const void *kern = p.nt ? reinterpret_cast<const void *>(rollout_wide_kernel<T, RW, true>)
+                            : reinterpret_cast<const void *>(rollout_wide_kernel<T, RW, false>);
+    const void *kern3 = p.nt ? reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, true>)
+                             : reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, false>);
     // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
     // (512 per lane) over the waves it must hold, 4 SIMDs per CU
-    const int vg = kernel_vgprs(reinterpret_cast<const void *>(kern));
-    const int fit = 512 / ((vg + 7) & ~7);
-    bool pipe = (2 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit;
-    if (const char *v = std::getenv("MAPF_WIDE_PIPE")) pipe = pipe && std::atoi(v) != 0;
+    const int fit = 512 / ((kernel_vgprs(kern) + 7) & ~7);
+    const bool pipe = (2 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit && tu.wide_pipe != 0;
     // the step's neighbour grid: over the scratch when one wave takes both roles (the step
     // runs while the scratch is free), else its own LDS if every env still fits
-    WideOut r = ro;
+    WideOut &r = p.r;
+    r.slots = slots;
+    r.xcd_remap = tu.xcd_remap != 0;
+    r.prio = tu.wide_prio;
+    r.bfsobs = tu.wide_bfsobs;
     r.grid = 0;
     if (!pipe && wide_grid_bytes(e) <= wide_scratch_bytes<T, RW>(e)) r.grid = 2;
     else if (wide_lds_bytes<T, RW>(e, 1) <= (occ > 1 ? cap : (size_t)64 * 1024)) r.grid = 1;
-    if (const char *v = std::getenv("MAPF_WIDE_GRID")) { if (std::atoi(v) == 0) r.grid = 0; }
+    if (tu.wide_grid == 0) r.grid = 0;
     // one barrier per step where the observation reads no BFS map and the extra LDS fits
-    r.overlap = pipe && e.C < 7 && wide_lds_bytes<T, RW>(e, r.grid, true) <= (occ > 1 ? cap : (size_t)64 * 1024);
-    if (const char *v = std::getenv("MAPF_WIDE_OVERLAP")) r.overlap = r.overlap && std::atoi(v) != 0;
+    r.overlap = pipe && e.C < 7 && wide_lds_bytes<T, RW>(e, r.grid, true) <= (occ > 1 ? cap : (size_t)64 * 1024) &&
+                tu.wide_overlap != 0;
 #ifdef MAPF_STAMPS
-    if (const char *v = std::getenv("MAPF_WIDE_EXP")) r.exp = std::atoi(v);
+    r.exp = tu.diag_exp;
 #endif
     size_t lds = wide_lds_bytes<T, RW>(e, r.grid, r.overlap);
     r.wpe = pipe ? 2 : 1;
@@ -466,11 +478,11 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     // on its SIMDs -- a SIMD asked for a fourth wave (4 x 152 VGPRs > 512) and part of the grid
     // ran in a second round (c4: 6.2 or 8.3 us per step by launch); one workgroup per CU is
     // spread evenly
-    const int fit3 = 512 / ((kernel_vgprs(reinterpret_cast<const void *>(kern3)) + 7) & ~7);
+    const int fit3 = 512 / ((kernel_vgprs(kern3) + 7) & ~7);
     const size_t lds3 = wide_a16(lds + wide_scratch_bytes<T, RW>(e));
     if (r.overlap && (3 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit3 && lds3 <= (occ > 1 ? cap : (size_t)64 * 1024) &&
         e.B % occ == 0 && 3 * occ <= 12 && (size_t)occ * lds3 + 32 <= (size_t)device_max_group_lds() &&
-        env_flag("MAPF_WIDE_OBS", 2) >= 2) {
+        tu.wide_obs >= 2) {
         r.wpe = 3;
         lds = lds3;
     }
@@ -481,36 +493,57 @@ static void launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, ArgRing
     // envs) ran 8 % slower than the older one through the whole launch and the launch
     // waited for it (tools/stamps_wide.py, "by dispatch rank in CU"): c5 85.5-85.9 -> 79.8
     // us per step, slack 1 (2: 80.0-80.7, 4: 80.9-81.3, 8: 82.4-83.1, groups unpaced 86.8).
-    // The pipelined form (c4) measured no gain from groups (its CUs share out the same
-    // throughput either way: balanced envs all ran at the slow env's pace) and 4-6 % slower,
-    // so it keeps one env per workgroup.  MAPF_WIDE_EPW overrides; the per-step barriers of
-    // the non-overlapped pipeline would couple the envs, so never there.
+    // The barrier-paced pipeline would couple the envs of a group, so never there.
     r.env_lds = (int)wide_a16(lds);
     r.epw = 1;
-    int epw = pipe ? (r.wpe == 3 ? occ : 1) : occ;
-    if (const char *v = std::getenv("MAPF_WIDE_EPW")) epw = std::atoi(v);
+    const int epw = tu.wide_epw > 0 ? tu.wide_epw : (pipe ? (r.wpe == 3 ? occ : 1) : occ);
     if (epw > 1 && e.B % epw == 0 && epw * r.wpe <= (r.wpe == 3 ? 12 : 8) && (!pipe || r.overlap) &&
         (size_t)epw * r.env_lds + 32 <= (size_t)device_max_group_lds())
         r.epw = epw;
-    r.pair = env_flag("MAPF_WIDE_PAIR", 0);
-    // pacing counters count observations: with two observers per env, not in order (no pacing)
-    r.fair = r.wpe == 1 ? env_flag("MAPF_WIDE_FAIR", 0) : 0;
-    r.slack = (r.wpe == 3 || r.fair > 0) ? -1 : env_flag("MAPF_WIDE_SLACK", 1);
+    r.pair = tu.wide_pair;
+    // pacing counters count observations: with two observers per env, not in order (no pacing).
+    // The stamps build's stepping-only experiment (diag_exp 1) publishes no progress: no pacing.
+    const bool stepping_only = r.exp == 1;
+    r.fair = r.wpe == 1 && !stepping_only ? tu.wide_fair : 0;
+    r.slack = (r.wpe == 3 || r.fair > 0 || stepping_only) ? -1 : tu.wide_slack;
     if (r.epw > 1) lds = (size_t)device_max_group_lds();   // the whole CU: one group per CU
     else if (cap > lds && cap <= 64 * 1024) lds = cap;
-    const dim3 grid_dim(e.B / r.epw), block_dim(64 * r.wpe * r.epw);
+    p.lds = lds;
+    p.grid = e.B / r.epw;
+    p.block = 64 * r.wpe * r.epw;
+    return p;
+}
+
+template <class T, int RW>
+static int launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, const mapf_tuning &tu, ArgRing &ring,
+                         hipStream_t s) {
+    const WidePlan p = plan_wide_t<T, RW>(e, ro.slots, tu);
+    WideOut r = p.r;
+    r.actions = ro.actions;
+    r.out = ro.out;
+    r.obs = ro.obs;
+    r.vec = ro.vec;
     if (r.wpe == 3) {
         const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
-        hipLaunchKernelGGL(kern3, grid_dim, block_dim, lds, s, args, steps);
-        return;
+        if (!args) return MAPF_ESTATE;
+        auto kern3 = p.nt ? rollout_wide3_kernel<T, RW, true> : rollout_wide3_kernel<T, RW, false>;
+        hipLaunchKernelGGL(kern3, dim3(p.grid), dim3(p.block), p.lds, s, args, steps);
+        return MAPF_OK;
     }
+    auto kern = p.nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
 #if MAPF_ARGS_PTR
     const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
-    hipLaunchKernelGGL(kern, grid_dim, block_dim, lds, s, args, steps);
+    if (!args) return MAPF_ESTATE;
+    hipLaunchKernelGGL(kern, dim3(p.grid), dim3(p.block), p.lds, s, args, steps);
 #else
     (void)ring;
-    hipLaunchKernelGGL(kern, grid_dim, block_dim, lds, s, e, steps, r);
+    hipLaunchKernelGGL(kern, dim3(p.grid), dim3(p.block), p.lds, s, e, steps, r);
 #endif
+    return MAPF_OK;
+}
+
+template <class T> constexpr const char *row_name() {
+    return std::is_same<T, uint32_t>::value ? "u32" : (std::is_same<T, uint64_t>::value ? "u64" : "Row2");
 }
 
 // the search row type of a W-wide map; RW = 2 above 64 rows
@@ -528,12 +561,27 @@ bool rollout_wide_fusable(const DevEnv &e) {
     return with_row_type(e, [&](auto t, auto rw) { return wide_fits<decltype(t), decltype(rw)::value>(e); });
 }
 
-void launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                         int slots, ArgRing &ring, hipStream_t s) {
-    const WideOut ro{actions, out, obs, vec, slots, env_flag("MAPF_XCD_REMAP", 1), 0, 0, 0,
-                     env_flag("MAPF_WIDE_PRIO", 1), 1, 1, 0, -1, 0, env_flag("MAPF_WIDE_BFSOBS", 1), 0};
+int launch_rollout_wide(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                        int slots, const mapf_tuning &tu, ArgRing &ring, hipStream_t s) {
+    WideOut ro{};
+    ro.actions = actions;
+    ro.out = out;
+    ro.obs = obs;
+    ro.vec = vec;
+    ro.slots = slots;
+    return with_row_type(e, [&](auto t, auto rw) {
+        return launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, tu, ring, s);
+    });
+}
+
+void describe_rollout_wide(const DevEnv &e, int slots, const mapf_tuning &tu, char *buf, size_t n) {
     with_row_type(e, [&](auto t, auto rw) {
-        launch_wide_t<decltype(t), decltype(rw)::value>(e, T, ro, ring, s);
+        const WidePlan p = plan_wide_t<decltype(t), decltype(rw)::value>(e, slots, tu);
+        std::snprintf(buf, n, "%s<%s,%d,%s> grid=%d block=%d lds=%zu wpe=%d epw=%d grid_mode=%d overlap=%d slack=%d "
+                              "fair=%d prio=%d bfsobs=%d pair=%d remap=%d",
+                      p.r.wpe == 3 ? "rollout_wide3_kernel" : "rollout_wide_kernel", row_name<decltype(t)>(),
+                      (int)decltype(rw)::value, p.nt ? "true" : "false", p.grid, p.block, p.lds, p.r.wpe, p.r.epw,
+                      p.r.grid, p.r.overlap, p.r.slack, p.r.fair, p.r.prio, p.r.bfsobs, p.r.pair, p.r.xcd_remap);
         return 0;
     });
 }

@@ -42,6 +42,17 @@ class State(ctypes.Structure):
     _fields_ = [(n, P) for n in ("pos", "goal", "last_action", "seq_cursor", "human", "human_path", "clock")]
 
 
+TUNING_FIELDS = ("roll_occ", "roll_group", "roll_fair", "roll_slack", "wide_nt", "wide_pipe", "wide_grid",
+                 "wide_overlap", "wide_obs", "wide_epw", "wide_pair", "wide_slack", "wide_fair", "wide_prio",
+                 "wide_bfsobs", "xcd_remap", "obs_envs", "step_block", "search_blocks", "band_blocks", "agent_lanes",
+                 "serial_search", "no_defer", "diag_exp")
+
+
+class Tuning(ctypes.Structure):
+    """include/mapf.h: mapf_tuning (launch forms; identical results whatever the values)."""
+    _fields_ = [(n, I32) for n in TUNING_FIELDS]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "mapf_last_error": (ctypes.c_char_p, []),
@@ -59,6 +70,10 @@ SIGNATURES = {
     "mapf_step_observe_random": (ctypes.c_int, [P, P, ctypes.POINTER(StepOut), P, P, P]),
     "mapf_rollout_random": (ctypes.c_int, [P, I32, I32, P, ctypes.POINTER(StepOut), P, P, P]),
     "mapf_rollout_random_fused": (ctypes.c_int, [P]),
+    "mapf_tuning_default": (None, [ctypes.POINTER(Tuning)]),
+    "mapf_get_tuning": (ctypes.c_int, [P, ctypes.POINTER(Tuning)]),
+    "mapf_set_tuning": (ctypes.c_int, [P, ctypes.POINTER(Tuning)]),
+    "mapf_rollout_plan": (ctypes.c_int, [P, I32, ctypes.c_char_p, I32]),
     "mapf_flush": (ctypes.c_int, [P, P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),

@@ -38,10 +38,25 @@ def _check(t, dtype, numel, device, name):
     return t
 
 
+def parse_tuning(text):
+    """ "roll_fair=2,wide_obs=1" -> {"roll_fair": 2, "wide_obs": 1} (mapf_tuning fields)."""
+    out = {}
+    for kv in (text or "").split(","):
+        if kv.strip():
+            k, v = kv.split("=")
+            out[k.strip()] = int(v)
+    return out
+
+
 class BatchedMapfGym:
     """B environments x N agents on one GPU (one handle per process/GPU)."""
 
-    def __init__(self, cfg: MapfConfig = None, device=None, **kw):
+    def __init__(self, cfg: MapfConfig = None, device=None, tuning=None, **kw):
+        """tuning: optional mapf_tuning fields (include/mapf.h) as a dict or a "k=v,k=v" string --
+        which form of a kernel the launches take; results are identical for every value
+        (see set_tuning)."""
+        if isinstance(tuning, str):
+            tuning = parse_tuning(tuning)
         if cfg is None:
             cfg = make_config(**kw)
         if not torch.cuda.is_available():
@@ -56,10 +71,10 @@ class BatchedMapfGym:
             _lib.check(_lib.lib().mapf_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
         self.h = h
         self.path_capacity = _lib.lib().mapf_path_capacity(self.h)
-        self.fused = bool(_lib.lib().mapf_step_observe_fused(self.h))   # step_observe = one launch
-        # rollout_random = one launch: 1 pair-lane kernel (c2), 2 one wave per env (c4, c5); 0 per-step launches
-        self.rollout_kernel = int(_lib.lib().mapf_rollout_random_fused(self.h))
-        self.rollout_fused = self.rollout_kernel != 0
+        if tuning:
+            self.set_tuning(**tuning)
+        else:
+            self._query_forms()
         dev = self.device
         B, N = self.B, self.N
         self.out = dict(
@@ -76,6 +91,49 @@ class BatchedMapfGym:
         self.obs = torch.zeros(B, N, self.C, self.F, self.F, dtype=torch.float32, device=dev)
         self.vec = torch.zeros(B, N, 4, dtype=torch.float32, device=dev)
         self.actions = torch.zeros(B, N, dtype=torch.int32, device=dev)
+
+    def _query_forms(self):
+        self.fused = bool(_lib.lib().mapf_step_observe_fused(self.h))   # step_observe = one launch
+        # rollout_random = one launch: 1 pair-lane kernel (c2), 2 one wave per env (c4, c5); 0 per-step launches
+        self.rollout_kernel = int(_lib.lib().mapf_rollout_random_fused(self.h))
+        self.rollout_fused = self.rollout_kernel != 0
+        self._roll_fast = None
+
+    @staticmethod
+    def default_tuning():
+        """mapf_tuning_default as a dict (include/mapf.h: mapf_tuning)."""
+        t = _lib.Tuning()
+        _lib.lib().mapf_tuning_default(ctypes.byref(t))
+        return {n: int(getattr(t, n)) for n in _lib.TUNING_FIELDS}
+
+    def tuning(self):
+        t = _lib.Tuning()
+        _lib.check(_lib.lib().mapf_get_tuning(self.h, ctypes.byref(t)))
+        return {n: int(getattr(t, n)) for n in _lib.TUNING_FIELDS}
+
+    def set_tuning(self, **fields):
+        """Change launch-form fields of mapf_tuning (unknown names raise, bad values raise
+        through the library's validation); the next launch takes the new form."""
+        t = _lib.Tuning()
+        _lib.check(_lib.lib().mapf_get_tuning(self.h, ctypes.byref(t)))
+        for k, v in fields.items():
+            if k not in _lib.TUNING_FIELDS:
+                raise KeyError(f"unknown tuning field {k!r}")
+            setattr(t, k, int(v))
+        _lib.check(_lib.lib().mapf_set_tuning(self.h, ctypes.byref(t)))
+        self._query_forms()
+
+    def rollout_plan(self, slots=False):
+        """The kernel (template instantiation + form) mapf_rollout_random launches now, as text."""
+        buf = ctypes.create_string_buffer(512)
+        kind = _lib.lib().mapf_rollout_plan(self.h, 1 if slots else 0, buf, 512)
+        if kind < 0:
+            _lib.check(kind)
+        return buf.value.decode()
+
+    def rollout_kernel_name(self, slots=False):
+        """The template instantiation alone, e.g. 'rollout_wide3_kernel<u64,1,false>'."""
+        return self.rollout_plan(slots).split(" ")[0]
 
     @staticmethod
     def _make_stepout(out):
@@ -246,7 +304,7 @@ class BatchedMapfGym:
             # built once -- a 20-step rollout takes ~300 us on the GPU, so the host's ~8 us of
             # argument checks and ctypes wrapping per call were 2-3 % of it
             key = (id(self.h), id(self.actions), id(self.obs), id(self.vec), id(self._stepout))
-            fast = getattr(self, "_roll_fast", None)
+            fast = self._roll_fast
             if fast is None or fast[0] != key:
                 fast = self._roll_fast = (key, _lib.lib().mapf_rollout_random, self.h, ctypes.byref(self._stepout),
                                           _ptr(self.actions), _ptr(self.obs), _ptr(self.vec))

@@ -11,6 +11,7 @@ import pytest
 import torch
 
 from golden_io import G1_NAMES, Fuzz, load, unpack_obs
+from kernel_registry import record_rollout_kernel
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -22,12 +23,12 @@ def need_gpu():
         pytest.fail("GPU tests need an MI355X")
 
 
-def mk_env(**kw):
+def mk_env(tuning=None, **kw):
     from mapf_amd.config import make_config
     from mapf_amd.env import BatchedMapfGym
     B = kw.pop("B")
     H, W = kw.pop("H"), kw.pop("W")
-    return BatchedMapfGym(make_config(B, H, W, **kw))
+    return BatchedMapfGym(make_config(B, H, W, **kw), tuning=tuning)
 
 
 def host(out):
@@ -278,30 +279,34 @@ def test_rollout_random_matches_oracle(name):
 
 GROUP_CASES = {
     "g_n8_20x20_f11": dict(B=64, H=20, W=20, n=8, fov=11, nch=6, steps=60, map="wh"),
+    "g_n8_20x20_f11_ragged61": dict(B=61, H=20, W=20, n=8, fov=11, nch=6, steps=60, map="wh"),
     "g_n6_16x16_f9_dahp_ragged": dict(B=45, H=16, W=16, n=6, fov=9, nch=6, steps=60, map="wh", da=1, hp=1),
 }
 
 
 @pytest.mark.parametrize("name,slack", [("g_n8_20x20_f11", 1), ("g_n8_20x20_f11", 0), ("g_n8_20x20_f11", -1),
-                                        ("g_n6_16x16_f9_dahp_ragged", 1), ("g_n6_16x16_f9_dahp_ragged", 3)])
-def test_rollout_random_cu_groups_match_oracle(name, slack, monkeypatch):
+                                        ("g_n6_16x16_f9_dahp_ragged", 1), ("g_n6_16x16_f9_dahp_ragged", 3),
+                                        ("g_n8_20x20_f11_ragged61", 1)])
+def test_rollout_random_cu_groups_match_oracle(name, slack):
     """The pair-lane rollout with all 16 waves of a CU in one workgroup (four 4-env quarters
     at their own LDS offsets, the waves paced within `slack` steps of the group's slowest;
-    ragged B: the envs past B never count) -- every slot bit-exact vs the oracle."""
-    monkeypatch.setenv("MAPF_ROLL_OCC", "4")
-    monkeypatch.setenv("MAPF_ROLL_GROUP", "1")
-    monkeypatch.setenv("MAPF_ROLL_SLACK", str(slack))
-    run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1)
+    ragged B -- 45: a short last quarter, 61: the last group's last quarter holds one env --
+    the envs past B never count) -- every slot bit-exact vs the oracle."""
+    run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1,
+                    tuning=dict(roll_occ=4, roll_group=1, roll_slack=slack), expect_name="rollout_random_kernel<true,4>")
 
 
-@pytest.mark.parametrize("name,fair", [("g_n8_20x20_f11", 4), ("g_n6_16x16_f9_dahp_ragged", 1)])
-def test_rollout_random_fair_priority_matches_oracle(name, fair, monkeypatch):
+@pytest.mark.parametrize("name,fair,path", [("g_n8_20x20_f11", 4, "rollout"), ("g_n6_16x16_f9_dahp_ragged", 1, "rollout"),
+                                            ("g_n8_20x20_f11", 4, "inplace1"), ("g_n8_20x20_f11", 4, "inplace"),
+                                            ("g_n8_20x20_f11_ragged61", 4, "inplace")])
+def test_rollout_random_fair_priority_matches_oracle(name, fair, path):
     """The pair-lane rollout with all 16 waves of a CU in one workgroup and issue priority by
     progress (a wave more than `fair` steps ahead of the group's slowest env drops to priority
-    0; ragged B: the envs past B never count) -- every slot bit-exact vs the oracle."""
-    monkeypatch.setenv("MAPF_ROLL_OCC", "4")
-    monkeypatch.setenv("MAPF_ROLL_FAIR", str(fair))
-    run_random_case(name, GROUP_CASES[name], "rollout", expect_rollout_kernel=1)
+    0; ragged B: the envs past B never count) -- slot buffers, and the in-place [B] buffers
+    (the form and plain stores c2's in-place rollout uses: rollout_random_kernel<false,4>) in
+    one-step launches and in 23-step launches -- bit-exact vs the oracle."""
+    run_random_case(name, GROUP_CASES[name], path, expect_rollout_kernel=1, tuning=dict(roll_occ=4, roll_fair=fair),
+                    expect_name="rollout_random_kernel<%s,4>" % ("true" if path == "rollout" else "false"))
 
 
 # the one-wave-per-env kernel's other search row layouts (u32 rows on two lane slots, u64 on
@@ -368,49 +373,58 @@ def test_rollout_on_fixed_episodes_equals_step_observe(name):
 
 @pytest.mark.parametrize("name,grid", [("c4_40x40_n16_f9_looping", 1), ("dense_12x12_n16_f9_dahp", 1),
                                        ("n7_24x24_f11_rand_dahp", 1), ("dense_12x12_n16_f9_dahp", 0)])
-def test_rollout_wide_one_wave_form_matches_oracle(name, grid, monkeypatch):
+def test_rollout_wide_one_wave_form_matches_oracle(name, grid):
     """The one-wave-per-env kernel in its unpipelined form (one wave steps and observes;
     the form c5 runs in) -- small configs otherwise run the two-wave pipelined form --
     with the step's neighbour grid over the scratch, and without it (the agent loop)."""
-    monkeypatch.setenv("MAPF_WIDE_PIPE", "0")
-    monkeypatch.setenv("MAPF_WIDE_GRID", str(grid))
     case = FUSED_CASES.get(name) or RANDOM_CASES[name]
-    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
+    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2), tuning=dict(wide_pipe=0, wide_grid=grid))
 
 
 @pytest.mark.parametrize("name,pipe,epw,pair,slack", [
     ("c4_40x40_n16_f9_looping", 1, 4, 0, 4), ("c4_40x40_n16_f9_looping", 1, 4, 1, 0),
     ("dense_12x12_n16_f9_dahp", 1, 2, 0, -1), ("dense_12x12_n16_f9_dahp", 0, 8, 0, 4),
     ("c5_80x80_n64_f11_bfsch", 0, 3, 0, 1), ("dense_12x12_n16_f9_dahp", 0, 4, 0, -3)])
-def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack, monkeypatch):
+def test_rollout_wide_env_groups_match_oracle(name, pipe, epw, pair, slack):
     """Several envs per workgroup (all the envs of a CU at full size), each at its own LDS
     offset, their pacing waves kept within `slack` steps of the group's slowest env: the
     same trajectories and observations as the oracle, in both wave-to-env orders."""
-    monkeypatch.setenv("MAPF_WIDE_PIPE", str(pipe))
-    monkeypatch.setenv("MAPF_WIDE_EPW", str(epw))
-    monkeypatch.setenv("MAPF_WIDE_PAIR", str(pair))
-    monkeypatch.setenv("MAPF_WIDE_SLACK", str(max(slack, -1)))
-    if slack < -1:      # issue priority by progress instead of waits (MAPF_WIDE_FAIR = -slack - 1)
-        monkeypatch.setenv("MAPF_WIDE_FAIR", str(-slack - 1))
+    tuning = dict(wide_pipe=pipe, wide_epw=epw, wide_pair=pair, wide_slack=max(slack, -1))
+    if slack < -1:      # issue priority by progress instead of waits (wide_fair = -slack - 1)
+        tuning["wide_fair"] = -slack - 1
     case = FUSED_CASES.get(name) or RANDOM_CASES[name]
-    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
+    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2), tuning=tuning)
 
 
 @pytest.mark.parametrize("name,nobs,bfsobs", [("c4_40x40_n16_f9_looping", 1, 1), ("dense_12x12_n16_f9_dahp", 1, 1),
                                               ("w_n12_70x30_f9", 1, 1), ("w_n10_96x60_f7_looping", 2, 1),
                                               ("dense_12x12_n16_f9_dahp", 2, 0), ("c4_40x40_n16_f9_looping", 2, 0)])
-def test_rollout_wide_observer_count_matches_oracle(name, nobs, bfsobs, monkeypatch):
-    """The overlapped two-wave form (MAPF_WIDE_OBS=1: one stepping, one observing wave) and the
+def test_rollout_wide_observer_count_matches_oracle(name, nobs, bfsobs):
+    """The overlapped two-wave form (wide_obs 1: one stepping, one observing wave) and the
     three-wave form (2: two observers taking alternate steps, the default where it fits), with
     the BFS maps searched by the observers (the default) or by the stepper -- every slot and
     the BFS maps bit-exact vs the oracle."""
-    monkeypatch.setenv("MAPF_WIDE_OBS", str(nobs))
-    monkeypatch.setenv("MAPF_WIDE_BFSOBS", str(bfsobs))
     case = FUSED_CASES.get(name) or RANDOM_CASES.get(name) or WIDE_SHAPES[name]
-    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2))
+    run_random_case(name, case, "rollout", expect_rollout_kernel=(1, 2), tuning=dict(wide_obs=nobs, wide_bfsobs=bfsobs))
 
 
-def run_random_case(name, case, path, expect_rollout_kernel=None):
+# In place: every step of a launch re-writes the same [B]-leading buffers (mapf_rollout_random
+# slots = 0) with plain stores where the buffer stays cache-resident -- the kernels the in-place
+# rollouts of c1 / c2 / c4 run (rollout_wide3_kernel<u32/u64,1,false>, rollout_random_kernel<false,*>),
+# which the slot-buffer cases above never launch (slot buffers force nontemporal stores).
+# "inplace1": one-step launches, every step compared; "inplace": 23-step launches, each launch's
+# last step compared (its buffers hold only that step), the oracle stepping through the others.
+@pytest.mark.parametrize("name,path", [("c4_40x40_n16_f9_looping", "inplace1"), ("c4_40x40_n16_f9_looping", "inplace"),
+                                       ("dense_12x12_n16_f9_dahp", "inplace1"), ("dense_12x12_n16_f9_dahp", "inplace"),
+                                       ("c1_10x10_n4_f11", "inplace1"), ("c1_10x10_n4_f11", "inplace"),
+                                       ("c5_80x80_n64_f11_bfsch", "inplace1"), ("w_n12_70x30_f9", "inplace"),
+                                       ("c2_20x20_n8_f11", "inplace1"), ("r_n6_16x16_f9_dahp", "inplace")])
+def test_rollout_in_place_matches_oracle(name, path):
+    case = FUSED_CASES.get(name) or ROLLOUT_CASES.get(name) or RANDOM_CASES.get(name) or WIDE_SHAPES[name]
+    run_random_case(name, case, path, expect_rollout_kernel=(1, 2))
+
+
+def run_random_case(name, case, path, expect_rollout_kernel=None, tuning=None, expect_name=None):
     B, H, W, n, fov, nch = case["B"], case["H"], case["W"], case["n"], case["fov"], case["nch"]
     rng = np.random.default_rng(5)
     maps, shared = build_maps(case, B, rng)
@@ -418,10 +432,15 @@ def run_random_case(name, case, path, expect_rollout_kernel=None):
     seed = 0x5EED0000 + len(name)
     env = mk_env(B=B, H=H, W=W, num_agents=n, fov=fov, num_channel=nch, use_da=case.get("da", 0),
                  use_hp=case.get("hp", 0), human_mode=human, goal_mode="random", fix_choice=1, shared_map=shared,
-                 seed=seed, env_offset=7)
+                 seed=seed, env_offset=7, tuning=tuning)
     env.reset_seeded(maps)
     if expect_rollout_kernel is not None:
         assert env.rollout_kernel in np.atleast_1d(expect_rollout_kernel), name
+    rolling = path in ("rollout", "inplace", "inplace1")
+    if rolling:
+        kname = env.rollout_kernel_name(slots=path == "rollout")
+        if expect_name is not None:
+            assert kname == expect_name, (name, env.rollout_plan(slots=path == "rollout"))
     hm = {"random": 1, "looping": 0}[human]
     cfg = O.make_config(H, W, n, fov, nch, use_da=case.get("da", 0), use_hp=case.get("hp", 0), human_mode=hm,
                         goal_mode=1, fix_choice=1, seed=seed, env_offset=7)
@@ -438,21 +457,25 @@ def run_random_case(name, case, path, expect_rollout_kernel=None):
         hp = oracles[b].human_path()
         np.testing.assert_array_equal(st["human_path"][b, :len(hp)], hp)
     checked_obs = 0
-    RT = 23                                   # rollout path: steps per mapf_rollout_random call
+    RT = 1 if path == "inplace1" else 23      # rollout paths: steps per mapf_rollout_random call
     roll = None
+    T = 0
     for t in range(case["steps"]):
-        if path == "rollout":
+        compare = True
+        if rolling:
             if t % RT == 0:
                 T = min(RT, case["steps"] - t)
-                roll = dict(actions=torch.zeros(T, B, n, dtype=torch.int32, device=env.device),
-                            obs=torch.full((T, B, n, nch, fov, fov), float("nan"), device=env.device),
-                            vec=torch.full((T, B, n, 4), float("nan"), device=env.device),
-                            out={k: torch.zeros((T,) + tuple(v.shape), dtype=v.dtype, device=env.device)
-                                 for k, v in env.out.items()})
-                env.rollout_random(T, slots=True, **roll)
+                k = T if path == "rollout" else 1          # in place: one [B]-leading set of buffers
+                roll = dict(actions=torch.full((k, B, n), -9, dtype=torch.int32, device=env.device),
+                            obs=torch.full((k, B, n, nch, fov, fov), float("nan"), device=env.device),
+                            vec=torch.full((k, B, n, 4), float("nan"), device=env.device),
+                            out={key: torch.full((k,) + tuple(v.shape), -7, dtype=v.dtype, device=env.device)
+                                 for key, v in env.out.items()})
+                env.rollout_random(T, slots=path == "rollout", **roll)
                 roll = dict(actions=roll["actions"].cpu().numpy(), obs=roll["obs"], vec=roll["vec"],
                             out=host(roll["out"]))
-            k = t % RT
+            k = t % RT if path == "rollout" else 0
+            compare = path == "rollout" or t % RT == T - 1
             a_host = roll["actions"][k]
             out = {key: v[k] for key, v in roll["out"].items()}
             obs, vec = roll["obs"][k], roll["vec"][k]
@@ -473,6 +496,10 @@ def run_random_case(name, case, path, expect_rollout_kernel=None):
             a_host = acts.cpu().numpy()
             out = host(env.step(acts))
             obs, vec = env.observe()
+        if not compare:                           # in place, inside a launch: the oracle steps on its own
+            for oe in oracles:
+                oe.step(oe.random_actions())
+            continue
         obs, vec = obs.cpu().numpy(), vec.cpu().numpy()
         for b in range(B):
             oe = oracles[b]
@@ -482,13 +509,13 @@ def run_random_case(name, case, path, expect_rollout_kernel=None):
                            ("actions_fixed", "fixed"), ("goals_reached", "goals"), ("constraints", "constr")]:
                 np.testing.assert_array_equal(out[k][b], o[key].astype(out[k].dtype), err_msg=f"{name} t={t} b={b} {k}")
             assert out["shadow_goals"][b] == o["shadow"]
-            if b % 4 == t % 4:
+            if b % 4 == t % 4 or path in ("inplace", "inplace1"):
                 oo, ov = oe.observe()
                 np.testing.assert_array_equal(obs[b], oo, err_msg=f"{name} t={t} b={b} obs")
                 np.testing.assert_array_equal(vec[b], ov, err_msg=f"{name} t={t} b={b} vec")
                 checked_obs += 1
-        # device state after the step (rollout path: only at the end of a call's T steps)
-        if (t % 20 == 19) if path != "rollout" else (t % RT == RT - 1 or t == case["steps"] - 1):
+        # device state after the step (rollout paths: only at the end of a call's T steps)
+        if (t % 20 == 19) if not rolling else (t % RT == T - 1):
             st = env.get_state()
             bfs = env.bfs().cpu().numpy()
             for b in range(B):
@@ -502,6 +529,8 @@ def run_random_case(name, case, path, expect_rollout_kernel=None):
     assert checked_obs > 0
     allow = case.get("allow", ())
     assert_no_errors(env, allow=allow)
+    if rolling:       # this instantiation is now oracle-compared (tests/test_gpu_ycoverage.py)
+        record_rollout_kernel(kname, f"{name} {path} vs oracle")
     if allow:   # the oracle counts the same events
         assert int(env.counters()[:8].sum()) == sum(oe.errors() for oe in oracles)
         fix = np.sum([oe.fix_counts() for oe in oracles], axis=0)
@@ -686,7 +715,8 @@ FULL_ROLLOUT = {"c2": (4096, 8, 20, 11, 6, True, 1, (1, 31, 45)),
                 "c5": (2048, 64, 80, 11, 7, False, 2, (1, 9, 23))}
 
 
-@pytest.mark.parametrize("cfg,slots", [("c2", True), ("c2", False), ("c4", True), ("c5", True), ("c5", False)])
+@pytest.mark.parametrize("cfg,slots", [("c2", True), ("c2", False), ("c4", True), ("c4", False), ("c5", True),
+                                       ("c5", False)])
 def test_full_size_rollout_equals_step_observe(cfg, slots):
     """c2 / c4 / c5 at full size: mapf_rollout_random (one launch of T steps) and T
     launches of mapf_step_observe_random on two envs with the same seed give identical
@@ -734,6 +764,8 @@ def test_full_size_rollout_equals_step_observe(cfg, slots):
     assert_no_errors(ro, allow=allow)
     assert_no_errors(so, allow=allow)
     assert (ro.counters()[:8] == so.counters()[:8]).all()
+    # equal to the per-step launches, which the oracle-compared cases pin
+    record_rollout_kernel(ro.rollout_kernel_name(slots), f"full-size {cfg} slots={slots} == step_observe")
 
 
 # --------------------------------------------------------------- GAE / normalise

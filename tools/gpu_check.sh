@@ -31,8 +31,8 @@ for s in $STEPS; do
       timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; stop_if_fatal $rc bench ;;
     sweep)
-      for cfg in ${SWEEP:-"MAPF_SEARCH_BLOCKS=32" "MAPF_SEARCH_BLOCKS=64" "MAPF_SEARCH_BLOCKS=128"}; do
-        env $cfg timeout -k 10 200 python3 bench.py --no-cpu --steps 2000 > "$OUT/sweep.log" 2>&1
+      for cfg in ${SWEEP:-"search_blocks=32" "search_blocks=64" "search_blocks=128"}; do
+        timeout -k 10 200 python3 bench.py --no-cpu --steps 2000 --path split --tune "$cfg" > "$OUT/sweep.log" 2>&1
         rc=$?; echo "sweep $cfg rc=$rc $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['breakdown_ms'])" "$OUT/sweep.log" 2>/dev/null)"
         stop_if_fatal $rc sweep
       done ;;

@@ -1,15 +1,14 @@
 #!/bin/bash
 # WRITE_SIZE / FETCH_SIZE passes (one rocprofv3 --pmc run per counter, kernel-trace only) of the
-# rollout kernels, 32-step launches:  PASSES="c2 c2slots c4 c5" bash tools/r3_pmc.sh
+# rollout kernels, 32-step launches:  PASSES="c2 c2inplace c4 c5" bash tools/pmc_passes.sh
 # -> gpurun_out/pmc_<pass>_<COUNTER>/ ; tools/pmc_report.py turns them into profiles/*.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
-for p in ${PASSES:-c2 c2slots c4 c5}; do
+# (bench.py's default rollout writes [T]-slot buffers; the *inplace passes re-write [B] buffers)
+for p in ${PASSES:-c2 c2inplace c4 c4inplace c5 c5inplace}; do
   case "$p" in
-    c2) args="--config c2" ;;
-    c2slots) args="--config c2 --slots" ;;
-    c4) args="--config c4" ;;
-    c5) args="--config c5" ;;
+    *inplace) args="--config ${p%inplace} --inplace" ;;
+    *) args="--config $p" ;;
   esac
   for ctr in WRITE_SIZE FETCH_SIZE; do
     rm -rf "$OUT/pmc_${p}_$ctr"

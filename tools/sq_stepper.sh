@@ -1,10 +1,10 @@
 #!/bin/bash
 # SQ counters of the c4 wide rollout kernel with the observation switched off (stamps build,
-# MAPF_WIDE_EXP=1): what the stepping wave's instructions are and where its cycles go.
+# TUNE=diag_exp=1): what the stepping wave's instructions are and where its cycles go.
 #   bash tools/sq_stepper.sh   (on the GPU box; writes gpurun_out/sq_stepper_*)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
-export CFG=${CFG:-c4} MAPF_WIDE_EXP=${MAPF_WIDE_EXP:-1}
+export CFG=${CFG:-c4} TUNE=${TUNE:-diag_exp=1}
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do

@@ -25,7 +25,7 @@ PHASES = ["loads+masks", "conflicts(j-loop)", "status+reward+outputs", "fixActio
 def main():
     B = int(os.environ.get("ENVS", "4096"))
     env = BatchedMapfGym(make_config(B, 20, 20, num_agents=8, fov=11, num_channel=6, human_mode="random",
-                                     goal_mode="random", fix_choice=1, seed=1234))
+                                     goal_mode="random", fix_choice=1, seed=1234), tuning=os.environ.get("TUNE", ""))
     env.reset_seeded(generate_warehouse(20, 20))
     split = os.environ.get("SPLIT", "0") == "1"     # default: the fused step+observe launch
     roll = os.environ.get("ROLLOUT", "0") == "1"    # the multi-step rollout launch (last step's phases)

@@ -26,7 +26,7 @@ p = bench.PRESETS[cfg]
 B, N, H, F, C = p["envs"], p["agents"], p["size"], p["fov"], p["channels"]
 world, shared = bench.make_maps(p["maps"], B, H, H, 0)
 env = BatchedMapfGym(make_config(B, H, H, num_agents=N, fov=F, num_channel=C, human_mode="random",
-                                 goal_mode="random", fix_choice=1, seed=1234, shared_map=shared))
+                                 goal_mode="random", fix_choice=1, seed=1234, shared_map=shared), tuning=os.environ.get("TUNE", ""))
 env.reset_seeded(world)
 assert env.rollout_kernel == 2, "not a wide-kernel config"
 env.rollout_random(16)

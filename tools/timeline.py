@@ -30,10 +30,11 @@ def q(x):
 
 def main():
     B = int(os.environ.get("ENVS", "4096"))
-    nsearch = int(os.environ.get("MAPF_SEARCH_BLOCKS", "64"))
-    nband = int(os.environ.get("MAPF_BAND_BLOCKS", "256"))
+    os.environ.setdefault("TUNE", "band_blocks=256")    # mapf_tuning fields (the zero band on by default here)
     env = BatchedMapfGym(make_config(B, 20, 20, num_agents=8, fov=11, num_channel=6, human_mode="random",
-                                     goal_mode="random", fix_choice=1, seed=1234))
+                                     goal_mode="random", fix_choice=1, seed=1234), tuning=os.environ.get("TUNE", ""))
+    tu = env.tuning()
+    nsearch, nband = tu["search_blocks"], tu["band_blocks"]
     env.reset_seeded(generate_warehouse(20, 20))
     for _ in range(60):
         env.step_observe(random_policy=True)
