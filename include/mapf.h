@@ -306,6 +306,26 @@ int mapf_normalize_advantages(const float *ret, const float *v, const float *cre
                               float *adv_out, float *cadv_out, int32_t M, double lagrange, int32_t mix,
                               void *stream);
 
+/* mapf_normalize_advantages over a minibatch split across ranks (model.py:106-113 on the GLOBAL
+ * minibatch).  Per rank, x = ret - v and c = cret - cv over its M rows, in fp64:
+ *   mapf_advantage_moments(mean = NULL): out[2] = {sum x, sum c}                -> all-reduce (sum)
+ *   mapf_advantage_moments(mean = {mean x, mean c}): out[2] = {sum (x - mean x)^2, sum (c - mean c)^2}
+ *                                                                            -> all-reduce (sum)
+ *   mapf_normalize_advantages_stats(stats = {mean x, mean c, var x, var c}, unbiased over all ranks'
+ *                                   rows): the normalisation of mapf_normalize_advantages.
+ * mean, out, stats: DEVICE double pointers; the other arrays DEVICE float [M]. */
+int mapf_advantage_moments(const float *ret, const float *v, const float *cret, const float *cv, int32_t M,
+                           const double *mean, double *out, void *stream);
+int mapf_normalize_advantages_stats(const float *ret, const float *v, const float *cret, const float *cv,
+                                    const double *stats, float *adv_out, float *cadv_out, int32_t M, double lagrange,
+                                    int32_t mix, void *stream);
+
+/* OneEpPerformance.episodeReward / episodeCostReward of every env (runner.py:95-96:
+ * `perf.episodeReward += np.sum(rewards)` once per step): x DEVICE float [T][B][N] (one
+ * rollout's rewards, goal reward included, or cost rewards); out DEVICE float [B] = the float32
+ * sum over t, in order, of numpy's float32 np.sum of x[t][b][0..N-1] (pairwise order; N <= 128). */
+int mapf_episode_sum(const float *x, int32_t T, int32_t B, int32_t N, float *out, void *stream);
+
 /* Model.step sampling (model.py:38-40): per row, inverse CDF of ps[M][5]
  * with a Philox uniform (key seed, counter (row, step)).  DEVICE. */
 int mapf_sample_actions(const float *ps, int32_t ps_stride, int32_t *actions, int64_t *actions64, int32_t M,

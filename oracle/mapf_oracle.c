@@ -959,6 +959,42 @@ void oc_gae(const float *r, const float *v, const float *v_last, float *adv, flo
     for (size_t k = 0; k < (size_t)T * M; ++k) { volatile float s = adv[k] + v[k]; ret[k] = s; }
 }
 
+/* ------------------------------------------------------------------ */
+/* OneEpPerformance.episodeReward / episodeCostReward (runner.py:95-96):
+ * `perf.episodeReward += np.sum(rewards)` once per step, rewards a float32
+ * [1, N] array.  np.sum = numpy's pairwise_sum over the N contiguous floats
+ * (below 8: in order from 0; else 8 strided accumulators combined
+ * ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the rest in order; N <= 128 is
+ * one block) added to the reduction's identity 0.  The python accumulator
+ * starts at int 0 and 0 + np.float32 is np.float32 (NEP 50): float32 over
+ * the steps.  x: T x B x N; out: B. */
+static float np_sum_f32(const float *a, int n) {
+    volatile float res;
+    if (n < 8) {
+        res = 0.f;
+        for (int i = 0; i < n; ++i) res = res + a[i];
+    } else {
+        volatile float r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
+        volatile float s01 = r[0] + r[1], s23 = r[2] + r[3], s45 = r[4] + r[5], s67 = r[6] + r[7];
+        volatile float lo = s01 + s23, hi = s45 + s67;
+        res = lo + hi;
+        for (; i < n; ++i) res = res + a[i];
+    }
+    volatile float z = 0.f + res;
+    return z;
+}
+void oc_episode_sum(const float *x, int T, int B, int N, float *out) {
+    for (int b = 0; b < B; ++b) {
+        volatile float acc = 0.f;
+        for (int t = 0; t < T; ++t) acc = acc + np_sum_f32(x + ((size_t)t * B + b) * N, N);
+        out[b] = acc;
+    }
+}
+
 /* Batched driver used as the CPU baseline: B independent envs, one lockstep
  * random-policy step + observe each (runner.py:64-100 order). Single thread. */
 typedef struct { oc_env **envs; int B; } oc_batch;

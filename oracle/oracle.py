@@ -83,6 +83,7 @@ def lib():
         L.oc_astar.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.oc_bfs_map.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.oc_gae.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.oc_episode_sum.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.oc_philox_word.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_uint64, ctypes.c_int]
         L.oc_philox_word.restype = ctypes.c_uint32
         L.oc_batch_create.restype = P
@@ -226,6 +227,15 @@ def gae(rewards, values, last_values, gamma=0.95, lam=0.95):
     adv = np.zeros_like(r); ret = np.zeros_like(r)
     lib().oc_gae(_p(r), _p(v), _p(lv), _p(adv), _p(ret), T, M, gamma, lam)
     return adv, ret
+
+
+def episode_sum(x):
+    """runner.py:95-96's per-env episodeReward: x [T, B, N] float32 -> [B] float32 (oc_episode_sum)."""
+    x = np.ascontiguousarray(x, np.float32)
+    T, B, N = x.shape
+    out = np.zeros(B, np.float32)
+    lib().oc_episode_sum(_p(x), T, B, N, _p(out))
+    return out
 
 
 def evict_order(pairs, restricted):

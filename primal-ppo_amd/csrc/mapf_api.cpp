@@ -931,6 +931,35 @@ int mapf_normalize_advantages(const float *ret, const float *v, const float *cre
     return MAPF_OK;
 }
 
+int mapf_advantage_moments(const float *ret, const float *v, const float *cret, const float *cv, int32_t M,
+                           const double *mean, double *out, void *stream) {
+    if (!ret || !v || !cret || !cv || !out) return fail(MAPF_EINVAL, "null argument");
+    if (M < 0) return fail(MAPF_EINVAL, "M must be >= 0");
+    launch_moments(ret, v, cret, cv, M, mean, out, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_normalize_advantages_stats(const float *ret, const float *v, const float *cret, const float *cv,
+                                    const double *stats, float *adv_out, float *cadv_out, int32_t M, double lagrange,
+                                    int32_t mix, void *stream) {
+    if (!ret || !v || !cret || !cv || !stats || !adv_out || !cadv_out) return fail(MAPF_EINVAL, "null argument");
+    if (M < 0) return fail(MAPF_EINVAL, "M must be >= 0");
+    if (M == 0) return MAPF_OK;
+    launch_normalize_stats(ret, v, cret, cv, stats, adv_out, cadv_out, M, (float)lagrange, (float)(lagrange + 1.0), mix,
+                           (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_episode_sum(const float *x, int32_t T, int32_t B, int32_t N, float *out, void *stream) {
+    if (!x || !out) return fail(MAPF_EINVAL, "null argument");
+    if (T < 0 || B < 1 || N < 1 || N > 128) return fail(MAPF_EINVAL, "need T >= 0, B >= 1, N in 1..128");
+    launch_episode_sum(x, T, B, N, out, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
 int mapf_sample_actions(const float *ps, int32_t ps_stride, int32_t *actions, int64_t *actions64, int32_t M,
                         uint64_t seed, uint32_t step, void *stream) {
     if (!ps || (!actions && !actions64)) return fail(MAPF_EINVAL, "null argument");

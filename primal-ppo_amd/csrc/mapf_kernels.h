@@ -167,6 +167,11 @@ void launch_gae(const float *r, const float *v, const float *vl, float *adv, flo
                 float gl, hipStream_t s);
 void launch_normalize(const float *ret, const float *v, const float *cret, const float *cv, float *adv,
                       float *cadv, int M, float lam, float lam1, int mix, hipStream_t s);
+void launch_moments(const float *ret, const float *v, const float *cret, const float *cv, int M, const double *mean,
+                    double *out, hipStream_t s);
+void launch_normalize_stats(const float *ret, const float *v, const float *cret, const float *cv, const double *stats,
+                            float *adv, float *cadv, int M, float lam, float lam1, int mix, hipStream_t s);
+void launch_episode_sum(const float *x, int T, int B, int N, float *out, hipStream_t s);
 void launch_sample(const float *ps, int stride, int32_t *a32, int64_t *a64, int M, uint64_t seed, uint32_t step,
                    hipStream_t s);
 

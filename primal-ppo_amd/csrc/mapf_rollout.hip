@@ -10,6 +10,12 @@
 //                    adv = (adv - lam * cadv) / (lam + 1).  Sums in f64.
 //  sample_kernel     Model.step (model.py:38-40): np.random.choice(5, p) as an
 //                    inverse CDF with a Philox uniform.
+//  moments_kernel /  the same statistics over a minibatch split across ranks: sums (then
+//  normalize_stats_  sums of squares about the global mean) to be all-reduced, then the
+//  kernel            normalisation with the global mean and unbiased variance.
+//  episode_sum_kernel  OneEpPerformance.episodeReward / episodeCostReward (runner.py:95-96):
+//                    each step's np.sum of the env's N float32 values (numpy's pairwise
+//                    order), accumulated in float32 over the T steps.
 #include "mapf_common.h"
 #include "mapf_kernels.h"
 
@@ -96,6 +102,92 @@ __global__ __launch_bounds__(256) void sample_kernel(const float *__restrict__ p
         if (u < cdf[a]) pick = a;                 // searchsorted(cdf, u, side='right')
     if (a32) a32[m] = pick;
     if (a64) a64[m] = pick;
+}
+
+// Two-pass moments of x = ret - v and c = cret - cv over this rank's M rows, in fp64:
+// mean == nullptr: out = {sum x, sum c}; else out = {sum (x - mean[0])^2, sum (c - mean[1])^2}.
+__global__ __launch_bounds__(1024) void moments_kernel(const float *__restrict__ ret, const float *__restrict__ v,
+                                                       const float *__restrict__ cret, const float *__restrict__ cv,
+                                                       int M, const double *__restrict__ mean, double *__restrict__ out) {
+    __shared__ double sh[16];
+    const double m0 = mean ? mean[0] : 0.0, m1 = mean ? mean[1] : 0.0;
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = threadIdx.x; k < M; k += blockDim.x) {
+        const double a = (double)__fsub_rn(ret[k], v[k]) - m0, c = (double)__fsub_rn(cret[k], cv[k]) - m1;
+        s0 += mean ? a * a : a;
+        s1 += mean ? c * c : c;
+    }
+    s0 = block_sum(s0, sh);
+    s1 = block_sum(s1, sh);
+    if (threadIdx.x == 0) { out[0] = s0; out[1] = s1; }
+}
+
+// stats = {mean x, mean c, unbiased var x, unbiased var c} (global, fp64) -> the normalisation of
+// normalize_kernel with those statistics
+__global__ __launch_bounds__(256) void normalize_stats_kernel(const float *__restrict__ ret, const float *__restrict__ v,
+                                                              const float *__restrict__ cret,
+                                                              const float *__restrict__ cv,
+                                                              const double *__restrict__ stats, float *__restrict__ adv,
+                                                              float *__restrict__ cadv, int M, float lam, float lam1,
+                                                              int mix) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= M) return;
+    const float mean0 = (float)stats[0], mean1 = (float)stats[1];
+    const float den0 = __fadd_rn((float)sqrt(stats[2]), 1e-6f), den1 = __fadd_rn((float)sqrt(stats[3]), 1e-6f);
+    float a = __fdiv_rn(__fsub_rn(__fsub_rn(ret[k], v[k]), mean0), den0);
+    const float c = __fdiv_rn(__fsub_rn(__fsub_rn(cret[k], cv[k]), mean1), den1);
+    if (mix) a = __fdiv_rn(__fsub_rn(a, __fmul_rn(lam, c)), lam1);
+    adv[k] = a;
+    cadv[k] = c;
+}
+
+// np.sum over a float32 [1, N] array (numpy's pairwise_sum, N <= 128: sequential below 8
+// elements, else 8 strided accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the
+// remainder in order; the reduction's identity 0 added first)
+__device__ inline float np_sum_f32(const float *a, int n) {
+    float res;
+    if (n < 8) {
+        res = 0.f;
+        for (int i = 0; i < n; ++i) res = __fadd_rn(res, a[i]);
+    } else {
+        float r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int i = 8;
+        for (; i < n - (n % 8); i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], a[i + j]);
+        res = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                        __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+        for (; i < n; ++i) res = __fadd_rn(res, a[i]);
+    }
+    return __fadd_rn(0.f, res);
+}
+
+// x [T][B][N]: out[b] = sum over t (float32, in order) of np_sum_f32(x[t][b][:]) -- the python
+// accumulator starts at int 0, and 0 + np.float32 stays np.float32 (NEP 50)
+__global__ __launch_bounds__(256) void episode_sum_kernel(const float *__restrict__ x, int T, int B, int N,
+                                                          float *__restrict__ out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) acc = __fadd_rn(acc, np_sum_f32(x + ((size_t)t * B + b) * N, N));
+    out[b] = acc;
+}
+
+void launch_moments(const float *ret, const float *v, const float *cret, const float *cv, int M, const double *mean,
+                    double *out, hipStream_t s) {
+    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(1024), 0, s, ret, v, cret, cv, M, mean, out);
+}
+
+void launch_normalize_stats(const float *ret, const float *v, const float *cret, const float *cv, const double *stats,
+                            float *adv, float *cadv, int M, float lam, float lam1, int mix, hipStream_t s) {
+    hipLaunchKernelGGL(normalize_stats_kernel, dim3((M + 255) / 256), dim3(256), 0, s, ret, v, cret, cv, stats, adv,
+                       cadv, M, lam, lam1, mix);
+}
+
+void launch_episode_sum(const float *x, int T, int B, int N, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(episode_sum_kernel, dim3((B + 255) / 256), dim3(256), 0, s, x, T, B, N, out);
 }
 
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,

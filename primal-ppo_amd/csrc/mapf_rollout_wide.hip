@@ -315,6 +315,8 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
     // t's maps are written after step t - 1's (ctr[3]: steps whose maps are done), so an agent's
     // later map wins; an observer that searched drains its stores before it counts.
     const bool bfs_obs = ovl && nobs >= 2 && observing && ro.bfsobs;
+    // several observers writing the same in-place buffers, in alternation
+    const bool inplace_multi = ovl && nobs >= 2 && observing && !ro.slots;
     WSTAMP_BEGIN();
     for (int t = 0; t < T_steps; ++t) {
         const size_t s = ro.slots ? (size_t)t : 0;
@@ -384,6 +386,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
                 bm = (uint64_t)lds_count(w) | ((uint64_t)lds_count(w + 1) << 32);
                 mygoal = Lt.sgoal[min(lane, e.N - 1)];
             }
+            // in place with several observers, the [B] buffer's last writer must be step T - 1's:
+            // each observer's last observation drains (vmcnt(0)) before it counts, and the final
+            // step's observer re-writes its observation once the others have (after the loop)
+            if (inplace_multi && t + nobs >= T_steps) __builtin_amdgcn_s_waitcnt(0x0F70);
             if (ovl) publish_count(ctr + 1 + obs_o, (uint32_t)(t / nobs + 1));   // ... and observed
             if (pacing || fairw) publish_count(prog + k, (uint32_t)(t + 1));
             if (bfs_obs) {
@@ -399,6 +405,23 @@ __device__ __attribute__((always_inline)) inline void rollout_wide_body(const De
             }
         }
         WSTAMP(3);
+    }
+    // In place, observers take alternate steps into the same [B] buffers, so step T - 2's stores
+    // (another wave's) may land after step T - 1's: once every other observer's last observation
+    // has drained, step T - 1's observer writes its observation again (its snapshot is still in the
+    // ring: the stepper has stopped) -- one extra observation per env per launch
+    if (inplace_multi && observer && T_steps >= 2 && (T_steps - 1) % nobs == obs_o) {
+        for (int o2 = 0; o2 < nobs; ++o2)
+            if (o2 != obs_o) wide_wait_ge(ctr + 1 + o2, (uint32_t)((T_steps - o2 + nobs - 1) / nobs));
+        const ObsLds Lt = snap_of(T_steps - 1);
+        for (int k = lane; k < L.swe + L.rowsz; k += 64) L.stream[k] = 0u;
+        wide_sync();
+#ifdef MAPF_STAMPS
+        const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true, ro.exp};
+#else
+        const ObsGroup G{lane, 64, 0, 1, L.stream, L.mapc, true};
+#endif
+        obs_emit<true, NT>(e, Lt, ro.obs, ro.vec, G, b, false);
     }
     if (stepper) step_regs_store(e, b, lane, rs);
     WSTAMP_END(b, role);

@@ -87,6 +87,9 @@ SIGNATURES = {
     "mapf_gae": (ctypes.c_int, [P, P, P, P, P, I32, I32, ctypes.c_double, ctypes.c_double, P]),
     "mapf_normalize_advantages": (ctypes.c_int, [P, P, P, P, P, P, I32, ctypes.c_double, I32, P]),
     "mapf_sample_actions": (ctypes.c_int, [P, I32, P, P, I32, ctypes.c_uint64, U32, P]),
+    "mapf_advantage_moments": (ctypes.c_int, [P, P, P, P, I32, P, P, P]),
+    "mapf_normalize_advantages_stats": (ctypes.c_int, [P, P, P, P, P, P, P, I32, ctypes.c_double, I32, P]),
+    "mapf_episode_sum": (ctypes.c_int, [P, I32, I32, I32, P, P]),
     # policy acting forward epilogues (csrc/mapf_policy.hip)
     "mapf_nhwc_bias_relu": (ctypes.c_int, [P, P, I64, I32, P]),
     "mapf_nhwc_bias_relu_pool2": (ctypes.c_int, [P, P, P, I32, I32, I32, I32, P]),

@@ -446,6 +446,47 @@ def normalize_advantages(returns, values, cost_returns, cost_values, lagrange=0.
     return adv, cadv
 
 
+def normalize_advantages_distributed(returns, values, cost_returns, cost_values, lagrange=0.0, mix=False, group=None):
+    """normalize_advantages over a minibatch split across the ranks of torch.distributed: this
+    rank's rows in, this rank's rows out, normalised with the GLOBAL mean and unbiased std
+    (model.py:106-113 on the whole minibatch).  Two-pass fp64 moments on the device
+    (mapf_advantage_moments), each pass all-reduced (2 small all-reduces), then
+    mapf_normalize_advantages_stats."""
+    import torch.distributed as dist
+    dev, M = returns.device, returns.numel()
+    if dev.type != "cuda":
+        raise ValueError("normalize_advantages_distributed: tensors must be on the GPU")
+    for name, t in (("returns", returns), ("values", values), ("cost_returns", cost_returns),
+                    ("cost_values", cost_values)):
+        _check(t, torch.float32, M, dev, name)
+    st, L = _stream(dev), _lib.lib()
+    ptrs = [_ptr(t) for t in (returns, values, cost_returns, cost_values)]
+    buf = torch.zeros(3, dtype=torch.float64, device=dev)          # sum x, sum c, rows
+    buf[2] = M
+    _lib.check(L.mapf_advantage_moments(*ptrs, M, None, _ptr(buf), st))
+    dist.all_reduce(buf, group=group)
+    mean = (buf[:2] / buf[2]).contiguous()
+    q = torch.zeros(2, dtype=torch.float64, device=dev)
+    _lib.check(L.mapf_advantage_moments(*ptrs, M, _ptr(mean), _ptr(q), st))
+    dist.all_reduce(q, group=group)
+    stats = torch.cat([mean, q / (buf[2] - 1).clamp_min(1)]).contiguous()
+    adv = torch.empty_like(returns)
+    cadv = torch.empty_like(returns)
+    _lib.check(L.mapf_normalize_advantages_stats(*ptrs, _ptr(stats), _ptr(adv), _ptr(cadv), M, float(lagrange),
+                                                 int(mix), st))
+    return adv, cadv
+
+
+def episode_sum(x):
+    """OneEpPerformance.episodeReward-style sums (runner.py:95-96) of every env: x [T, B, N] float32
+    on the GPU -> [B] float32, each step's numpy float32 np.sum over N accumulated in float32."""
+    T, B, N = x.shape
+    _check(x, torch.float32, T * B * N, x.device, "x")
+    out = torch.empty(B, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().mapf_episode_sum(_ptr(x), T, B, N, _ptr(out), _stream(x.device)))
+    return out
+
+
 def sample_actions(ps, seed, step, out32=None, out64=None):
     """model.py:38-40 on device: ps [..., 5] float32 -> actions."""
     ps2 = ps.reshape(-1, ps.shape[-1])

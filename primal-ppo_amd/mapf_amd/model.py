@@ -4,8 +4,9 @@ Mirrors the reference's Model (model.py:13-231) and Lagrangian multipliers
 (lagrange.py:26-88), with the device-resident pieces of the hot path:
   * step(): the policy forward + on-device categorical sampling (mapf_sample_actions
     in place of np.random.choice, model.py:38-40);
-  * train(): advantage normalisation by the HIP kernel (mapf_normalize_advantages,
-    model.py:106-113) -- statistics over the GLOBAL minibatch when distributed --
+  * train(): advantage normalisation by the HIP kernels (mapf_normalize_advantages,
+    model.py:106-113) -- statistics over the GLOBAL minibatch when distributed (two-pass
+    fp64 moments all-reduced, mapf_normalize_advantages_stats) --
     then the reference's loss (:115-170), AMP GradScaler, and between backward and
     unscale the RCCL all-reduce of the flattened gradient bucket (SURVEY.md §3.4:
     the only exchange step of the path).
@@ -211,12 +212,13 @@ class Model:
 
         lam = self.lagrange.get_lagrangian_param()
         distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        if dev.type == "cuda" and not distributed:
-            from .env import normalize_advantages
-            advantage, cost_advantage = normalize_advantages(returns.contiguous(), old_v.contiguous(),
-                                                             cost_returns.contiguous(), old_cv.contiguous(),
-                                                             lagrange=lam, mix=TrainingParameters.MINUS_ADV_WITH_CADV)
-        else:
+        if dev.type == "cuda":
+            # the HIP normalisation; distributed: global two-pass moments all-reduced into it
+            from .env import normalize_advantages, normalize_advantages_distributed
+            fn = normalize_advantages_distributed if distributed else normalize_advantages
+            advantage, cost_advantage = fn(returns.contiguous(), old_v.contiguous(), cost_returns.contiguous(),
+                                           old_cv.contiguous(), lagrange=lam, mix=TrainingParameters.MINUS_ADV_WITH_CADV)
+        else:                   # CPU (the gloo tests' host path): torch, global statistics when distributed
             advantage = _normalize(returns - old_v)
             cost_advantage = _normalize(cost_returns - old_cv)
             if TrainingParameters.MINUS_ADV_WITH_CADV:

@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from .config import EnvParameters, NetParameters, TrainingParameters
-from .env import BatchedMapfGym, gae
+from .env import BatchedMapfGym, episode_sum, gae
 
 
 class DeviceMaps:
@@ -367,9 +367,10 @@ class DeviceRunner:
         per = {
             "staticCollide": (st == -1).sum(dim=(0, 2)), "humanCollide": (st == -2).sum(dim=(0, 2)),
             "agentCollide": (st == -3).sum(dim=(0, 2)), "shadowGoals": self.shadow.sum(dim=0),
-            # np.sum over float32 rewards per step, accumulated in a python float (runner.py:95-98)
-            "episodeReward": self.rewards.sum(dim=2).double().sum(dim=0),
-            "episodeCostReward": self.cost_rewards.sum(dim=2).double().sum(dim=0),
+            # np.sum over each step's float32 rewards (pairwise order), accumulated from the python
+            # int 0 -- which stays np.float32 (NEP 50): float32 over the steps (runner.py:95-96)
+            "episodeReward": episode_sum(self.rewards),
+            "episodeCostReward": episode_sum(self.cost_rewards),
             "totalGoals": self.goals.sum(dim=(0, 2)), "constraintViolations": self.constraints.sum(dim=(0, 2))}
         return {k: v.double().cpu().numpy() for k, v in per.items()}
 

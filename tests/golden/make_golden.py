@@ -135,8 +135,13 @@ def greedy_actions(rng, env, n, p_greedy):
     return acts
 
 
+PERF = {}        # g1 episode -> the reference's OneEpPerformance counters after every step (g1_perf.npz)
+PERF_FIELDS = ["staticCollide", "humanCollide", "agentCollide", "shadowGoals", "episodeReward", "episodeCostReward",
+               "totalGoals", "constraintViolations"]
+
+
 def run_episode(name, world, n, fov, nch, steps, seed, use_da=False, use_hp=False,
-                human_seq=None, n_goals=60, p_greedy=0.6):
+                human_seq=None, n_goals=60, p_greedy=0.6, save=True):
     set_params(n, fov)
     rng = np.random.default_rng(seed)
     free = free_cells(world)
@@ -175,6 +180,12 @@ def run_episode(name, world, n, fov, nch, steps, seed, use_da=False, use_hp=Fals
         hpath0=np.array(env.human.path), obs0=np.packbits(obs0.astype(np.uint8)), vec0=vec0,
         bfs0=np.array([a.bfsMap for a in env.agentList]).astype(np.int16))
     choice0 = CHOICE_HITS[0]
+    # runner.py:66-99's counter loop, statement for statement, with the reference's own class
+    # (util.OneEpPerformance) over this episode's steps; a copy of the rewards takes the
+    # GOAL_REWARD additions (rec keeps calculateActionReward's values)
+    oneEpisodePerformance = util.OneEpPerformance()
+    perf_log = {k: [] for k in PERF_FIELDS}
+    perf_types = {}
     for t in range(steps):
         actions = greedy_actions(rng, env, n, p_greedy)
         pos_before = np.array([a.getPos() for a in env.agentList])
@@ -190,6 +201,27 @@ def run_episode(name, world, n, fov, nch, steps, seed, use_da=False, use_hp=Fals
         for i in range(n):
             d = mg.Agent.dirDict[int(fixed[i])]
             assert tuple(pos_before[i] + np.array(d)) == tuple(pos_after[i])
+        actionStatus, rewards, shadowGoals, costRewards = st, rw.copy(), sh, cost
+        goalsReached, constraintsViolated = goals, constr
+        for value in actionStatus:
+            if value == -1:
+                oneEpisodePerformance.staticCollide += 1
+            elif value == -2:
+                oneEpisodePerformance.humanCollide += 1
+            elif value == -3:
+                oneEpisodePerformance.agentCollide += 1
+        oneEpisodePerformance.shadowGoals += shadowGoals
+        for i, value in enumerate(goalsReached):
+            if (value == 1):
+                rewards[0, i] += alg.EnvParameters.GOAL_REWARD
+        oneEpisodePerformance.episodeReward += np.sum(rewards)
+        oneEpisodePerformance.episodeCostReward += np.sum(costRewards)
+        oneEpisodePerformance.totalGoals += np.sum(goalsReached)
+        oneEpisodePerformance.constraintViolations += np.sum(constraintsViolated)
+        for k in PERF_FIELDS:
+            v = getattr(oneEpisodePerformance, k)
+            perf_log[k].append(float(v))
+            perf_types[k] = type(v).__name__
         obs, vec = env.getAllObservations()
         rec["actions"].append(actions.astype(np.int64)); rec["status"].append(st.astype(np.int8))
         rec["reward"].append(rw[0]); rec["shadow"].append(sh); rec["cost"].append(cost[0])
@@ -211,6 +243,13 @@ def run_episode(name, world, n, fov, nch, steps, seed, use_da=False, use_hp=Fals
                     human_mode=0 if human_seq is None else 2, bfs_final=final_bfs,
                     hseq=np.array(hseq_in if hseq_in is not None else [hs]), steps=steps,
                     choice_hits=CHOICE_HITS[0] - choice0))
+    PERF[name] = {k: np.array(v, np.float64) for k, v in perf_log.items()}
+    PERF[name]["types"] = np.array([perf_types[k] for k in PERF_FIELDS])
+    if not save:    # g1perf: the episode must be the committed one
+        old = np.load(os.path.join(OUT, f"{name}.npz"))
+        for k in ("actions", "status", "reward", "shadow", "cost", "goals", "constr", "pos"):
+            assert np.array_equal(old[k], out[k]), (name, k)
+        return
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
     nfix_total = sum(1 for s in out["status"] if np.any((s < 0) & (s > -4)))
     print(f"{name}: steps={steps} goals={out['goals'].sum():.0f} fixsteps={nfix_total} "
@@ -582,7 +621,26 @@ def g8_render():
     print("g8_render:", {k: v.shape for k, v in out.items() if not k.startswith("colors")})
 
 
+def g1_episodes(save=True):
+    run_episode("g1_c1", warehouse(10, 10), 4, 11, 6, 200, 11, save=save)
+    run_episode("g1_c2", warehouse(20, 20), 8, 11, 6, 200, 12, save=save)
+    run_episode("g1_f9", warehouse(20, 20), 8, 9, 6, 200, 13, save=save)
+    run_episode("g1_dahp", warehouse(20, 20), 8, 9, 6, 150, 14, use_da=True, use_hp=True, save=save)
+    np.random.seed(5)
+    run_episode("g1_randwh", mapgen.generateWarehouse(num_block=[10, 16]), 6, 9, 5, 150, 15, save=save)
+    run_episode("g1_dense", warehouse(10, 10), 16, 9, 6, 200, 16, p_greedy=0.3, save=save)
+    run_episode("g1_fixedpath", warehouse(12, 12), 6, 9, 6, 150, 17, human_seq=12, use_da=True, use_hp=True,
+                save=save)
+    out = {f"{name}__{k}": v for name, d in PERF.items() for k, v in d.items()}
+    out["fields"] = np.array(PERF_FIELDS)
+    np.savez_compressed(os.path.join(OUT, "g1_perf.npz"), **out)
+    print("g1_perf:", {name: {k: d[k][-1] for k in PERF_FIELDS} for name, d in PERF.items()})
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["g1perf"]:     # the reference's counter loop over the committed g1 episodes only
+        g1_episodes(save=False)
+        sys.exit(0)
     if sys.argv[1:] == ["g8"]:
         g8_render()
         sys.exit(0)
@@ -601,14 +659,7 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["g5"]:
         g5_net()
         sys.exit(0)
-    run_episode("g1_c1", warehouse(10, 10), 4, 11, 6, 200, 11)
-    run_episode("g1_c2", warehouse(20, 20), 8, 11, 6, 200, 12)
-    run_episode("g1_f9", warehouse(20, 20), 8, 9, 6, 200, 13)
-    run_episode("g1_dahp", warehouse(20, 20), 8, 9, 6, 150, 14, use_da=True, use_hp=True)
-    np.random.seed(5)
-    run_episode("g1_randwh", mapgen.generateWarehouse(num_block=[10, 16]), 6, 9, 5, 150, 15)
-    run_episode("g1_dense", warehouse(10, 10), 16, 9, 6, 200, 16, p_greedy=0.3)
-    run_episode("g1_fixedpath", warehouse(12, 12), 6, 9, 6, 150, 17, human_seq=12, use_da=True, use_hp=True)
+    g1_episodes()
     g2_fuzz(3000, 21)
     g2_evict()
     g7_warehouses()

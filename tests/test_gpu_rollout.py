@@ -248,3 +248,127 @@ def test_driver_block_verbatim_over_device_runners_c3(n_runners):
         assert torch.equal(got[0], r1.obs[0, 0]) and torch.equal(got[1], r1.obs[7, 0])
         assert torch.equal(got[2], r1.obs[T - 1, B - 1])
     assert all(np.isfinite(float(np.asarray(s))) for k, s in enumerate(losses[-1]) if k != 8)
+
+
+class _ScriptedModel:
+    """Model.step / Model.value stand-in that plays a g1 episode's scripted actions (the
+    reference's recorded actions) into DeviceRunner's buffers: the runner's counter loop then
+    sees exactly the reference episode."""
+
+    def __init__(self, actions, B):
+        self.actions = torch.from_numpy(np.ascontiguousarray(actions)).cuda()    # [T, N]
+        self.B = B
+
+    def step(self, obs, vec, hidden, seed=0, step=0, actions_out=None, actions32_out=None):
+        t = step % self.actions.shape[0]
+        a = self.actions[t].unsqueeze(0).expand(self.B, -1)
+        actions_out.copy_(a)
+        actions32_out.copy_(a)
+        z = torch.zeros(self.B, a.shape[1], 1, device="cuda")
+        return actions_out, torch.full((self.B, a.shape[1], 5), 0.2, device="cuda"), z, None, None, z
+
+    def value(self, obs, vec, hidden):
+        z = torch.zeros(self.B, self.actions.shape[1], 1, device="cuda")
+        return z, z
+
+
+@pytest.mark.parametrize("name", ["g1_c1", "g1_c2", "g1_dahp", "g1_dense", "g1_fixedpath"])
+def test_device_runner_performance_matches_reference(name):
+    """OneEpPerformance (runner.py:66-99) of DeviceRunner over a reference episode (g1, replayed
+    with its scripted actions on B replicas) == the reference's own counter loop over the same
+    episode (g1_perf, util.OneEpPerformance), every env, every counter bit for bit -- the float32
+    episodeReward / episodeCostReward accumulation included (episodeCostReward feeds the
+    Lagrangian, model.py:180)."""
+    from mapf_amd.config import make_config
+    from mapf_amd.env import BatchedMapfGym
+    from mapf_amd.runner import PERF_FIELDS, DeviceRunner
+    z = load(name)
+    perf = load("g1_perf")
+    n, fov, nch = int(z["n"]), int(z["fov"]), int(z["nch"])
+    world = z["map"]
+    H, W = world.shape
+    hmode = int(z["human_mode"])
+    B, T = 5, int(z["steps"])
+    env = BatchedMapfGym(make_config(B, H, W, num_agents=n, fov=fov, num_channel=nch, use_da=int(z["use_da"]),
+                                     use_hp=int(z["use_hp"]), human_mode=hmode, goal_mode="sequence", fix_choice=0,
+                                     max_seq=z["seq"].shape[1], max_human_seq=max(2, len(z["hseq"]))))
+    seqs = [z["seq"][i, :z["seq_len"][i]] for i in range(n)]
+    if hmode == 2:
+        env.reset_fixed(world, [seqs] * B, human_seq=[z["hseq"]] * B)
+    else:
+        env.reset_fixed(world, [seqs] * B, [z["hstart"]] * B, [z["hgoal"]] * B)
+    runner = DeviceRunner(env, _ScriptedModel(z["actions"], B), n_steps=T)
+    _, p = runner.run()
+    per_env = runner.performance_per_env()
+    np.testing.assert_array_equal(runner.status.cpu().numpy()[:, 0], z["status"])   # the reference episode
+    for k in PERF_FIELDS:
+        want = perf[f"{name}__{k}"][T - 1]
+        np.testing.assert_array_equal(per_env[k], np.full(B, want), err_msg=k)
+        assert getattr(p, k) == want, k
+    assert per_env["episodeReward"].dtype == np.float64
+
+
+def test_episode_sum_matches_oracle():
+    from mapf_amd.env import episode_sum
+    g = np.random.default_rng(9)
+    vals = np.array([-0.3, -0.5, -1.0, 0.0, 1.5, -0.25, 1.2, -0.02], np.float32)
+    for N in (1, 4, 7, 8, 9, 16, 17, 64):
+        x = np.where(g.random((256, 33, N)) < 0.5, g.choice(vals, (256, 33, N)),
+                     g.normal(size=(256, 33, N))).astype(np.float32)
+        got = episode_sum(torch.from_numpy(x).cuda()).cpu().numpy()
+        np.testing.assert_array_equal(got, O.episode_sum(x), err_msg=f"N={N}")
+
+
+def _norm_worker(rank, world, port, x, y, lam, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path[:0] = [root, os.path.join(root, "primal-ppo_amd")]
+        from mapf_amd.env import normalize_advantages_distributed
+        torch.cuda.set_device(0)
+        sl = slice(rank * len(x) // world, (rank + 1) * len(x) // world)
+        xt, yt = torch.from_numpy(x[sl]).cuda(), torch.from_numpy(y[sl]).cuda()
+        zero = torch.zeros_like(xt)
+        adv, cadv = normalize_advantages_distributed(xt, zero, yt, zero, lagrange=lam, mix=True)
+        q.put((rank, adv.cpu().numpy(), cadv.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_normalize_distributed_two_ranks_equal_one_process():
+    """two ranks (gloo, both on this GPU) each holding half of a minibatch,
+    normalised by the HIP path with all-reduced two-pass moments (mapf_advantage_moments,
+    mapf_normalize_advantages_stats), give the one-process HIP normalisation of the whole
+    minibatch within 1e-5 -- the product path Model.train takes when distributed."""
+    import socket
+    import torch.multiprocessing as mp
+    from mapf_amd.env import normalize_advantages
+    z = load("g4_gae")
+    x, y = z["norm_x"].reshape(-1), z["norm_y"].reshape(-1)
+    lam = float(z["norm_lam"])
+    xt, yt = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    zero = torch.zeros_like(xt)
+    adv1, cadv1 = normalize_advantages(xt, zero, yt, zero, lagrange=lam, mix=True)
+    np.testing.assert_allclose(adv1.cpu().numpy(), z["norm_mixed"].reshape(-1), rtol=1e-5, atol=1e-5)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_norm_worker, args=(r, 2, port, x, y, lam, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    adv2 = np.concatenate([r[1] for r in res])
+    cadv2 = np.concatenate([r[2] for r in res])
+    np.testing.assert_allclose(adv2, adv1.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(cadv2, cadv1.cpu().numpy(), rtol=1e-5, atol=1e-6)

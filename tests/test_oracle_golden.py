@@ -159,3 +159,59 @@ def test_random_policy_stream_is_uniform():
     assert acts.min() >= 0 and acts.max() <= 4
     np.testing.assert_allclose(freq, 0.2, atol=0.015)
     assert not np.array_equal(acts[:, 0], acts[:, 8])
+
+
+PERF_FIELDS = ["staticCollide", "humanCollide", "agentCollide", "shadowGoals", "episodeReward", "episodeCostReward",
+               "totalGoals", "constraintViolations"]
+
+
+def oracle_perf(outs, prefix):
+    """runner.py:66-99's counters over the first `prefix` steps of oracle step outputs (the
+    float sums through the oracle's restatement of numpy's, oc_episode_sum)."""
+    from mapf_amd.config import EnvParameters
+    st = np.stack([o["status"] for o in outs[:prefix]])
+    goals = np.stack([o["goals"] for o in outs[:prefix]]).astype(np.float32)
+    rw = np.stack([o["reward"] for o in outs[:prefix]]).astype(np.float32)
+    rt = (rw + np.where(goals == 1, np.float32(EnvParameters.GOAL_REWARD), np.float32(0))).astype(np.float32)
+    cost = np.stack([o["cost"] for o in outs[:prefix]]).astype(np.float32)
+    return {"staticCollide": int((st == -1).sum()), "humanCollide": int((st == -2).sum()),
+            "agentCollide": int((st == -3).sum()), "shadowGoals": int(sum(int(o["shadow"]) for o in outs[:prefix])),
+            "episodeReward": float(O.episode_sum(rt[:, None, :])[0]),
+            "episodeCostReward": float(O.episode_sum(cost[:, None, :])[0]),
+            "totalGoals": float(goals.sum(dtype=np.float64)),
+            "constraintViolations": float(np.stack([o["constr"] for o in outs[:prefix]]).sum(dtype=np.float64))}
+
+
+@pytest.mark.parametrize("name", G1_NAMES)
+def test_oracle_one_episode_performance_matches_reference(name):
+    """g1_perf: the reference's OneEpPerformance counters (runner.py:66-99, run by
+    make_golden.py over the same episode with util.OneEpPerformance) after every step; the
+    oracle's step outputs and its float32 np.sum restatement give the same values bit for bit
+    (episodeReward / episodeCostReward are np.float32 accumulators in the reference)."""
+    z = load(name)
+    perf = load("g1_perf")
+    assert list(perf["fields"]) == PERF_FIELDS
+    assert list(perf[f"{name}__types"]) == ["int", "int", "int", "int", "float32", "float32", "float64", "float64"]
+    env = replay_g1(z)
+    outs = [env.step(z["actions"][t]) for t in range(int(z["steps"]))]
+    for prefix in sorted({1, 2, 7, 50, len(outs)}):
+        got = oracle_perf(outs, prefix)
+        for k in PERF_FIELDS:
+            assert got[k] == perf[f"{name}__{k}"][prefix - 1], (name, prefix, k, got[k], perf[f"{name}__{k}"][prefix - 1])
+
+
+def test_oracle_episode_sum_is_numpy_sum():
+    """oc_episode_sum == the reference's accumulation written with numpy itself, N = 1..64."""
+    g = np.random.default_rng(4)
+    vals = np.array([-0.3, -0.5, -1.0, 0.0, 1.5, -0.25, 1.2, -0.02, 0.1], np.float32)
+    for N in list(range(1, 18)) + [23, 31, 32, 33, 64]:
+        x = np.where(g.random((40, 3, N)) < 0.5, g.choice(vals, (40, 3, N)),
+                     g.normal(size=(40, 3, N)) * 3).astype(np.float32)
+        want = []
+        for b in range(3):
+            acc = 0
+            for t in range(40):
+                acc += np.sum(x[t, b][None, :])
+            assert type(acc) is np.float32
+            want.append(acc)
+        np.testing.assert_array_equal(O.episode_sum(x), np.array(want, np.float32))
