@@ -282,12 +282,16 @@ def main():
                     out={k: torch.zeros((TS,) + tuple(v.shape), dtype=v.dtype, device=dev)
                          for k, v in env.out.items()})
 
+    launchers = {}
+
     def rollout(n):
         if roll is None:
             env.rollout_random(n)
-        else:
-            env.rollout_random(n, slots=True, actions=roll["actions"][:n], obs=roll["obs"][:n],
-                               vec=roll["vec"][:n], out={k: v[:n] for k, v in roll["out"].items()})
+        else:                        # slots [0, n): the call prepared once per launch length
+            if n not in launchers:
+                launchers[n] = env.rollout_launcher(n, slots=True, actions=roll["actions"][:n], obs=roll["obs"][:n],
+                                                    vec=roll["vec"][:n], out={k: v[:n] for k, v in roll["out"].items()})
+            launchers[n]()
 
     def one_step():
         if path == "split":

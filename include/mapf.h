@@ -306,6 +306,13 @@ int mapf_normalize_advantages(const float *ret, const float *v, const float *cre
                               float *adv_out, float *cadv_out, int32_t M, double lagrange, int32_t mix,
                               void *stream);
 
+/* mapf_normalize_advantages with the multiplier in DEVICE memory, lam_dev[2] = {f32(lagrange),
+ * f32(lagrange + 1)} (computed on the host in double, as mapf_normalize_advantages does): the
+ * form a captured hipGraph of the update replays with a new multiplier every update. */
+int mapf_normalize_advantages_dlam(const float *ret, const float *v, const float *cret, const float *cv,
+                                   float *adv_out, float *cadv_out, int32_t M, const float *lam_dev, int32_t mix,
+                                   void *stream);
+
 /* mapf_normalize_advantages over a minibatch split across ranks (model.py:106-113 on the GLOBAL
  * minibatch).  Per rank, x = ret - v and c = cret - cv over its M rows, in fp64:
  *   mapf_advantage_moments(mean = NULL): out[2] = {sum x, sum c}                -> all-reduce (sum)
@@ -383,6 +390,15 @@ int mapf_ppo_loss(const float *new_ps, const float *old_ps, const int64_t *actio
                   const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
                   const float *coef, float *loss, float *terms, float *grad_ps, float *grad_v, float *grad_cv,
                   float *grad_sig, void *stream);
+
+/* mapf_ppo_loss with coef[6] in DEVICE memory (captured-graph updates: the Lagrangian term changes
+ * every update without re-capturing). */
+int mapf_ppo_loss_dcoef(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,
+                        const float *old_v, const float *returns, const float *new_cv, const float *old_cv,
+                        const float *cost_returns, const float *advantage, const float *cost_advantage,
+                        const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
+                        const float *coef_dev, float *loss, float *terms, float *grad_ps, float *grad_v,
+                        float *grad_cv, float *grad_sig, void *stream);
 
 #ifdef __cplusplus
 }

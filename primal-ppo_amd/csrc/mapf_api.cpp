@@ -925,8 +925,18 @@ int mapf_normalize_advantages(const float *ret, const float *v, const float *cre
                               float *cadv_out, int32_t M, double lagrange, int32_t mix, void *stream) {
     if (!ret || !v || !cret || !cv || !adv_out || !cadv_out) return fail(MAPF_EINVAL, "null argument");
     if (M < 1) return fail(MAPF_EINVAL, "M must be >= 1");
-    launch_normalize(ret, v, cret, cv, adv_out, cadv_out, M, (float)lagrange, (float)(lagrange + 1.0), mix,
+    launch_normalize(ret, v, cret, cv, adv_out, cadv_out, M, (float)lagrange, (float)(lagrange + 1.0), mix, nullptr,
                      (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_normalize_advantages_dlam(const float *ret, const float *v, const float *cret, const float *cv,
+                                   float *adv_out, float *cadv_out, int32_t M, const float *lam_dev, int32_t mix,
+                                   void *stream) {
+    if (!ret || !v || !cret || !cv || !adv_out || !cadv_out || !lam_dev) return fail(MAPF_EINVAL, "null argument");
+    if (M < 1) return fail(MAPF_EINVAL, "M must be >= 1");
+    launch_normalize(ret, v, cret, cv, adv_out, cadv_out, M, 0.f, 1.f, mix, lam_dev, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return MAPF_OK;
 }

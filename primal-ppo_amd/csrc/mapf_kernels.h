@@ -166,7 +166,7 @@ void launch_reset_seeded(const DevEnv &e, hipStream_t s);
 void launch_gae(const float *r, const float *v, const float *vl, float *adv, float *ret, int T, int M, float g,
                 float gl, hipStream_t s);
 void launch_normalize(const float *ret, const float *v, const float *cret, const float *cv, float *adv,
-                      float *cadv, int M, float lam, float lam1, int mix, hipStream_t s);
+                      float *cadv, int M, float lam, float lam1, int mix, const float *lamd, hipStream_t s);
 void launch_moments(const float *ret, const float *v, const float *cret, const float *cv, int M, const double *mean,
                     double *out, hipStream_t s);
 void launch_normalize_stats(const float *ret, const float *v, const float *cret, const float *cv, const double *stats,

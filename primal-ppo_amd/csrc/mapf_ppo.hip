@@ -36,6 +36,7 @@ struct Args {
     long R;
     int A, sig_fp16;
     float clip, ent, vc, valid, cvc, costlam;
+    const float *coefd;      // non-null: the six coefficients read from device memory (graph replays)
 };
 
 __device__ inline float r16(float x) { return __half2float(__float2half_rn(x)); }
@@ -60,6 +61,10 @@ __device__ inline float value_term(float v, float ov, float r, float c, float &g
 }
 
 __global__ __launch_bounds__(1024) void ppo_loss_kernel(Args a) {
+    if (a.coefd) {
+        a.clip = a.coefd[0]; a.ent = a.coefd[1]; a.vc = a.coefd[2];
+        a.valid = a.coefd[3]; a.cvc = a.coefd[4]; a.costlam = a.coefd[5];
+    }
     constexpr int NS = 7;              // policy, entropy, critic, valid, cost critic, cost, clipped
     float s[NS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float invR = 1.f / (float)a.R, invRA = 1.f / ((float)a.R * (float)a.A);
@@ -143,21 +148,45 @@ using namespace mapf;
 
 extern "C" {
 
+static int ppo_loss(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,
+                    const float *old_v, const float *returns, const float *new_cv, const float *old_cv,
+                    const float *cost_returns, const float *advantage, const float *cost_advantage,
+                    const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
+                    const float *coef, bool coef_on_device, float *loss, float *terms, float *grad_ps, float *grad_v,
+                    float *grad_cv, float *grad_sig, void *stream) {
+    if (!new_ps || !old_ps || !action || !new_v || !old_v || !returns || !new_cv || !old_cv || !cost_returns ||
+        !advantage || !cost_advantage || !policy_sig || !train_valid || !coef || !loss || !terms || !grad_ps || !grad_v ||
+        !grad_cv || !grad_sig || R < 1 || A < 1 || A > 64)
+        return MAPF_EINVAL;
+    const float h[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float *c = coef_on_device ? h : coef;
+    ppo::Args a{new_ps, old_ps, new_v, old_v, returns, new_cv, old_cv, cost_returns, advantage, cost_advantage,
+                policy_sig, train_valid, action, loss, terms, grad_ps, grad_v, grad_cv, grad_sig, (long)R, (int)A,
+                sig_fp16 ? 1 : 0, c[0], c[1], c[2], c[3], c[4], c[5], coef_on_device ? coef : nullptr};
+    hipLaunchKernelGGL(ppo::ppo_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
 int mapf_ppo_loss(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,
                   const float *old_v, const float *returns, const float *new_cv, const float *old_cv,
                   const float *cost_returns, const float *advantage, const float *cost_advantage,
                   const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
                   const float *coef, float *loss, float *terms, float *grad_ps, float *grad_v, float *grad_cv,
                   float *grad_sig, void *stream) {
-    if (!new_ps || !old_ps || !action || !new_v || !old_v || !returns || !new_cv || !old_cv || !cost_returns ||
-        !advantage || !cost_advantage || !policy_sig || !train_valid || !coef || !loss || !terms || !grad_ps || !grad_v ||
-        !grad_cv || !grad_sig || R < 1 || A < 1 || A > 64)
-        return MAPF_EINVAL;
-    ppo::Args a{new_ps, old_ps, new_v, old_v, returns, new_cv, old_cv, cost_returns, advantage, cost_advantage,
-                policy_sig, train_valid, action, loss, terms, grad_ps, grad_v, grad_cv, grad_sig, (long)R, (int)A,
-                sig_fp16 ? 1 : 0, coef[0], coef[1], coef[2], coef[3], coef[4], coef[5]};
-    hipLaunchKernelGGL(ppo::ppo_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
-    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+    return ppo_loss(new_ps, old_ps, action, new_v, old_v, returns, new_cv, old_cv, cost_returns, advantage,
+                    cost_advantage, policy_sig, sig_fp16, train_valid, R, A, coef, false, loss, terms, grad_ps, grad_v,
+                    grad_cv, grad_sig, stream);
+}
+
+int mapf_ppo_loss_dcoef(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,
+                        const float *old_v, const float *returns, const float *new_cv, const float *old_cv,
+                        const float *cost_returns, const float *advantage, const float *cost_advantage,
+                        const float *policy_sig, int32_t sig_fp16, const float *train_valid, int64_t R, int32_t A,
+                        const float *coef_dev, float *loss, float *terms, float *grad_ps, float *grad_v,
+                        float *grad_cv, float *grad_sig, void *stream) {
+    return ppo_loss(new_ps, old_ps, action, new_v, old_v, returns, new_cv, old_cv, cost_returns, advantage,
+                    cost_advantage, policy_sig, sig_fp16, train_valid, R, A, coef_dev, true, loss, terms, grad_ps,
+                    grad_v, grad_cv, grad_sig, stream);
 }
 
 }  // extern "C"

@@ -57,8 +57,9 @@ __device__ inline double block_sum(double x, double *sh) {
 __global__ __launch_bounds__(1024) void normalize_kernel(const float *__restrict__ ret, const float *__restrict__ v,
                                                          const float *__restrict__ cret, const float *__restrict__ cv,
                                                          float *__restrict__ adv, float *__restrict__ cadv, int M,
-                                                         float lam, float lam1, int mix) {
+                                                         float lam, float lam1, int mix, const float *lamd) {
     __shared__ double sh[16];
+    if (lamd) { lam = lamd[0]; lam1 = lamd[1]; }     // {lam, f32(lam + 1)} in device memory (graph replays)
     double s0 = 0.0, s1 = 0.0;
     for (int k = threadIdx.x; k < M; k += blockDim.x) {
         s0 += (double)__fsub_rn(ret[k], v[k]);
@@ -196,8 +197,9 @@ void launch_gae(const float *r, const float *v, const float *vl, float *adv, flo
 }
 
 void launch_normalize(const float *ret, const float *v, const float *cret, const float *cv, float *adv, float *cadv,
-                      int M, float lam, float lam1, int mix, hipStream_t s) {
-    hipLaunchKernelGGL(normalize_kernel, dim3(1), dim3(1024), 0, s, ret, v, cret, cv, adv, cadv, M, lam, lam1, mix);
+                      int M, float lam, float lam1, int mix, const float *lamd, hipStream_t s) {
+    hipLaunchKernelGGL(normalize_kernel, dim3(1), dim3(1024), 0, s, ret, v, cret, cv, adv, cadv, M, lam, lam1, mix,
+                       lamd);
 }
 
 void launch_sample(const float *ps, int stride, int32_t *a32, int64_t *a64, int M, uint64_t seed, uint32_t step,

@@ -42,11 +42,14 @@ class _FusedPPOLoss(torch.autograd.Function):
         grads = [torch.empty(R, A, device=new_ps.device), torch.empty(R, device=new_ps.device),
                  torch.empty(R, device=new_ps.device), torch.empty(R, A, device=new_ps.device)]
         p = lambda t: ctypes.c_void_p(t.data_ptr())
-        c = (ctypes.c_float * 6)(*coef)
         st = ctypes.c_void_p(torch.cuda.current_stream(new_ps.device).cuda_stream)
-        _lib.check(_lib.lib().mapf_ppo_loss(*[p(t) for t in ins], *[p(t) for t in vecs[:6]], p(vecs[6]),
-                                            p(vecs[7]), p(sig), int(policy_sig.dtype == torch.float16), p(tv), R, A,
-                                            c, p(loss), p(terms), *[p(g) for g in grads], st))
+        if isinstance(coef, torch.Tensor):     # device coefficients (the captured update)
+            fn, c = _lib.lib().mapf_ppo_loss_dcoef, p(coef)
+        else:
+            fn, c = _lib.lib().mapf_ppo_loss, (ctypes.c_float * 6)(*coef)
+        _lib.check(fn(*[p(t) for t in ins], *[p(t) for t in vecs[:6]], p(vecs[6]), p(vecs[7]), p(sig),
+                      int(policy_sig.dtype == torch.float16), p(tv), R, A, c, p(loss), p(terms),
+                      *[p(g) for g in grads], st))
         ctx.save_for_backward(*grads)
         ctx.meta = [(t.shape, t.dtype) for t in (new_ps, new_v, new_cv, policy_sig)]
         ctx.mark_non_differentiable(terms)
@@ -131,8 +134,13 @@ class Model:
         self.num_agents = num_agents or EnvParameters.N_AGENTS
         self._flat = None
         self.fused_loss = True        # GPU: the loss terms + their gradient in one launch (_FusedPPOLoss)
+        self.graph_update = True      # GPU, one rank: the whole update as one captured hipGraph (_DeviceUpdate)
+        self._updates = {}
         if global_model:
-            self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr)
+            # fused Adam on the GPU: one launch for every parameter, and the AMP found-inf skip taken
+            # on the device (optimizer.found_inf), so the update has no host synchronisation
+            self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr,
+                                                  fused=self.device.type == "cuda")
             self.lagrange = get_lagrangian(LagrangianParameters.LAGRANGIAN_TYPE, TrainingParameters.COST_LIMIT_PER_AGENT)
             self.net_scaler = torch.amp.GradScaler(self.device.type, enabled=self.device.type == "cuda")
             self.broadcast_weights()
@@ -204,7 +212,6 @@ class Model:
         """model.py:78-199.  Inputs may be numpy arrays (reference contract) or device tensors."""
         dev = self.device
         t = lambda x: (torch.from_numpy(x) if isinstance(x, np.ndarray) else x).to(dev)
-        self.net_optimizer.zero_grad()
         observation, vector = t(observation), t(vector)
         returns, old_v, cost_returns, old_cv = t(returns).float(), t(old_v).float(), t(cost_returns).float(), t(old_cv).float()
         action = t(action).long().unsqueeze(-1)
@@ -212,6 +219,9 @@ class Model:
 
         lam = self.lagrange.get_lagrangian_param()
         distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if dev.type == "cuda" and self.fused_loss:      # the device update (fused loss, captured graph)
+            return self._train_device(observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps,
+                                      input_state, train_valid, episode_cost, lam, distributed)
         if dev.type == "cuda":
             # the HIP normalisation; distributed: global two-pass moments all-reduced into it
             from .env import normalize_advantages, normalize_advantages_distributed
@@ -224,17 +234,7 @@ class Model:
             if TrainingParameters.MINUS_ADV_WITH_CADV:
                 advantage = (advantage - lam * cost_advantage) / (lam + 1)
 
-        if dev.type == "cuda" and self.fused_loss:
-            with torch.autocast(device_type="cuda"):
-                new_ps, new_v, block, policy_sig, _, _, new_cv = self.network(observation, vector, input_state)
-            T = TrainingParameters
-            all_loss, terms = _FusedPPOLoss.apply(
-                new_ps, new_v, new_cv, policy_sig, old_ps, action, old_v, returns, old_cv, cost_returns, advantage,
-                cost_advantage, train_valid,
-                (T.CLIP_RANGE, T.ENTROPY_COEF, T.VALUE_COEF, T.VALID_COEF, T.COST_VALUE_COEF, T.COST_COEF * lam))
-            policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss, clip_frac = terms.unbind()
-            return self._finish_update(all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss,
-                                       cost_loss, clip_frac, advantage, cost_advantage, episode_cost, distributed)
+        self.net_optimizer.zero_grad()
         with torch.autocast(device_type=dev.type, enabled=dev.type == "cuda"):
             new_ps, new_v, block, policy_sig, _, _, new_cv = self.network(observation, vector, input_state)
             new_p = new_ps.gather(-1, action)
@@ -262,6 +262,38 @@ class Model:
         return self._finish_update(all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss,
                                    cost_loss, clip_frac, advantage, cost_advantage, episode_cost, distributed)
 
+    # ------------------------------------------------------------ the device update
+    def _train_device(self, observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, input_state,
+                      train_valid, episode_cost, lam, distributed):
+        """model.py:78-199 on the GPU with no host synchronisation inside the update: HIP
+        normalisation (multiplier in device memory), autocast forward, the fused loss (its
+        coefficients in device memory), backward, [RCCL all-reduce of the gradient bucket],
+        AMP unscale + found-inf on the device, clip, fused Adam skipping on found-inf, loss-scale
+        update -- GradScaler's semantics (init 2^16, x2 every 2000 finite steps, x0.5 on inf).
+        One rank: after two eager updates of a minibatch shape the same body is captured into a
+        hipGraph and every later update of that shape is one replay (the host launched ~1,500
+        small ops per update).  Distributed: eager (the all-reduce sits between backward and
+        unscale, model.py:177-185)."""
+        key = (tuple(observation.shape), tuple(vector.shape), tuple(old_ps.shape), tuple(train_valid.shape),
+               input_state is None)
+        upd = self._updates.get(key)
+        if upd is None:
+            upd = self._updates[key] = _DeviceUpdate(self, observation, vector, returns, old_ps, train_valid, action)
+        T = TrainingParameters
+        upd.load(observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, train_valid,
+                 coef=(T.CLIP_RANGE, T.ENTROPY_COEF, T.VALUE_COEF, T.VALID_COEF, T.COST_VALUE_COEF, T.COST_COEF * lam),
+                 lam=lam)
+        upd.run(graph=self.graph_update and not distributed and input_state is None, allreduce=distributed)
+        # the Lagrangian step (host, model.py:180) depends only on the episode cost
+        if distributed:   # every rank must update the multiplier with the same episode cost
+            c = torch.tensor([float(episode_cost)], dtype=torch.float64, device=self.device)
+            dist.all_reduce(c)
+            episode_cost = c.item() / dist.get_world_size()
+        self.lagrange.update_lagrangian_multiplier(episode_cost / EnvParameters.N_AGENTS)
+        self.network.weights_updated()        # replays bump no tensor version: drop the fp16 acting copies
+        stats = upd.stats.cpu().numpy()       # one device -> host copy
+        return [np.asarray(v) for v in stats] + [self.lagrange.get_lagrangian_param()]
+
     def _finish_update(self, all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss,
                        clip_frac, advantage, cost_advantage, episode_cost, distributed):
         """model.py:177-199: backward, gradient exchange, Lagrangian step, clip, Adam, stats."""
@@ -281,3 +313,87 @@ class Model:
             all_loss, policy_loss, entropy, critic_loss, valid_loss, cost_critic_loss, cost_loss, clip_frac, grad_norm,
             torch.mean(advantage), torch.mean(cost_advantage))]).cpu().numpy()       # one device -> host copy
         return [np.asarray(v) for v in stats] + [self.lagrange.get_lagrangian_param()]
+
+
+class _DeviceUpdate:
+    """The static buffers and the body of one minibatch shape's device update (Model._train_device)."""
+
+    WARMUP = 2          # eager updates before the capture (allocator, MIOpen find, Adam state)
+
+    def __init__(self, model, observation, vector, returns, old_ps, train_valid, action):
+        dev = model.device
+        self.model = model
+        e = lambda x, dt=torch.float32: torch.zeros(tuple(x.shape), dtype=dt, device=dev)   # noqa: E731
+        self.obs, self.vec = e(observation), e(vector)
+        self.ret, self.cret, self.v, self.cv = e(returns), e(returns), e(returns), e(returns)
+        self.action = e(action, torch.int64)
+        self.old_ps, self.tv = e(old_ps), e(train_valid)
+        self.dyn = torch.zeros(8, dtype=torch.float32, device=dev)     # coef[6], lam, f32(lam + 1)
+        sc = model.net_scaler                  # its settings (torch.amp.GradScaler: 2^16, x2 / 2000, x0.5)
+        self.scale = torch.full((1,), float(sc._init_scale), dtype=torch.float32, device=dev)
+        self.growth = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.amp = (float(sc._growth_factor), float(sc._backoff_factor), int(sc._growth_interval))
+        self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(11, dtype=torch.float32, device=dev)
+        self.graph = None
+        self.eager_runs = 0
+
+    def load(self, observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, train_valid, coef, lam):
+        for dst, src in ((self.obs, observation), (self.vec, vector), (self.ret, returns), (self.cret, cost_returns),
+                         (self.v, old_v), (self.cv, old_cv), (self.old_ps, old_ps), (self.tv, train_valid)):
+            dst.copy_(src.reshape(dst.shape), non_blocking=True)
+        self.action.copy_(action.reshape(self.action.shape), non_blocking=True)
+        # host double -> f32 exactly as the host-argument kernels round them
+        h = torch.tensor(list(coef) + [lam, lam + 1.0], dtype=torch.float64).float()
+        self.dyn.copy_(h.pin_memory() if torch.cuda.is_available() else h, non_blocking=True)
+
+    def body(self, allreduce=False):
+        m, net, opt = self.model, self.model.network, self.model.net_optimizer
+        T = TrainingParameters
+        opt.zero_grad(set_to_none=True)
+        from .env import normalize_advantages_dlam
+        adv, cadv = normalize_advantages_dlam(self.ret.reshape(-1), self.v.reshape(-1), self.cret.reshape(-1),
+                                              self.cv.reshape(-1), self.dyn[6:8], T.MINUS_ADV_WITH_CADV)
+        adv, cadv = adv.view(self.ret.shape), cadv.view(self.ret.shape)
+        with torch.autocast(device_type="cuda", cache_enabled=False):
+            new_ps, new_v, block, policy_sig, _, _, new_cv = net(self.obs, self.vec, None)
+        all_loss, terms = _FusedPPOLoss.apply(new_ps, new_v, new_cv, policy_sig, self.old_ps, self.action.unsqueeze(-1),
+                                              self.v, self.ret, self.cv, self.cret, adv, cadv, self.tv, self.dyn[:6])
+        (all_loss * self.scale).backward()
+        if allreduce:
+            m._allreduce_grads()
+        params = [p for p in net.parameters() if p.grad is not None]
+        self.found_inf.zero_()
+        torch._amp_foreach_non_finite_check_and_unscale_([p.grad for p in params], self.found_inf,
+                                                         self.scale.double().reciprocal().float())
+        grad_norm = torch.nn.utils.clip_grad_norm_(params, T.MAX_GRAD_NORM)
+        opt.grad_scale, opt.found_inf = None, self.found_inf     # fused Adam: skipped on the device when inf
+        opt.step()
+        opt.grad_scale = opt.found_inf = None
+        torch._amp_update_scale_(self.scale, self.growth, self.found_inf, *self.amp)
+        self.stats.copy_(torch.stack([t.detach().float().reshape(()) for t in (
+            all_loss, terms[0], terms[1], terms[2], terms[3], terms[4], terms[5], terms[6], grad_norm,
+            torch.mean(adv), torch.mean(cadv))]))
+
+    def run(self, graph=True, allreduce=False):
+        if not graph or self.eager_runs < self.WARMUP:
+            if graph:                       # warm-up on a side stream, as capture wants
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    self.body()
+                torch.cuda.current_stream().wait_stream(s)
+            else:
+                self.body(allreduce=allreduce)
+            self.eager_runs += 1
+            return
+        if self.graph is None:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self.body()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = g
+        self.graph.replay()

@@ -181,6 +181,11 @@ class SCRIMPNet(nn.Module):
         self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
 
+    def weights_updated(self):
+        """Forget the acting path's fp16 weight copies: an update replayed from a captured graph
+        changes the parameters without bumping their version counters (_half's key)."""
+        self._h16.clear()
+
     def forward(self, obs, vector, input_state=None):
         """Returns (policy, value, blocking, policy_sig, x, policy_logits, cost_value) like net.py:101-155.
         obs: [..., N, C, F, F] (any leading shape); the agent axis is num_agents (EnvParameters.N_AGENTS

@@ -1,0 +1,85 @@
+"""The PPO update on the device (Model._train_device, model.py:78-199 of the reference): the
+whole AMP update -- HIP normalisation, forward, fused loss, backward, unscale + found-inf,
+clip, fused Adam, loss-scale update -- captured once per minibatch shape and replayed.  The
+replays must apply the same updates as the eager body (same kernels; MIOpen's backward may
+reduce in another order, so to fp16-backward tolerance), change the weights, keep the AMP
+state on the device, and leave the acting path on the new weights."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(g, rows=64, n=8):
+    obs = (torch.rand(rows, n, 6, 9, 9, device="cuda", generator=g) < 0.3).float()
+    vec = torch.randn(rows, n, 4, device="cuda", generator=g)
+    ret, v, cret, cv = (torch.randn(rows, n, device="cuda", generator=g) for _ in range(4))
+    act = torch.randint(0, 5, (rows, n), device="cuda", generator=g)
+    ps = torch.softmax(torch.randn(rows, n, 5, device="cuda", generator=g), -1)
+    tv = (torch.rand(rows, n, 5, device="cuda", generator=g) < 0.7).float()
+    return obs, vec, ret, cret, v, cv, act, ps, tv
+
+
+def test_graphed_updates_equal_eager_updates():
+    from mapf_amd.model import Model
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(0)
+    m1 = Model(0, "cuda", global_model=True, numChannel=6, num_agents=8, fov=9)
+    m2 = copy.deepcopy(m1)
+    m2.graph_update = False
+    for m in (m1, m2):
+        m.network.eval()                        # no dropout: both see the same net
+        m.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    batches = [_batch(g) for _ in range(6)]
+    w0 = m1.network.conv1.weight.detach().clone()
+    for k, (obs, vec, ret, cret, v, cv, act, ps, tv) in enumerate(batches):
+        s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
+        s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
+        assert all(np.isfinite(float(x)) for x in s1), (k, s1)
+        for i, (a, b) in enumerate(zip(s1, s2)):
+            assert abs(float(a) - float(b)) <= 2e-3 * max(1.0, abs(float(b))), (k, i, a, b)
+        assert len(m1.network._h16) == 0        # the acting path's fp16 weights are re-read
+    upd = next(iter(m1._updates.values()))
+    assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
+    assert not torch.equal(m1.network.conv1.weight, w0)            # ... which moved the weights
+    # the weights after six updates: Adam's steps are ~lr * sign(grad), a sign flips where a
+    # gradient is ~0 under another reduction order -- compare the bulk, not every element
+    for (n1, p1), (_, p2) in zip(m1.network.named_parameters(), m2.network.named_parameters()):
+        d = (p1 - p2).abs()
+        assert (d <= 1e-6 + 1e-4 * p2.abs()).float().mean().item() > 0.98, n1
+    torch.testing.assert_close(m1._updates[next(iter(m1._updates))].scale,
+                               m2._updates[next(iter(m2._updates))].scale)
+    # acting after graphed updates == acting of a model holding the same weights
+    saved, m1._updates = m1._updates, {}         # (captured graphs are not copyable)
+    m3 = copy.deepcopy(m1)
+    m1._updates = saved
+    obs, vec = batches[0][0], batches[0][1]
+    torch.manual_seed(5)
+    a1 = m1.network(obs, vec)
+    torch.manual_seed(5)
+    a3 = m3.network(obs, vec)
+    with torch.no_grad():
+        torch.manual_seed(5)
+        f1 = m1.network(obs, vec)
+        torch.manual_seed(5)
+        f3 = m3.network(obs, vec)
+    torch.testing.assert_close(a1[0], a3[0])
+    torch.testing.assert_close(f1[0], f3[0])
+
+
+def test_update_shapes_get_their_own_graphs():
+    from mapf_amd.model import Model
+    torch.manual_seed(0)
+    m = Model(0, "cuda", global_model=True, numChannel=6, num_agents=8, fov=9)
+    m.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for rows in (32, 48, 32, 48, 32, 48, 32):
+        b = _batch(g, rows)
+        s = m.train(*b[:8], None, b[8], 0.5)
+        assert all(np.isfinite(float(x)) for k, x in enumerate(s) if k != 8)
+    assert len(m._updates) == 2 and all(u.graph is not None for u in m._updates.values())

@@ -18,7 +18,9 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=256)
-    ap.add_argument("--updates", type=int, default=5)
+    ap.add_argument("--updates", type=int, default=20)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from mapf_amd.config import EnvParameters, make_config
@@ -26,7 +28,7 @@ def main():
     from mapf_amd.maps import generate_warehouse
     from mapf_amd.model import Model
     from mapf_amd.runner import DeviceRunner
-    N = 8
+    N = args.agents
     EnvParameters.N_AGENTS = N
     EnvParameters.FOV_SIZE = 9
     env = BatchedMapfGym(make_config(args.rows, 20, 20, num_agents=N, fov=9, num_channel=6, human_mode="random",
@@ -41,14 +43,24 @@ def main():
     def upd():
         return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
                            sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
-    for _ in range(3):
-        upd()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.updates):
-        upd()
-    torch.cuda.synchronize()
-    print(f"update: {(time.perf_counter() - t0) / args.updates * 1e3:.2f} ms for {args.rows} x {N} rows", flush=True)
+    res = {}
+    for mode in ("graph", "eager", "graph"):      # Model.graph_update: one captured hipGraph per update
+        model.graph_update = mode == "graph"
+        for _ in range(3):
+            upd()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.updates):
+            t0 = time.perf_counter()
+            upd()                                  # returns host stats: synchronises every update
+            ts.append(time.perf_counter() - t0)
+        res.setdefault(mode, []).append(float(np.median(ts)) * 1e3)
+        print(f"update ({mode}): median {np.median(ts) * 1e3:.2f} ms, mean {np.mean(ts) * 1e3:.2f} ms for "
+              f"{args.rows} x {N} rows", flush=True)
+    import json
+    print(json.dumps({"rows": args.rows, "agents": N, "median_ms": res}), flush=True)
+    if args.no_profile:
+        return
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
         for _ in range(args.updates):
