@@ -330,10 +330,10 @@ class _DeviceUpdate:
         self.old_ps, self.tv = e(old_ps), e(train_valid)
         self.dyn = torch.zeros(8, dtype=torch.float32, device=dev)     # coef[6], lam, f32(lam + 1)
         sc = model.net_scaler                  # its settings (torch.amp.GradScaler: 2^16, x2 / 2000, x0.5)
-        self.scale = torch.full((1,), float(sc._init_scale), dtype=torch.float32, device=dev)
-        self.growth = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.scale = torch.full((), float(sc._init_scale), dtype=torch.float32, device=dev)   # 0-dim, as GradScaler's
+        self.growth = torch.zeros((), dtype=torch.int32, device=dev)
         self.amp = (float(sc._growth_factor), float(sc._backoff_factor), int(sc._growth_interval))
-        self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
         self.stats = torch.zeros(11, dtype=torch.float32, device=dev)
         self.graph = None
         self.eager_runs = 0
