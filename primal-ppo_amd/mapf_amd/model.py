@@ -139,8 +139,9 @@ class Model:
         if global_model:
             # fused Adam on the GPU: one launch for every parameter, and the AMP found-inf skip taken
             # on the device (optimizer.found_inf), so the update has no host synchronisation
-            self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr,
-                                                  fused=self.device.type == "cuda")
+            gpu = self.device.type == "cuda"
+            self.net_optimizer = torch.optim.Adam(self.network.parameters(), lr=TrainingParameters.lr, fused=gpu,
+                                                  capturable=gpu)
             self.lagrange = get_lagrangian(LagrangianParameters.LAGRANGIAN_TYPE, TrainingParameters.COST_LIMIT_PER_AGENT)
             self.net_scaler = torch.amp.GradScaler(self.device.type, enabled=self.device.type == "cuda")
             self.broadcast_weights()
