@@ -37,6 +37,7 @@ def test_graphed_updates_equal_eager_updates():
     g = torch.Generator(device="cuda").manual_seed(1)
     batches = [_batch(g) for _ in range(6)]
     w0 = m1.network.conv1.weight.detach().clone()
+    init = [p.detach().clone() for p in m1.network.parameters()]
     for k, (obs, vec, ret, cret, v, cv, act, ps, tv) in enumerate(batches):
         s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
@@ -47,11 +48,12 @@ def test_graphed_updates_equal_eager_updates():
     upd = next(iter(m1._updates.values()))
     assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
     assert not torch.equal(m1.network.conv1.weight, w0)            # ... which moved the weights
-    # the weights after six updates: Adam's steps are ~lr * sign(grad), a sign flips where a
-    # gradient is ~0 under another reduction order -- compare the bulk, not every element
-    for (n1, p1), (_, p2) in zip(m1.network.named_parameters(), m2.network.named_parameters()):
-        d = (p1 - p2).abs()
-        assert (d <= 1e-6 + 1e-4 * p2.abs()).float().mean().item() > 0.98, n1
+    # the weights after six updates: Adam's steps are ~lr * m / sqrt(v), and the first layers'
+    # fp16 gradients differ by ~2 % under another backward reduction order (MIOpen), so the
+    # update DIRECTIONS are compared: the overall relative difference of the six-step deltas
+    d1 = torch.cat([(p1.detach() - p0).flatten() for p1, p0 in zip(m1.network.parameters(), init)])
+    d2 = torch.cat([(p2.detach() - p0).flatten() for p2, p0 in zip(m2.network.parameters(), init)])
+    assert d2.norm() > 0 and ((d1 - d2).norm() / d2.norm()).item() < 5e-2
     torch.testing.assert_close(m1._updates[next(iter(m1._updates))].scale,
                                m2._updates[next(iter(m2._updates))].scale)
     # acting after graphed updates == acting of a model holding the same weights
