@@ -31,7 +31,8 @@ def test_graphed_updates_equal_eager_updates():
     m1 = Model(0, "cuda", global_model=True, numChannel=6, num_agents=8, fov=9)
     m2 = copy.deepcopy(m1)
     m2.graph_update = False
-    for m in (m1, m2):
+    m4 = copy.deepcopy(m2)                      # a second eager twin: the backward's own run-to-run spread
+    for m in (m1, m2, m4):
         m.network.eval()                        # no dropout: both see the same net
         m.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -41,6 +42,7 @@ def test_graphed_updates_equal_eager_updates():
     for k, (obs, vec, ret, cret, v, cv, act, ps, tv) in enumerate(batches):
         s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
+        m4.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         assert all(np.isfinite(float(x)) for x in s1), (k, s1)
         for i, (a, b) in enumerate(zip(s1, s2)):
             assert abs(float(a) - float(b)) <= 2e-3 * max(1.0, abs(float(b))), (k, i, a, b)
@@ -49,11 +51,15 @@ def test_graphed_updates_equal_eager_updates():
     assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
     assert not torch.equal(m1.network.conv1.weight, w0)            # ... which moved the weights
     # the weights after six updates: Adam's steps are ~lr * m / sqrt(v), and the first layers'
-    # fp16 gradients differ by ~2 % under another backward reduction order (MIOpen), so the
-    # update DIRECTIONS are compared: the overall relative difference of the six-step deltas
-    d1 = torch.cat([(p1.detach() - p0).flatten() for p1, p0 in zip(m1.network.parameters(), init)])
-    d2 = torch.cat([(p2.detach() - p0).flatten() for p2, p0 in zip(m2.network.parameters(), init)])
-    assert d2.norm() > 0 and ((d1 - d2).norm() / d2.norm()).item() < 5e-2
+    # fp16 gradients differ by ~2 % between runs of the same eager update (MIOpen's backward
+    # reduction order), which Adam's early steps amplify -- so the graphed deltas are held to the
+    # spread of two eager twins, not to zero
+    delta = lambda m: torch.cat([(p.detach() - p0).flatten() for p, p0 in zip(m.network.parameters(), init)])  # noqa
+    d1, d2, d4 = delta(m1), delta(m2), delta(m4)
+    r_ge = ((d1 - d2).norm() / d2.norm()).item()
+    r_ee = ((d4 - d2).norm() / d2.norm()).item()
+    print(f"relative delta difference: graph vs eager {r_ge:.4f}, eager vs eager {r_ee:.4f}")
+    assert d2.norm() > 0 and r_ge <= max(2.5 * r_ee, 0.02), (r_ge, r_ee)
     torch.testing.assert_close(m1._updates[next(iter(m1._updates))].scale,
                                m2._updates[next(iter(m2._updates))].scale)
     # acting after graphed updates == acting of a model holding the same weights
