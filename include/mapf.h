@@ -391,6 +391,16 @@ int mapf_ppo_loss(const float *new_ps, const float *old_ps, const int64_t *actio
                   const float *coef, float *loss, float *terms, float *grad_ps, float *grad_v, float *grad_cv,
                   float *grad_sig, void *stream);
 
+/* SCRIMPNet's 128- and 256-channel convolutions (net.py:104-111: conv1a / conv1b 3x3 128->128,
+ * conv2 2x2 128->256, conv2a / conv2b 2x2 256->256, stride 1, zero padding `pad`) as an MFMA
+ * implicit GEMM (csrc/mapf_conv.hip).  x: fp16 NHWC [nimg][H][W][Cin]; w_packed: fp16
+ * [Cout][ks][ks][Cin] (torch's weight permuted); y: fp16 NHWC [nimg][Ho][Wo][Cout], Ho = H + 2 pad -
+ * ks + 1.  fp32 accumulation, output rounded to fp16; relu = 1: then + bias (fp16, rounded again)
+ * and ReLU -- the autocast conv followed by mapf_nhwc_bias_relu.  MAPF_EINVAL for other shapes. */
+int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                       int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, int32_t relu,
+                       void *stream);
+
 /* mapf_ppo_loss with coef[6] in DEVICE memory (captured-graph updates: the Lagrangian term changes
  * every update without re-capturing). */
 int mapf_ppo_loss_dcoef(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,

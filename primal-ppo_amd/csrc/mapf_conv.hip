@@ -1,0 +1,212 @@
+// primal-ppo_amd/csrc/mapf_conv.hip -- SCRIMPNet's convolutions (net.py:101-112, under
+// torch.autocast: fp16 operands, fp32 accumulation, fp16 output) as an implicit GEMM on the
+// gfx950 matrix cores, for the acting forward (Model.step / Model.value, no grad).
+//
+//   out[img][oy][ox][n] = sum_{ky, kx, c} in[img][oy + ky - P][ox + kx - P][c] * w[n][ky][kx][c]
+//
+// GEMM view: M = images x Ho x Wo output pixels (NHWC rows), N = Cout, K = KS * KS * Cin,
+// K ordered (ky, kx, c) so that one K-chunk of 64 is 64 consecutive channels of ONE input
+// pixel: a row of the A tile is a contiguous 128-B run of the NHWC input (or zeros where the
+// tap falls in the padding) -- the im2col matrix is never built.  The packed weight is
+// [Cout][KS][KS][Cin] fp16 (torch's [Cout][Cin][KS][KS] permuted once, net.py caches it).
+//
+// Workgroup: WAVES waves, BM = 32 * WAVES output pixels x all Cout channels (the input of a
+// pixel tile is read once per tap, from L2/L1: each input pixel is reused by KS^2 taps).  Each
+// wave owns 32 rows x Cout: Cout/32 accumulators of v_mfma_f32_32x32x16_f16 (16 fp32 per lane
+// each).  K loop over 64-wide chunks staged by LDS-DMA (global_load_lds_dwordx4: no staging
+// registers) into two LDS buffers: chunk c + 1's copies are in flight while the matrix cores
+// work on chunk c (a counted vmcnt retires only chunk c's, then a raw barrier).  LDS rows are
+// 128 B with the 16-B pieces XOR-swizzled by row & 7 -- on the SOURCE side: a DMA instruction
+// writes its 64 lanes' 16 B linearly (8 rows x 8 pieces), so lane l fetches logical piece
+// (l & 7) ^ (row & 7) -- and the 32 rows a ds_read_b128 fragment load touches spread over
+// every bank.  Taps in the padding fetch 16 zero bytes (a zero block in the code object).
+// Epilogue: fp32 accumulators -> fp16 (the conv's own rounding), optionally + bias (rounded
+// again, as torch adds the bias to the fp16 conv output) and ReLU -- through an LDS transpose
+// so every output row leaves as 16-B stores.
+#include <hip/hip_fp16.h>
+
+#include "mapf.h"
+#include "mapf_common.h"
+
+namespace mapf {
+namespace conv {
+
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f16_t __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 64;              // K per chunk: 64 fp16 = one 128-B row per A / B row
+
+__device__ __attribute__((aligned(16))) uint4 g_zero16[1];   // the padding taps' source (zero-initialised)
+
+template <int CIN, int COUT, int KS, int WAVES>
+struct Cfg {
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int NT = COUT / 32;                  // accumulator tiles along N per wave
+    static constexpr int BM = 32 * WAVES;                 // output pixels per workgroup
+    static constexpr int K = KS * KS * CIN;
+    static constexpr int CB = CIN / BK;                   // chunks per tap
+    static constexpr int NCHUNK = KS * KS * CB;
+    static constexpr int A_BYTES = BM * BK * 2, B_BYTES = COUT * BK * 2, BUF = A_BYTES + B_BYTES;
+    static constexpr int JA = BM / 8 / WAVES;             // DMA instructions (8 rows each) per wave per chunk
+    static constexpr int JB = COUT / 8 / WAVES;
+    static constexpr int LDS = 2 * BUF > BM * COUT * 2 ? 2 * BUF : BM * COUT * 2;
+    static_assert(CIN % BK == 0 && COUT % 32 == 0 && (COUT / 8) % WAVES == 0, "shape");
+    static_assert(JA + JB <= 15, "vmcnt field");
+};
+
+// byte offset of 16-B piece q of row r in a swizzled 128-B-row tile
+__device__ inline int swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
+
+__device__ inline uint32_t f2h(float f) { return (uint32_t)__half_as_ushort(__float2half_rn(f)); }
+__device__ inline float h2f(uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xFFFFu))); }
+
+__device__ inline void dma16(const void *src, void *lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
+
+// epi: 0 = raw fp16 conv output, 1 = + bias, ReLU
+template <int CIN, int COUT, int KS, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *__restrict__ in,
+                                                                const uint16_t *__restrict__ w,
+                                                                const uint16_t *__restrict__ bias,
+                                                                uint16_t *__restrict__ out, int M, int H, int W,
+                                                                int Ho, int Wo, int pad, int epi) {
+    using C = Cfg<CIN, COUT, KS, WAVES>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int m0 = (int)blockIdx.x * C::BM;
+    const int HWo = Ho * Wo;
+    // lane l of a DMA instruction fills row 8j + (l >> 3), physical piece l & 7 = logical piece q
+    const int q = (lane & 7) ^ ((lane >> 3) & 7);
+    // this lane's A rows (one per DMA instruction): the output pixel's input pixel index and (oy, ox)
+    int apix[C::JA], ayx[C::JA];
+#pragma unroll
+    for (int j = 0; j < C::JA; ++j) {
+        const int m = m0 + 8 * (wave * C::JA + j) + (lane >> 3);
+        if (m < M) {
+            const int img = m / HWo, pos = m - img * HWo, oy = pos / Wo, ox = pos - oy * Wo;
+            apix[j] = img * H * W + oy * W + ox;
+            ayx[j] = (oy << 16) | ox;
+        } else {
+            apix[j] = 0;
+            ayx[j] = (-30000 << 16);               // every tap out of range
+        }
+    }
+    auto issue = [&](int c, int buf) {             // chunk c -> LDS buffer buf (DMA, in flight)
+        const int tap = c / C::CB, cb = c - tap * C::CB;
+        const int ky = tap / KS, kx = tap - ky * KS;
+        char *A = smem + buf * C::BUF;
+        char *B = A + C::A_BYTES;
+        const int dpix = (ky - pad) * W + (kx - pad);
+#pragma unroll
+        for (int j = 0; j < C::JA; ++j) {
+            const int iy = (ayx[j] >> 16) + ky - pad, ix = (ayx[j] & 0xFFFF) + kx - pad;
+            const void *src = (iy >= 0 && iy < H && ix >= 0 && ix < W)
+                                  ? (const void *)(in + (size_t)(apix[j] + dpix) * CIN + cb * BK + q * 8)
+                                  : (const void *)g_zero16;
+            dma16(src, A + 8 * (wave * C::JA + j) * 128);
+        }
+#pragma unroll
+        for (int j = 0; j < C::JB; ++j) {
+            const int n = 8 * (wave * C::JB + j) + (lane >> 3);
+            dma16(w + (size_t)n * C::K + c * BK + q * 8, B + 8 * (wave * C::JB + j) * 128);
+        }
+    };
+
+    f16_t acc[C::NT];
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b)
+        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+    issue(0, 0);
+    const int fr = lane & 31, fh = lane >> 5;     // fragment row within a 32-tile, K half
+    for (int c = 0; c < C::NCHUNK; ++c) {
+        if (c + 1 < C::NCHUNK) {
+            issue(c + 1, (c + 1) & 1);            // buffer (c+1)&1 was last read in chunk c-1 (barrier since)
+            // chunk c's copies (issued before chunk c + 1's) have landed: vmcnt(JA + JB)
+            __builtin_amdgcn_s_waitcnt(0x0F70 | (C::JA + C::JB));
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __builtin_amdgcn_s_barrier();             // ... in every wave
+        const char *A = smem + (c & 1) * C::BUF;
+        const char *B = A + C::A_BYTES;
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {       // 16-deep MFMA steps
+            const int qq = 2 * s + fh;
+            const h8_t af = *reinterpret_cast<const h8_t *>(A + swz(wave * 32 + fr, qq));
+#pragma unroll
+            for (int b = 0; b < C::NT; ++b) {
+                const h8_t bf = *reinterpret_cast<const h8_t *>(B + swz(b * 32 + fr, qq));
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): this wave's fragment reads are done
+        __builtin_amdgcn_s_barrier();             // ... in every wave: buffer c&1 may be refilled
+    }
+
+    // epilogue: fp16 tile [BM][COUT] in LDS (row-major, 16-B pieces swizzled by row & 7 within
+    // each 128-B group), then 16-B stores of whole output rows
+    char *T = smem;
+    constexpr int RB = COUT * 2;                  // bytes per tile row
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b) {
+        const int n = b * 32 + fr;
+        const float bv = epi ? h2f(bias[n]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            float v = h2f(f2h(acc[b][r]));                    // the conv's fp16 output
+            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);        // + bias (fp16), ReLU
+            const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
+            *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
+                (uint16_t)f2h(v);
+        }
+    }
+    __syncthreads();
+    constexpr int PIECES_ROW = RB / 16;
+    for (int p = t; p < C::BM * PIECES_ROW; p += C::THREADS) {
+        const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
+        const int m = m0 + row;
+        if (m >= M) continue;
+        const int g = pc >> 3, pq = pc & 7;
+        const uint4 v = *reinterpret_cast<const uint4 *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4));
+        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) = v;
+    }
+}
+
+template <int CIN, int COUT, int KS, int WAVES>
+static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, uint16_t *out, int M, int H, int W,
+                   int Ho, int Wo, int pad, int epi, hipStream_t s) {
+    using C = Cfg<CIN, COUT, KS, WAVES>;
+    hipLaunchKernelGGL((conv_igemm_kernel<CIN, COUT, KS, WAVES>), dim3((M + C::BM - 1) / C::BM), dim3(C::THREADS),
+                       C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi);
+}
+
+}  // namespace conv
+}  // namespace mapf
+
+using namespace mapf;
+
+extern "C" {
+
+int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                       int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, int32_t relu,
+                       void *stream) {
+    if (!x || !w_packed || !y || (relu && !bias)) return MAPF_EINVAL;
+    if (nimg < 1 || H < 1 || W < 1 || pad < 0 || pad >= ks) return MAPF_EINVAL;
+    const int Ho = H + 2 * pad - ks + 1, Wo = W + 2 * pad - ks + 1;
+    if (Ho < 1 || Wo < 1) return MAPF_EINVAL;
+    const int64_t M64 = nimg * Ho * Wo;
+    if (M64 > (int64_t)0x7FFFFFFF - 1024 || nimg * H * W > (int64_t)0x7FFFFFFF / 512) return MAPF_EINVAL;
+    const int M = (int)M64, epi = relu ? 1 : 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 4>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    else if (Cin == 128 && Cout == 256 && ks == 2) conv::launch<128, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    else return MAPF_EINVAL;
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+}  // extern "C"

@@ -179,7 +179,10 @@ class SCRIMPNet(nn.Module):
         self.fused_acting = True      # no-grad GPU forward through _forward_fused (csrc/mapf_policy.hip)
         self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
         self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
+        self.own_conv = True           # 128/256-channel convolutions as the MFMA implicit GEMM (mapf_conv_nhwc_f16)
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
+
+    _OWN_CONV = {(128, 128, 3), (128, 256, 2), (256, 256, 2)}    # (Cin, Cout, kernel) of mapf_conv_nhwc_f16
 
     def weights_updated(self):
         """Forget the acting path's fp16 weight copies: an update replayed from a captured graph
@@ -253,8 +256,20 @@ class SCRIMPNet(nn.Module):
             v = vector.reshape(-1, NetParameters.VECTOR_LEN)
 
             def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
-                y = F.conv2d(x, h16(m.weight), None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
                 b = h16(m.bias)
+                co, ci, ks, _ = m.weight.shape
+                if self.own_conv and (ci, co, ks) in self._OWN_CONV and x.is_contiguous(memory_format=torch.channels_last):
+                    # the MFMA implicit GEMM (csrc/mapf_conv.hip); bias + ReLU in its epilogue unless pooled
+                    p = m.padding[0]
+                    B_, _, H_, W_ = x.shape
+                    y = torch.empty((B_, co, H_ + 2 * p - ks + 1, W_ + 2 * p - ks + 1), dtype=torch.float16,
+                                    device=dev, memory_format=torch.channels_last)
+                    chk(lib.mapf_conv_nhwc_f16(ptr(x), ptr(h16(m.weight, "ohwi")), ptr(b), ptr(y), B_, H_, W_, ci, co,
+                                               ks, p, 0 if pool else 1, st))
+                    if not pool:
+                        return y
+                else:
+                    y = F.conv2d(x, h16(m.weight), None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
                 B_, C_, H_, W_ = y.shape
                 if pool:
                     out = torch.empty((B_, C_, H_ // 2, W_ // 2), dtype=y.dtype, device=dev,
@@ -263,6 +278,7 @@ class SCRIMPNet(nn.Module):
                     return out
                 chk(lib.mapf_nhwc_bias_relu(ptr(y), ptr(b), B_ * H_ * W_, C_, st))
                 return y
+            # (a pooled layer's raw output takes bias + ReLU + pool in one pass: mapf_nhwc_bias_relu_pool2)
 
             x = conv(conv(conv(x, self.conv1), self.conv1a), self.conv1b, pool=True)
             x = conv(conv(conv(x, self.conv2), self.conv2a), self.conv2b, pool=True)
@@ -300,6 +316,7 @@ class SCRIMPNet(nn.Module):
         return policy, value, blocking, policy_sig, x, logits, cost_value
 
     _HALF_VIEWS = {"sumT": lambda t: t.sum(0).transpose(0, 1), "sum": lambda t: t.sum(0),
+                   "ohwi": lambda t: t.permute(0, 2, 3, 1),        # conv weight for mapf_conv_nhwc_f16
                    "q": lambda t: t[:t.shape[0] // 3], "kv": lambda t: t[t.shape[0] // 3:]}
 
     def _half(self, t, view=None):

@@ -26,7 +26,7 @@ def _net(n_agents=8):
 @pytest.mark.parametrize("B,own", [(5, True), (256, True), (256, False)])
 def test_fused_acting_forward_matches_torch_path(B, own):
     net = _net().eval()                        # dropout off: both paths deterministic
-    net.fused_attention = net.fused_residual_ln = own
+    net.fused_attention = net.fused_residual_ln = net.own_conv = own
     g = torch.Generator(device="cuda").manual_seed(B)
     obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
     vec = torch.randn(B, 8, 4, device="cuda", generator=g)
@@ -195,3 +195,37 @@ def test_fp16_weight_cache_follows_in_place_updates():
         ref = net(obs, vec)
     torch.testing.assert_close(got[1].float(), ref[1].float(), rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(got[5].float(), ref[5].float(), rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("ci,co,ks,H,B", [(128, 128, 3, 9, 37), (128, 128, 3, 11, 3), (128, 256, 2, 4, 50),
+                                         (256, 256, 2, 5, 33), (256, 256, 2, 6, 7), (128, 128, 3, 9, 1)])
+@pytest.mark.parametrize("relu", [0, 1])
+def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
+    """mapf_conv_nhwc_f16 (MFMA implicit GEMM, csrc/mapf_conv.hip) == the autocast conv (fp16
+    operands, fp32 accumulation, fp16 output; + fp16 bias, ReLU) to fp16 rounding -- ragged
+    pixel counts (the last workgroup's rows past M), every padding tap, 3x3 and 2x2."""
+    from mapf_amd import _lib
+    g = torch.Generator(device="cuda").manual_seed(ci + co + H + B)
+    cl = torch.channels_last
+    x = torch.randn(B, ci, H, H, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    w = (torch.randn(co, ci, ks, ks, device="cuda", generator=g) / (ci * ks * ks) ** 0.5).half()
+    b = torch.randn(co, device="cuda", generator=g).half()
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), None, 1, 1).half()
+    if relu:
+        ref = torch.relu((ref.float() + b.float()).half().float()).half()
+    Ho = H + 2 - ks + 1
+    y = torch.full((B, co, Ho, Ho), float("nan"), dtype=torch.float16, device="cuda").contiguous(memory_format=cl)
+    wp = w.permute(0, 2, 3, 1).contiguous()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().mapf_conv_nhwc_f16(_p(x), _p(wp), _p(b), _p(y), B, H, H, ci, co, ks, 1, relu, st))
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_conv_kernel_rejects_other_shapes():
+    from mapf_amd import _lib
+    x = torch.zeros(1, dtype=torch.float16, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert _lib.lib().mapf_conv_nhwc_f16(_p(x), _p(x), _p(x), _p(x), 1, 9, 9, 6, 128, 3, 1, 1, st) == -1
+    assert _lib.lib().mapf_conv_nhwc_f16(_p(x), _p(x), _p(x), _p(x), 1, 9, 9, 128, 128, 3, 3, 1, st) == -1

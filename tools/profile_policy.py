@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--nchw", action="store_true", help="keep the network NCHW")
     ap.add_argument("--no-find", action="store_true", help="torch.backends.cudnn.benchmark off (no MIOpen find)")
     ap.add_argument("--torch-path", action="store_true", help="the PyTorch forward, not the fused acting path")
+    ap.add_argument("--miopen-conv", action="store_true", help="MIOpen for every convolution (no mapf_conv_nhwc_f16)")
+    ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
     from mapf_amd.model import Model
     dev = torch.device("cuda", 0)
@@ -33,6 +35,7 @@ def main():
     if args.no_find:
         torch.backends.cudnn.benchmark = False
     model.network.fused_acting = not args.torch_path
+    model.network.own_conv = not args.miopen_conv
     for _ in range(3):
         model.step(obs, vec, None)
     torch.cuda.synchronize()
@@ -40,7 +43,10 @@ def main():
     for _ in range(10):
         model.step(obs, vec, None)
     torch.cuda.synchronize()
-    print(f"model.step: {(time.perf_counter() - t0) / 10 * 1e3:.2f} ms for {B * N} agents", flush=True)
+    print(f"model.step: {(time.perf_counter() - t0) / 10 * 1e3:.2f} ms for {B * N} agents "
+          f"(own conv {model.network.own_conv})", flush=True)
+    if args.no_profile:
+        return
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
         for _ in range(3):
