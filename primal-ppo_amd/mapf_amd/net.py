@@ -268,6 +268,14 @@ class SCRIMPNet(nn.Module):
                                                ks, p, 0 if pool else 1, st))
                     if not pool:
                         return y
+                elif (self.own_conv and m.padding[0] == 0 and x.shape[2] == ks and x.shape[3] == ks
+                      and x.is_contiguous(memory_format=torch.channels_last)):
+                    # a kernel covering its whole input (conv3: 3x3 on 3x3 -> 1x1) is a plain GEMM over
+                    # the NHWC pixel, K ordered (ky, kx, c): [B, KS*KS*Cin] x [Cout, KS*KS*Cin]^T
+                    B_ = x.shape[0]
+                    y = F.linear(x.permute(0, 2, 3, 1).reshape(B_, -1), h16(m.weight, "ohwi2d"))
+                    chk(lib.mapf_nhwc_bias_relu(ptr(y), ptr(b), B_, co, st))
+                    return y.view(B_, co, 1, 1)
                 else:
                     y = F.conv2d(x, h16(m.weight), None, m.stride, m.padding).contiguous(memory_format=torch.channels_last)
                 B_, C_, H_, W_ = y.shape
@@ -317,6 +325,7 @@ class SCRIMPNet(nn.Module):
 
     _HALF_VIEWS = {"sumT": lambda t: t.sum(0).transpose(0, 1), "sum": lambda t: t.sum(0),
                    "ohwi": lambda t: t.permute(0, 2, 3, 1),        # conv weight for mapf_conv_nhwc_f16
+                   "ohwi2d": lambda t: t.permute(0, 2, 3, 1).reshape(t.shape[0], -1),   # ... as a GEMM operand
                    "q": lambda t: t[:t.shape[0] // 3], "kv": lambda t: t[t.shape[0] // 3:]}
 
     def _half(self, t, view=None):
