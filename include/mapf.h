@@ -367,6 +367,17 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
 int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
                           int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
                           float eps, uint16_t *z, void *stream);
+/* 512 x 512 Linear (w: fp16 [512 out][512 in], torch's layout; bias fp16 [512]) on `rows` contiguous fp16
+ * rows a[rows][512] with its epilogue, one launch (MFMA GEMM; the linear's fp16 output stays on chip):
+ *   mapf_linear512_gelu_dropout        out = dropout(gelu(a w^T + b)) fp16    = lin + mapf_gelu_dropout_f16
+ *   mapf_linear512_residual_layernorm  x += dropout(a w^T + b); z = LayerNorm(x) fp16
+ *                                                                  = lin + mapf_dropout_residual_layernorm
+ * The same dropout masks as those kernels for the same seed (only the GEMM's summation order differs). */
+int mapf_linear512_gelu_dropout(const uint16_t *a, const uint16_t *w, const uint16_t *bias, uint16_t *out, int64_t rows,
+                                float p, uint64_t seed, void *stream);
+int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                      const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
+                                      float p, uint64_t seed, void *stream);
 /* out[B][q_rows][512] = softmax(q k^T * scale) v per head (heads = 16, head_dim = 32, n <= 32 tokens;
  * fp16 in/out, fp32 scores and softmax, P rounded to fp16 for P.V like flash SDPA) --
  * transformer.py:48-85's attention for the first q_rows queries.  Strides in fp16 elements between

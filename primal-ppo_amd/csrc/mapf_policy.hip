@@ -377,6 +377,141 @@ inline int grid_for(long items, int per_block) {
     return (int)(g < 1 ? 1 : g);
 }
 
+// ---- 512 x 512 linear layers with their epilogues on the MFMA -------------------------
+// y = A W^T + b (torch Linear under autocast: fp16 operands, fp32 accumulation, the bias added
+// before the ONE rounding to fp16, as hipBLASLt's bias epilogue does), N = K = 512, then
+//   EPI 0  out = dropout(gelu(y))                  (MLP_Block af1 + do1: gelu_dropout_f16's arithmetic)
+//   EPI 1  x += dropout(y); z = LayerNorm(x) fp16  (Residual do1 / do2 + the next PreNorm:
+//          dropout_residual_layernorm's arithmetic)
+// with the same mask bits (float4 index row * 128 + col / 4 of the [M, 512] tensor) as the
+// separate launches, so only the GEMM's summation order differs from lin() + the epilogue kernel;
+// the linear's fp16 output never goes to HBM.  Workgroup: 64 rows x all 512 columns, 8 waves
+// as 2 (rows) x 4 (columns), 32 x 128 per wave (4 accumulators of v_mfma_f32_32x32x16_f16).  K in
+// chunks of 64 staged by LDS-DMA (A: 64 rows x 128 B, W: 512 rows x 128 B; two buffers, 144 KiB,
+// source-side XOR swizzle as csrc/mapf_conv.hip), then the fp16 y tile goes through LDS and each
+// wave takes whole rows for the elementwise epilogue (ln_row).
+typedef _Float16 gh8_t __attribute__((ext_vector_type(8)));
+typedef float gf16_t __attribute__((ext_vector_type(16)));
+constexpr int GL_BM = 64, GL_BK = 64, GL_D = 512;
+constexpr int GL_ABYTES = GL_BM * GL_BK * 2, GL_BBYTES = GL_D * GL_BK * 2, GL_BUF = GL_ABYTES + GL_BBYTES;
+constexpr int GL_LDS = 2 * GL_BUF;
+static_assert(GL_BM * GL_D * 2 <= GL_LDS, "epilogue tile");
+
+__device__ __attribute__((aligned(16))) uint4 g_lin_zero[1];    // source of the rows past M
+
+__device__ inline int gl_swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
+__device__ inline void gl_dma16(const void *src, void *lds) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+// byte offset of column n (fp16) of row r in the swizzled [64][512] fp16 epilogue tile
+__device__ inline int gl_tile(int r, int n) {
+    const int byte = n * 2;
+    return r * 1024 + (byte >> 7) * 128 + ((((byte >> 4) & 7) ^ (r & 7)) << 4) + (byte & 15);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
+                                                        const uint16_t *__restrict__ bias, long M,
+                                                        uint16_t *__restrict__ out, float *__restrict__ x,
+                                                        const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                        uint16_t *__restrict__ z, float eps, uint32_t thr, float scale,
+                                                        uint64_t seed) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const long m0 = (long)blockIdx.x * GL_BM;
+    const int q = (lane & 7) ^ ((lane >> 3) & 7);             // logical piece this lane fetches
+    const long rowA = m0 + 8 * wave + (lane >> 3);             // wave w fills A rows 8w..8w+7
+    const uint16_t *srcA = rowA < M ? A + rowA * GL_D + q * 8 : nullptr;
+    auto issue = [&](int c, int buf) {
+        char *As = smem + buf * GL_BUF;
+        char *Bs = As + GL_ABYTES;
+        gl_dma16(srcA ? (const void *)(srcA + c * GL_BK) : (const void *)g_lin_zero, As + 8 * wave * 128);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {                          // wave w fills W rows 64w..64w+63
+            const int n = 64 * wave + 8 * j + (lane >> 3);
+            gl_dma16(W + (size_t)n * GL_D + c * GL_BK + q * 8, Bs + (64 * wave + 8 * j) * 128);
+        }
+    };
+    const int wm = wave & 1, wn = wave >> 1, fr = lane & 31, fh = lane >> 5;
+    gf16_t acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+    constexpr int NCH = GL_D / GL_BK;
+    issue(0, 0);
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) {
+            issue(c + 1, (c + 1) & 1);
+            __builtin_amdgcn_s_waitcnt(0x0F70 | 9);            // vmcnt(9): chunk c's 9 copies have landed
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __builtin_amdgcn_s_barrier();
+        const char *As = smem + (c & 1) * GL_BUF;
+        const char *Bs = As + GL_ABYTES;
+#pragma unroll
+        for (int s = 0; s < GL_BK / 16; ++s) {
+            const int qq = 2 * s + fh;
+            const gh8_t af = *reinterpret_cast<const gh8_t *>(As + gl_swz(32 * wm + fr, qq));
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const gh8_t bf = *reinterpret_cast<const gh8_t *>(Bs + gl_swz(128 * wn + 32 * b + fr, qq));
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+    }
+    // y = fp16(acc + bias) -> LDS tile
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int n = 128 * wn + 32 * b + fr;
+        const float bv = h2f(bias[n]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            *reinterpret_cast<uint16_t *>(smem + gl_tile(row, n)) = (uint16_t)f2h(acc[b][r] + bv);
+        }
+    }
+    __syncthreads();
+    // elementwise epilogue: wave w takes rows w, w + 8, ...; lane holds columns 4l..4l+3 and 256+4l..
+    for (int row = wave; row < GL_BM; row += 8) {
+        const long g = m0 + row;
+        if (g >= M) break;
+        const uint2 y0 = *reinterpret_cast<const uint2 *>(smem + gl_tile(row, 4 * lane));
+        const uint2 y1 = *reinterpret_cast<const uint2 *>(smem + gl_tile(row, 256 + 4 * lane));
+        const long i0 = g * 128 + lane, i1 = i0 + 64;          // float4 indices of the [M, 512] tensor
+        const unsigned k0 = thr ? keep4(seed, (uint64_t)i0, thr) : 15u, k1 = thr ? keep4(seed, (uint64_t)i1, thr) : 15u;
+        if (EPI == 0) {
+            uint2 o[2];
+            const uint2 yv[2] = {y0, y1};
+            const unsigned kk[2] = {k0, k1};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t in[4] = {yv[h].x, yv[h].x >> 16, yv[h].y, yv[h].y >> 16};
+                uint32_t r4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float a = h2f(in[e]);
+                    const float gl = h2f(f2h(0.5f * a * (1.f + erff(a * 0.70710678118654752f))));
+                    r4[e] = ((kk[h] >> e) & 1u) ? f2h(gl * scale) : 0u;
+                }
+                o[h] = pack4(r4[0], r4[1], r4[2], r4[3]);
+            }
+            reinterpret_cast<uint2 *>(out)[i0] = o[0];
+            reinterpret_cast<uint2 *>(out)[i1] = o[1];
+        } else {
+            float4 *xr = reinterpret_cast<float4 *>(x);
+            const float4 a = add_dropped(xr[i0], y0, k0, scale);
+            const float4 c = add_dropped(xr[i1], y1, k1, scale);
+            xr[i0] = a;
+            xr[i1] = c;
+            ln_row(a, c, lane, gamma, beta, eps, z + g * 512);
+        }
+    }
+}
+
 }  // namespace pol
 }  // namespace mapf
 
@@ -436,6 +571,27 @@ int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *
     if (n == 0) return MAPF_OK;
     hipLaunchKernelGGL(pol::gelu_dropout_f16, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, h,
                        (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_linear512_gelu_dropout(const uint16_t *a, const uint16_t *w, const uint16_t *bias, uint16_t *out, int64_t rows,
+                                float p, uint64_t seed, void *stream) {
+    if (!a || !w || !bias || !out || rows < 0 || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::linear512_kernel<0>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
+                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, out, nullptr, nullptr, nullptr,
+                       nullptr, 0.f, pol::drop_threshold(p), 1.f / (1.f - p), seed);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                      const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
+                                      float p, uint64_t seed, void *stream) {
+    if (!a || !w || !bias || !x || !gamma || !beta || !z || rows < 0 || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
+                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
+                       pol::drop_threshold(p), 1.f / (1.f - p), seed);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

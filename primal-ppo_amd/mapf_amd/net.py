@@ -180,6 +180,7 @@ class SCRIMPNet(nn.Module):
         self.fused_attention = True   # short-sequence attention kernel (mapf_attention_f16) instead of SDPA
         self.fused_residual_ln = True  # residual + next LayerNorm in one pass (mapf_dropout_residual_layernorm)
         self.own_conv = True           # 128/256-channel convolutions as the MFMA implicit GEMM (mapf_conv_nhwc_f16)
+        self.fused_linear = True       # 512x512 linears + their dropout/residual/LayerNorm or GELU epilogue, one launch
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
 
     _OWN_CONV = {(128, 128, 3), (128, 256, 2), (256, 256, 2)}    # (Cin, Cout, kernel) of mapf_conv_nhwc_f16
@@ -368,6 +369,29 @@ class SCRIMPNet(nn.Module):
                                                     x.numel() // d, d, float(norm.eps), drop(m), next(seeds), st))
             return z
 
+        fused_lin = self.fused_linear and d == 512 and self.fused_residual_ln
+
+        def lin_residual(m, inp, x, drop_m, norm):     # x += dropout(m(inp)); LayerNorm(x) -> fp16, one launch
+            if not fused_lin or norm is None or m.weight.shape != (512, 512):
+                return residual(x, lin(m, inp), drop_m, norm)
+            inp = inp.contiguous()
+            z = torch.empty(x.shape, dtype=torch.float16, device=x.device)
+            chk(lib.mapf_linear512_residual_layernorm(ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x),
+                                                      ptr(norm.weight), ptr(norm.bias), ptr(z), x.numel() // d,
+                                                      float(norm.eps), drop(drop_m), next(seeds), st))
+            return z
+
+        def lin_gelu(m, inp, drop_m):                   # dropout(gelu(m(inp))), one launch
+            if not fused_lin or m.weight.shape != (512, 512):
+                hid = lin(m, inp).contiguous()
+                chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(drop_m), next(seeds), st))
+                return hid
+            inp = inp.contiguous()
+            hid = torch.empty(inp.shape[:-1] + (512,), dtype=torch.float16, device=inp.device)
+            chk(lib.mapf_linear512_gelu_dropout(ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(hid),
+                                                inp.numel() // 512, drop(drop_m), next(seeds), st))
+            return hid
+
         def attend(q, k, v, rows, q_ts, kv_ts, a):     # fp16 [b, rows, d], heads concatenated
             o = torch.empty(b, rows, d, dtype=torch.float16, device=x.device)
             chk(lib.mapf_attention_f16(ptr(q), ptr(k), ptr(v), ptr(o), b, n, rows, q_ts, q_ts * (n if rows > 1 else 1),
@@ -389,7 +413,7 @@ class SCRIMPNet(nn.Module):
                     qkv = qkv.view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
                     out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, n, d)
-                yf = residual(x, lin(a.nn1, out), a.do1, ff.fn.norm)
+                yf = lin_residual(a.nn1, out, x, a.do1, ff.fn.norm)
             else:                               # the last block: token 0's query only (see _Encoder)
                 w, bias = a.to_qkv.weight, a.to_qkv.bias
                 q = F.linear(y[:, 0], h16(w, "q"), h16(bias, "q"))
@@ -403,8 +427,7 @@ class SCRIMPNet(nn.Module):
                     out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, 1, d)
                 x = x[:, :1].contiguous()
-                yf = residual(x, lin(a.nn1, out), a.do1, ff.fn.norm)
-            hid = lin(f.nn1, yf).contiguous()
-            chk(lib.mapf_gelu_dropout_f16(ptr(hid), hid.numel(), drop(f.do1), next(seeds), st))
-            y = residual(x, lin(f.nn2, hid), f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
+                yf = lin_residual(a.nn1, out, x, a.do1, ff.fn.norm)
+            hid = lin_gelu(f.nn1, yf, f.do1)
+            y = lin_residual(f.nn2, hid, x, f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
         return x

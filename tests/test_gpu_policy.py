@@ -26,7 +26,7 @@ def _net(n_agents=8):
 @pytest.mark.parametrize("B,own", [(5, True), (256, True), (256, False)])
 def test_fused_acting_forward_matches_torch_path(B, own):
     net = _net().eval()                        # dropout off: both paths deterministic
-    net.fused_attention = net.fused_residual_ln = net.own_conv = own
+    net.fused_attention = net.fused_residual_ln = net.own_conv = net.fused_linear = own
     g = torch.Generator(device="cuda").manual_seed(B)
     obs = (torch.rand(B, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
     vec = torch.randn(B, 8, 4, device="cuda", generator=g)
@@ -229,3 +229,43 @@ def test_conv_kernel_rejects_other_shapes():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     assert _lib.lib().mapf_conv_nhwc_f16(_p(x), _p(x), _p(x), _p(x), 1, 9, 9, 6, 128, 3, 1, 1, st) == -1
     assert _lib.lib().mapf_conv_nhwc_f16(_p(x), _p(x), _p(x), _p(x), 1, 9, 9, 128, 128, 3, 3, 1, st) == -1
+
+
+@pytest.mark.parametrize("rows", [1, 63, 64, 1000])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_linear512_epilogues_equal_linear_then_epilogue(rows, p):
+    """mapf_linear512_gelu_dropout / _residual_layernorm (MFMA GEMM + epilogue, one launch) == torch's
+    fp16 Linear followed by mapf_gelu_dropout_f16 / mapf_dropout_residual_layernorm with the same
+    seed: the same dropout masks (every dropped element dropped in both), values to fp16 rounding of
+    the GEMM's other summation order; ragged row counts (the last workgroup's rows past M)."""
+    from mapf_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a = torch.randn(rows, 512, device="cuda", generator=g).half()
+    w = (torch.randn(512, 512, device="cuda", generator=g) / 512 ** 0.5).half()
+    b = (torch.randn(512, device="cuda", generator=g) * 0.1).half()
+    seed = 1234 + rows
+    # GELU + dropout
+    ref = torch.nn.functional.linear(a, w, b).contiguous()
+    _lib.check(L.mapf_gelu_dropout_f16(_p(ref), ref.numel(), p, seed, st))
+    out = torch.full_like(ref, float("nan"))
+    _lib.check(L.mapf_linear512_gelu_dropout(_p(a), _p(w), _p(b), _p(out), rows, p, seed, st))
+    torch.cuda.synchronize()
+    assert torch.equal(out == 0, ref == 0) or p == 0.0
+    torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    # dropout + residual + LayerNorm
+    gamma = 1 + 0.1 * torch.randn(512, device="cuda", generator=g)
+    beta = 0.1 * torch.randn(512, device="cuda", generator=g)
+    x0 = torch.randn(rows, 512, device="cuda", generator=g)
+    x1, z1 = x0.clone(), torch.empty(rows, 512, dtype=torch.float16, device="cuda")
+    y = torch.nn.functional.linear(a, w, b).contiguous()
+    _lib.check(L.mapf_dropout_residual_layernorm(_p(x1), _p(y), _p(gamma), _p(beta), _p(z1), rows, 512, 1e-5, p,
+                                                 seed, st))
+    x2, z2 = x0.clone(), torch.full((rows, 512), float("nan"), dtype=torch.float16, device="cuda")
+    _lib.check(L.mapf_linear512_residual_layernorm(_p(a), _p(w), _p(b), _p(x2), _p(gamma), _p(beta), _p(z2), rows,
+                                                   1e-5, p, seed, st))
+    torch.cuda.synchronize()
+    assert torch.equal(x2 == x0, x1 == x0)            # the same elements dropped
+    torch.testing.assert_close(x2, x1, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(z2.float(), z1.float(), rtol=2e-2, atol=2e-2)

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--no-find", action="store_true", help="torch.backends.cudnn.benchmark off (no MIOpen find)")
     ap.add_argument("--torch-path", action="store_true", help="the PyTorch forward, not the fused acting path")
     ap.add_argument("--miopen-conv", action="store_true", help="MIOpen for every convolution (no mapf_conv_nhwc_f16)")
+    ap.add_argument("--unfused-linear", action="store_true", help="hipBLASLt linears + separate epilogue kernels")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
     from mapf_amd.model import Model
@@ -36,6 +37,7 @@ def main():
         torch.backends.cudnn.benchmark = False
     model.network.fused_acting = not args.torch_path
     model.network.own_conv = not args.miopen_conv
+    model.network.fused_linear = not args.unfused_linear
     for _ in range(3):
         model.step(obs, vec, None)
     torch.cuda.synchronize()
@@ -44,7 +46,7 @@ def main():
         model.step(obs, vec, None)
     torch.cuda.synchronize()
     print(f"model.step: {(time.perf_counter() - t0) / 10 * 1e3:.2f} ms for {B * N} agents "
-          f"(own conv {model.network.own_conv})", flush=True)
+          f"(own conv {model.network.own_conv}, fused linear {model.network.fused_linear})", flush=True)
     if args.no_profile:
         return
     from torch.profiler import ProfilerActivity, profile
