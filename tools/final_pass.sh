@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=${TAG:-r04}
-for st in ${STEPS:-pytest smoke bench profile}; do
+for st in ${STEPS:-pytest smoke bench profile rollout}; do
   case "$st" in
     pytest)
       timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v ${PYTEST_ARGS:-} --timeout 300 --timeout-method thread \
@@ -29,5 +29,12 @@ for st in ${STEPS:-pytest smoke bench profile}; do
       done ;;
     profile)
       CONFIGS="${CONFIGS:-c2 c4 c5}" bash tools/c45_profile.sh || exit 1 ;;
+    rollout)   # c3: policy in the loop (4096 x 8, FOV 9) + PPO updates; c4-shaped updates (1024 x 16, 40x40)
+      timeout -k 10 400 python3 tools/bench_rollout.py --train > gpurun_out/${TAG}_rollout_c3.jsonl 2>&1 \
+        || { tail -5 gpurun_out/${TAG}_rollout_c3.jsonl; exit 1; }
+      grep '^{' gpurun_out/${TAG}_rollout_c3.jsonl | cut -c1-300
+      timeout -k 10 400 python3 tools/bench_rollout.py --envs 1024 --agents 16 --size 40 --train \
+        > gpurun_out/${TAG}_rollout_c4.jsonl 2>&1 || { tail -5 gpurun_out/${TAG}_rollout_c4.jsonl; exit 1; }
+      grep '^{' gpurun_out/${TAG}_rollout_c4.jsonl | cut -c1-300 ;;
   esac
 done
