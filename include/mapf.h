@@ -412,6 +412,13 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
                        int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, int32_t relu,
                        void *stream);
 
+/* conv1 (net.py:104, 3x3, padding 1, Cin = num_channel <= 7, Cout = 128) from the fp32 NCHW observation
+ * x_nchw [nimg][Cin][H][W] (cast to fp16 as autocast does); w fp16 [Cout][Cin][3][3] (torch's layout);
+ * y fp16 NHWC [nimg][H][W][Cout] = relu(fp16(fp16(conv) + bias)) -- the MIOpen path's NHWC copy, cast,
+ * conv and mapf_nhwc_bias_relu in one launch. */
+int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                        int32_t Cin, int32_t H, int32_t W, int32_t Cout, void *stream);
+
 /* mapf_ppo_loss with coef[6] in DEVICE memory (captured-graph updates: the Lagrangian term changes
  * every update without re-capturing). */
 int mapf_ppo_loss_dcoef(const float *new_ps, const float *old_ps, const int64_t *action, const float *new_v,

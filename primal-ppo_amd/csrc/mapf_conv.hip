@@ -184,6 +184,106 @@ static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, 
                        C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi);
 }
 
+// The first convolution (conv1, net.py:104: Cin = num_channel <= 7, 3x3, padding 1) straight from
+// the fp32 NCHW observation: K = Cin * 9 <= 63 (torch's (c, ky, kx) order, padded to 64 with zeros)
+// is ONE chunk, so each workgroup builds its 128 im2col rows in LDS from the observation (cast to
+// fp16 as autocast does), multiplies by the whole weight (Cout x 64, LDS) and writes
+// relu(fp16(fp16(acc) + bias)) as NHWC fp16 -- the observation's NHWC copy and cast, the conv and
+// the bias / ReLU pass of the MIOpen path in one launch.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict__ in, const uint16_t *__restrict__ w,
+                                                         const uint16_t *__restrict__ bias, uint16_t *__restrict__ out,
+                                                         int M, int C, int H, int W) {
+    constexpr int BM = 128, NT = COUT / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *As = smem, *Bs = smem + BM * 128;
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int m0 = (int)blockIdx.x * BM;
+    const int HW = H * W, K = C * 9;
+    // im2col rows: thread t builds half a row (32 k) of row t >> 1
+    {
+        const int r = t >> 1, kh = (t & 1) * 32, m = m0 + r;
+        int img = 0, oy = -1000, ox = 0;
+        if (m < M) {
+            img = m / HW;
+            const int pos = m - img * HW;
+            oy = pos / W;
+            ox = pos - oy * W;
+        }
+        const float *src = in + (size_t)img * C * HW;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {              // 4 pieces of 8 k
+            uint32_t hv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = kh + 8 * q + e;
+                const int c = k / 9, tap = k - c * 9, iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+                float v = 0.f;
+                if (k < K && iy >= 0 && iy < H && ix >= 0 && ix < W) v = src[(size_t)c * HW + iy * W + ix];
+                hv[e] = f2h(v);
+            }
+            const uint4 pk = make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
+                                        hv[6] | (hv[7] << 16));
+            *reinterpret_cast<uint4 *>(As + swz(r, (kh >> 3) + q)) = pk;
+        }
+    }
+    // the weight, zero-padded to K = 64: thread t builds 16-B pieces of rows t >> 3 + 32 i
+    for (int p = t; p < COUT * 8; p += 256) {
+        const int n = p >> 3, q = p & 7;
+        uint32_t hv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 8 * q + e;
+            hv[e] = k < K ? (uint32_t)w[(size_t)n * K + k] : 0u;
+        }
+        *reinterpret_cast<uint4 *>(Bs + swz(n, q)) =
+            make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+    }
+    __syncthreads();
+    const int fr = lane & 31, fh = lane >> 5;
+    f16_t acc[NT];
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int qq = 2 * s + fh;
+        const h8_t af = *reinterpret_cast<const h8_t *>(As + swz(wave * 32 + fr, qq));
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+            const h8_t bf = *reinterpret_cast<const h8_t *>(Bs + swz(b * 32 + fr, qq));
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+        }
+    }
+    __syncthreads();                                // As / Bs reads done: the tile reuses the LDS
+    char *T = smem;
+    constexpr int RB = COUT * 2;
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+        const int n = b * 32 + fr;
+        const float bv = h2f(bias[n]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            const float v = fmaxf(h2f(f2h(h2f(f2h(acc[b][r])) + bv)), 0.f);
+            const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
+            *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
+                (uint16_t)f2h(v);
+        }
+    }
+    __syncthreads();
+    constexpr int PIECES_ROW = RB / 16;
+    for (int p = t; p < BM * PIECES_ROW; p += 256) {
+        const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
+        const int m = m0 + row;
+        if (m >= M) continue;
+        const int g = pc >> 3, pq = pc & 7;
+        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) =
+            *reinterpret_cast<const uint4 *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4));
+    }
+}
+
 }  // namespace conv
 }  // namespace mapf
 
@@ -206,6 +306,20 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
     else if (Cin == 128 && Cout == 256 && ks == 2) conv::launch<128, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else return MAPF_EINVAL;
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                        int32_t Cin, int32_t H, int32_t W, int32_t Cout, void *stream) {
+    if (!x_nchw || !w || !bias || !y) return MAPF_EINVAL;
+    if (nimg < 1 || Cin < 1 || Cin > 7 || H < 1 || W < 1 || Cout != 128) return MAPF_EINVAL;
+    const int64_t M64 = nimg * H * W;
+    if (M64 > (int64_t)0x7FFFFFFF - 1024) return MAPF_EINVAL;
+    const int M = (int)M64;
+    const size_t lds = (size_t)128 * Cout * 2 > (size_t)128 * 128 + (size_t)Cout * 128 ? (size_t)128 * Cout * 2
+                                                                                       : (size_t)128 * 128 + (size_t)Cout * 128;
+    hipLaunchKernelGGL(conv::conv_first_kernel<128>, dim3((M + 127) / 128), dim3(256), lds, (hipStream_t)stream, x_nchw,
+                       w, bias, y, M, (int)Cin, (int)H, (int)W);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

@@ -253,7 +253,7 @@ class SCRIMPNet(nn.Module):
         with torch.autocast(device_type="cuda"):
             n_agents = self.num_agents or EnvParameters.N_AGENTS
             F_ = self.fov or obs.shape[-1]
-            x = obs.reshape(-1, self.num_channel, F_, F_).contiguous(memory_format=torch.channels_last)
+            x = obs.reshape(-1, self.num_channel, F_, F_)
             v = vector.reshape(-1, NetParameters.VECTOR_LEN)
 
             def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
@@ -289,7 +289,17 @@ class SCRIMPNet(nn.Module):
                 return y
             # (a pooled layer's raw output takes bias + ReLU + pool in one pass: mapf_nhwc_bias_relu_pool2)
 
-            x = conv(conv(conv(x, self.conv1), self.conv1a), self.conv1b, pool=True)
+            xin = obs.reshape(-1, self.num_channel, F_, F_)
+            if (self.own_conv and self.num_channel <= 7 and self.conv1.weight.shape[0] == 128 and
+                    xin.dtype == torch.float32 and xin.is_contiguous()):
+                # conv1 from the fp32 NCHW observation: cast, im2col, MFMA, bias + ReLU in one launch
+                x1 = torch.empty((xin.shape[0], 128, F_, F_), dtype=torch.float16, device=dev,
+                                 memory_format=torch.channels_last)
+                chk(lib.mapf_conv_first_f32(ptr(xin), ptr(h16(self.conv1.weight)), ptr(h16(self.conv1.bias)),
+                                            ptr(x1), xin.shape[0], self.num_channel, F_, F_, 128, st))
+            else:
+                x1 = conv(x.contiguous(memory_format=torch.channels_last), self.conv1)
+            x = conv(conv(x1, self.conv1a), self.conv1b, pool=True)
             x = conv(conv(conv(x, self.conv2), self.conv2a), self.conv2b, pool=True)
             x = conv(x, self.conv3).flatten(1)
             g = F.relu(lin(self.fully_connected_1, v))

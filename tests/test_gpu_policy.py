@@ -269,3 +269,23 @@ def test_linear512_epilogues_equal_linear_then_epilogue(rows, p):
     assert torch.equal(x2 == x0, x1 == x0)            # the same elements dropped
     torch.testing.assert_close(x2, x1, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(z2.float(), z1.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("C,H,B", [(6, 9, 37), (6, 11, 5), (7, 9, 130), (5, 9, 1)])
+def test_conv_first_kernel_vs_torch(C, H, B):
+    """mapf_conv_first_f32 (conv1 from the fp32 NCHW observation, one MFMA chunk) == autocast conv1
+    + bias + ReLU to fp16 rounding; 0/1 observations as the env writes them and general values."""
+    from mapf_amd import _lib
+    g = torch.Generator(device="cuda").manual_seed(C * 100 + B)
+    for obs in ((torch.rand(B, C, H, H, device="cuda", generator=g) < 0.3).float(),
+                torch.randn(B, C, H, H, device="cuda", generator=g)):
+        w = (torch.randn(128, C, 3, 3, device="cuda", generator=g) / (C * 9) ** 0.5).half()
+        b = (torch.randn(128, device="cuda", generator=g) * 0.1).half()
+        ref = torch.nn.functional.conv2d(obs.half().float(), w.float(), None, 1, 1).half()
+        ref = torch.relu((ref.float() + b.float()).half().float()).half()
+        y = torch.full((B, 128, H, H), float("nan"), dtype=torch.float16, device="cuda").contiguous(
+            memory_format=torch.channels_last)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(_lib.lib().mapf_conv_first_f32(_p(obs), _p(w.contiguous()), _p(b), _p(y), B, C, H, H, 128, st))
+        torch.cuda.synchronize()
+        torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
