@@ -212,7 +212,7 @@ def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
     b = torch.randn(co, device="cuda", generator=g).half()
     ref = torch.nn.functional.conv2d(x.float(), w.float(), None, 1, 1).half()
     if relu:
-        ref = torch.relu((ref.float() + b.float()).half().float()).half()
+        ref = torch.relu((ref.float() + b.float().view(1, -1, 1, 1)).half().float()).half()
     Ho = H + 2 - ks + 1
     y = torch.full((B, co, Ho, Ho), float("nan"), dtype=torch.float16, device="cuda").contiguous(memory_format=cl)
     wp = w.permute(0, 2, 3, 1).contiguous()
@@ -282,7 +282,7 @@ def test_conv_first_kernel_vs_torch(C, H, B):
         w = (torch.randn(128, C, 3, 3, device="cuda", generator=g) / (C * 9) ** 0.5).half()
         b = (torch.randn(128, device="cuda", generator=g) * 0.1).half()
         ref = torch.nn.functional.conv2d(obs.half().float(), w.float(), None, 1, 1).half()
-        ref = torch.relu((ref.float() + b.float()).half().float()).half()
+        ref = torch.relu((ref.float() + b.float().view(1, -1, 1, 1)).half().float()).half()
         y = torch.full((B, 128, H, H), float("nan"), dtype=torch.float16, device="cuda").contiguous(
             memory_format=torch.channels_last)
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
