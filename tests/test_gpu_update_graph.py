@@ -43,9 +43,15 @@ def test_graphed_updates_equal_eager_updates():
         s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         m4.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-        assert all(np.isfinite(float(x)) for x in s1), (k, s1)
+        # (grad_norm, stats[8], is inf when the fp16 backward overflowed: the AMP step is then
+        # skipped on the device and the scale halved -- in both models alike)
+        assert all(np.isfinite(float(x)) for i, x in enumerate(s1) if i != 8), (k, s1)
         for i, (a, b) in enumerate(zip(s1, s2)):
-            assert abs(float(a) - float(b)) <= 2e-3 * max(1.0, abs(float(b))), (k, i, a, b)
+            a, b = float(a), float(b)
+            if i == 8 and not (np.isfinite(a) and np.isfinite(b)):
+                assert np.isinf(a) == np.isinf(b), (k, a, b)
+                continue
+            assert abs(a - b) <= 2e-3 * max(1.0, abs(b)), (k, i, a, b)
         assert len(m1.network._h16) == 0        # the acting path's fp16 weights are re-read
     upd = next(iter(m1._updates.values()))
     assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
