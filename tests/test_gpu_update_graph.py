@@ -42,7 +42,7 @@ def test_graphed_updates_equal_eager_updates():
     for k, (obs, vec, ret, cret, v, cv, act, ps, tv) in enumerate(batches):
         s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-        m4.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
+        s4 = m4.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
         # (grad_norm, stats[8], is inf when the fp16 backward overflowed: the AMP step is then
         # skipped on the device and the scale halved -- in both models alike)
         assert all(np.isfinite(float(x)) for i, x in enumerate(s1) if i != 8), (k, s1)
@@ -51,7 +51,12 @@ def test_graphed_updates_equal_eager_updates():
             if i == 8 and not (np.isfinite(a) and np.isfinite(b)):
                 assert np.isinf(a) == np.isinf(b), (k, a, b)
                 continue
-            assert abs(a - b) <= 2e-3 * max(1.0, abs(b)), (k, i, a, b)
+            # the gradient norm is the stat most sensitive to the weights' run-to-run drift (see
+            # below): held to 2 % or to the eager twins' own spread at this update
+            tol = 2e-3 * max(1.0, abs(b))
+            if i == 8 and k > 0:
+                tol = max(2e-2 * abs(b), 3 * abs(float(s4[i]) - b))
+            assert abs(a - b) <= tol, (k, i, a, b, float(s4[i]))
         assert len(m1.network._h16) == 0        # the acting path's fp16 weights are re-read
     upd = next(iter(m1._updates.values()))
     assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
