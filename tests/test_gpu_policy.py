@@ -43,6 +43,31 @@ def test_fused_acting_forward_matches_torch_path(B, own):
         torch.testing.assert_close(o.float(), r.float(), rtol=3e-2, atol=3e-2, msg=name)
 
 
+@pytest.mark.parametrize("own_conv,fused_linear,training", [(True, True, False), (True, False, False),
+                                                              (True, True, True)])
+def test_fused_acting_forward_is_deterministic(own_conv, fused_linear, training):
+    """the acting forward is a function of weights and inputs: bit-identical over repeated
+    calls and on a deep copy of the network (a kernel that reads memory it did not write, or
+    races on LDS, shows up here first)"""
+    import copy
+    net = _net().train(training)               # training: dropout on, masks from the seeded Philox stream
+    net.own_conv, net.fused_linear = own_conv, fused_linear
+    g = torch.Generator(device="cuda").manual_seed(9)
+    obs = (torch.rand(300, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
+    vec = torch.randn(300, 8, 4, device="cuda", generator=g)
+    twin = copy.deepcopy(net)
+    with torch.no_grad():
+        call = lambda m: (torch.manual_seed(4), m(obs, vec))[1]    # noqa
+        runs = [call(net) for _ in range(3)] + [call(twin)]
+        junk = torch.full((1 << 26,), float("nan"), device="cuda")   # recycle the freed blocks as NaN
+        del junk
+        runs.append(call(net))
+    names = ["policy", "value", "blocking", "policy_sig", "x", "logits", "cost_value"]
+    for j, r in enumerate(runs[1:], 1):
+        bad = [n for n, a, b in zip(names, runs[0], r) if not torch.equal(a, b)]
+        assert not bad, (j, bad, [(a.float() - b.float()).abs().max().item() for a, b in zip(runs[0], r)])
+
+
 def test_training_forward_keeps_torch_ops():
     net = _net()
     obs = (torch.rand(4, 8, 6, 9, 9, device="cuda") < 0.25).float()
