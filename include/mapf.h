@@ -413,7 +413,8 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
                        void *stream);
 
 /* conv1 (net.py:104, 3x3, padding 1, Cin = num_channel <= 7, Cout = 128) from the fp32 NCHW observation
- * x_nchw [nimg][Cin][H][W] (cast to fp16 as autocast does); w fp16 [Cout][Cin][3][3] (torch's layout);
+ * x_nchw [nimg][Cin][H][W] (cast to fp16 as autocast does); w fp16 [Cout][64]: torch's [Cout][Cin][3][3]
+ * flattened per output channel (K = Cin * 9 in (c, ky, kx) order) and zero-padded to 64;
  * y fp16 NHWC [nimg][H][W][Cout] = relu(fp16(fp16(conv) + bias)) -- the MIOpen path's NHWC copy, cast,
  * conv and mapf_nhwc_bias_relu in one launch. */
 int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *bias, uint16_t *y, int64_t nimg,

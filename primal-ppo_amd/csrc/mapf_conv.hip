@@ -16,10 +16,10 @@
 // each).  K loop over 64-wide chunks staged by LDS-DMA (global_load_lds_dwordx4: no staging
 // registers) into two LDS buffers: chunk c + 1's copies are in flight while the matrix cores
 // work on chunk c (a counted vmcnt retires only chunk c's, then a raw barrier).  LDS rows are
-// 128 B with the 16-B pieces XOR-swizzled by row & 7 -- on the SOURCE side: a DMA instruction
-// writes its 64 lanes' 16 B linearly (8 rows x 8 pieces), so lane l fetches logical piece
-// (l & 7) ^ (row & 7) -- and the 32 rows a ds_read_b128 fragment load touches spread over
-// every bank.  Taps in the padding fetch 16 zero bytes (a zero block in the code object).
+// 128 B with the 16-B pieces XOR-swizzled by (row >> 1) & 7 (swz below) -- on the SOURCE side: a
+// DMA instruction writes its 64 lanes' 16 B linearly (8 rows x 8 pieces), so lane l fetches the
+// logical piece that lands in its physical slot -- and each 16-lane group of a ds_read_b128
+// fragment load gets 16 distinct bank slots.  Taps in the padding fetch 16 zero bytes (a zero block in the code object).
 // Epilogue: fp32 accumulators -> fp16 (the conv's own rounding), optionally + bias (rounded
 // again, as torch adds the bias to the fp16 conv output) and ReLU -- through an LDS transpose
 // so every output row leaves as 16-B stores.
@@ -38,6 +38,24 @@ constexpr int BK = 64;              // K per chunk: 64 fp16 = one 128-B row per 
 
 __device__ __attribute__((aligned(16))) uint4 g_zero16[1];   // the padding taps' source (zero-initialised)
 
+// byte offset of 16-B piece q of row r in a swizzled 128-B-row tile.  ds_read_b128 serves a wave in
+// four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32), each conflict-free
+// when its 16 lanes hit the 16 distinct 16-B slots of the 256-B bank row; a fragment load reads rows
+// 0..31 (lane & 31) at one piece, and two 128-B rows share a bank row, so the XOR key is
+// (r >> 1) & 7: with r & 1 it gives every row of a group its own slot ((r & 7) would pair rows
+// r and r + 8 of a group on one slot: 2-way).
+__device__ inline int swz_key(int r) { return (r >> 1) & 7; }
+__device__ inline int swz(int r, int q) { return r * 128 + ((q ^ swz_key(r)) << 4); }
+// the logical piece lane l fetches when one DMA instruction fills rows 8 g .. 8 g + 7 lane-linearly
+__device__ inline int dma_piece(int lane, int g) { return (lane & 7) ^ swz_key(8 * g + (lane >> 3)); }
+
+__device__ inline uint32_t f2h(float f) { return (uint32_t)__half_as_ushort(__float2half_rn(f)); }
+__device__ inline float h2f(uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xFFFFu))); }
+
+__device__ inline void dma16(const void *src, void *lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
+
 template <int CIN, int COUT, int KS, int WAVES>
 struct Cfg {
     static constexpr int THREADS = 64 * WAVES;
@@ -54,16 +72,6 @@ struct Cfg {
     static_assert(JA + JB <= 15, "vmcnt field");
 };
 
-// byte offset of 16-B piece q of row r in a swizzled 128-B-row tile
-__device__ inline int swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
-
-__device__ inline uint32_t f2h(float f) { return (uint32_t)__half_as_ushort(__float2half_rn(f)); }
-__device__ inline float h2f(uint32_t h) { return __half2float(__ushort_as_half((unsigned short)(h & 0xFFFFu))); }
-
-__device__ inline void dma16(const void *src, void *lds_base) {
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
-}
-
 // epi: 0 = raw fp16 conv output, 1 = + bias, ReLU
 template <int CIN, int COUT, int KS, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *__restrict__ in,
@@ -77,8 +85,9 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int m0 = (int)blockIdx.x * C::BM;
     const int HWo = Ho * Wo;
-    // lane l of a DMA instruction fills row 8j + (l >> 3), physical piece l & 7 = logical piece q
-    const int q = (lane & 7) ^ ((lane >> 3) & 7);
+    // lane l of a DMA instruction filling rows 8 g .. 8 g + 7 writes row 8 g + (l >> 3), physical
+    // piece l & 7 = logical piece dma_piece(l, g), which depends on g only through its parity
+    const int q0 = dma_piece(lane, 0), q1 = dma_piece(lane, 1);
     // this lane's A rows (one per DMA instruction): the output pixel's input pixel index and (oy, ox)
     int apix[C::JA], ayx[C::JA];
 #pragma unroll
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *
             ayx[j] = (oy << 16) | ox;
         } else {
             apix[j] = 0;
-            ayx[j] = (-30000 << 16);               // every tap out of range
+            ayx[j] = (int)0x80000000u;             // every tap out of range
         }
     }
     auto issue = [&](int c, int buf) {             // chunk c -> LDS buffer buf (DMA, in flight)
@@ -102,14 +111,16 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *
 #pragma unroll
         for (int j = 0; j < C::JA; ++j) {
             const int iy = (ayx[j] >> 16) + ky - pad, ix = (ayx[j] & 0xFFFF) + kx - pad;
-            const void *src = (iy >= 0 && iy < H && ix >= 0 && ix < W)
-                                  ? (const void *)(in + (size_t)(apix[j] + dpix) * CIN + cb * BK + q * 8)
-                                  : (const void *)g_zero16;
+            const bool ok = ((unsigned)iy < (unsigned)H) & ((unsigned)ix < (unsigned)W);
+            const int q = ((wave * C::JA + j) & 1) ? q1 : q0;
+            const void *src = ok ? (const void *)(in + (size_t)(apix[j] + dpix) * CIN + cb * BK + q * 8)
+                                 : (const void *)g_zero16;
             dma16(src, A + 8 * (wave * C::JA + j) * 128);
         }
 #pragma unroll
         for (int j = 0; j < C::JB; ++j) {
             const int n = 8 * (wave * C::JB + j) + (lane >> 3);
+            const int q = ((wave * C::JB + j) & 1) ? q1 : q0;
             dma16(w + (size_t)n * C::K + c * BK + q * 8, B + 8 * (wave * C::JB + j) * 128);
         }
     };
@@ -185,102 +196,100 @@ static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, 
 }
 
 // The first convolution (conv1, net.py:104: Cin = num_channel <= 7, 3x3, padding 1) straight from
-// the fp32 NCHW observation: K = Cin * 9 <= 63 (torch's (c, ky, kx) order, padded to 64 with zeros)
-// is ONE chunk, so each workgroup builds its 128 im2col rows in LDS from the observation (cast to
-// fp16 as autocast does), multiplies by the whole weight (Cout x 64, LDS) and writes
-// relu(fp16(fp16(acc) + bias)) as NHWC fp16 -- the observation's NHWC copy and cast, the conv and
-// the bias / ReLU pass of the MIOpen path in one launch.
+// the fp32 NCHW observation: K = Cin * 9 <= 63 (torch's (c, ky, kx) order, zero-padded to 64: the
+// packed weight is [Cout][64] fp16) is ONE chunk.  A workgroup of 128 output pixels copies the
+// (at most (127 / HW) + 2) images they lie in, cast to fp16 as autocast does, into an LDS image
+// with a zero border; builds its 128 im2col rows from it (each (pixel, channel) writes its 9 taps);
+// multiplies them by the weight, whose fragments every wave holds in registers (the MFMA row
+// operand, read once from L2); and writes relu(fp16(fp16(acc) + bias)) as NHWC fp16 from
+// registers (C^T accumulators: 4 consecutive channels of a pixel per 8-B store) -- the MIOpen
+// path's NHWC copy and cast, the conv and the bias / ReLU pass in one launch.
 template <int COUT>
 __global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict__ in, const uint16_t *__restrict__ w,
                                                          const uint16_t *__restrict__ bias, uint16_t *__restrict__ out,
-                                                         int M, int C, int H, int W) {
+                                                         int M, int C, int H, int W, int nimg) {
     constexpr int BM = 128, NT = COUT / 32;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *As = smem, *Bs = smem + BM * 128;
+    char *As = smem;                                   // [128][64] fp16 im2col rows, swizzled
+    uint16_t *Img = reinterpret_cast<uint16_t *>(smem + BM * 128);   // [n][C][H + 2][W + 2] fp16
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int fr = lane & 31, fh = lane >> 5;
     const int m0 = (int)blockIdx.x * BM;
-    const int HW = H * W, K = C * 9;
-    // im2col rows: thread t builds half a row (32 k) of row t >> 1
-    {
-        const int r = t >> 1, kh = (t & 1) * 32, m = m0 + r;
-        int img = 0, oy = -1000, ox = 0;
-        if (m < M) {
-            img = m / HW;
-            const int pos = m - img * HW;
-            oy = pos / W;
-            ox = pos - oy * W;
-        }
-        const float *src = in + (size_t)img * C * HW;
+    const int HW = H * W, K = C * 9, PW = W + 2, PP = (H + 2) * PW;
+    const int img_lo = m0 / HW;
+    int img_hi = (m0 + BM - 1) / HW;
+    if (img_hi > nimg - 1) img_hi = nimg - 1;
+    const int n = img_hi - img_lo + 1;
+    // the weight's fragments (row operand): channel 32 i + fr, k = 16 s + 8 fh .. + 7
+    h8_t wf[NT][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {              // 4 pieces of 8 k
-            uint32_t hv[8];
+    for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = kh + 8 * q + e;
-                const int c = k / 9, tap = k - c * 9, iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
-                float v = 0.f;
-                if (k < K && iy >= 0 && iy < H && ix >= 0 && ix < W) v = src[(size_t)c * HW + iy * W + ix];
-                hv[e] = f2h(v);
-            }
-            const uint4 pk = make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
-                                        hv[6] | (hv[7] << 16));
-            *reinterpret_cast<uint4 *>(As + swz(r, (kh >> 3) + q)) = pk;
-        }
-    }
-    // the weight, zero-padded to K = 64: thread t builds 16-B pieces of rows t >> 3 + 32 i
-    for (int p = t; p < COUT * 8; p += 256) {
-        const int n = p >> 3, q = p & 7;
-        uint32_t hv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = 8 * q + e;
-            hv[e] = k < K ? (uint32_t)w[(size_t)n * K + k] : 0u;
-        }
-        *reinterpret_cast<uint4 *>(Bs + swz(n, q)) =
-            make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+        for (int s = 0; s < 4; ++s)
+            wf[i][s] = *reinterpret_cast<const h8_t *>(w + (size_t)(32 * i + fr) * 64 + 16 * s + 8 * fh);
+    // 1. zero the LDS images (the border stays zero), 2. copy the interior, cast to fp16
+    const int img_words = (n * C * PP + 1) >> 1;
+    for (int e = t; e < img_words; e += 256) reinterpret_cast<uint32_t *>(Img)[e] = 0u;
+    __syncthreads();
+    const float *src = in + (size_t)img_lo * C * HW;
+    const int count = n * C * HW;
+    for (int e = t; e < count; e += 256) {
+        const int ic = e / HW, rem = e - ic * HW, y = rem / W, x = rem - y * W;
+        Img[ic * PP + (y + 1) * PW + x + 1] = (uint16_t)f2h(src[e]);
     }
     __syncthreads();
-    const int fr = lane & 31, fh = lane >> 5;
+    // 3. im2col: thread t fills row t >> 1, channels (t & 1), (t & 1) + 2, ...; the odd thread
+    //    also zeroes k = K .. 63
+    {
+        const int r = t >> 1, m = m0 + r;
+        auto put = [&](int k, uint32_t v) {
+            *reinterpret_cast<uint16_t *>(As + swz(r, k >> 3) + (k & 7) * 2) = (uint16_t)v;
+        };
+        if (m < M) {
+            const int img = m / HW, pos = m - img * HW, oy = pos / W, ox = pos - oy * W;
+            const uint16_t *base = Img + (img - img_lo) * C * PP + oy * PW + ox;
+            for (int c = t & 1; c < C; c += 2) {
+                const uint16_t *p = base + c * PP;
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) put(c * 9 + ky * 3 + kx, p[ky * PW + kx]);
+            }
+        } else {
+            for (int k = t & 1; k < K; k += 2) put(k, 0u);
+        }
+        if (t & 1)
+            for (int k = K; k < 64; ++k) put(k, 0u);
+    }
+    __syncthreads();
     f16_t acc[NT];
 #pragma unroll
-    for (int b = 0; b < NT; ++b)
-        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+    for (int i = 0; i < NT; ++i)
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const int qq = 2 * s + fh;
-        const h8_t af = *reinterpret_cast<const h8_t *>(As + swz(wave * 32 + fr, qq));
+        const h8_t pf = *reinterpret_cast<const h8_t *>(As + swz(wave * 32 + fr, 2 * s + fh));
 #pragma unroll
-        for (int b = 0; b < NT; ++b) {
-            const h8_t bf = *reinterpret_cast<const h8_t *>(Bs + swz(b * 32 + fr, qq));
-            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
-        }
+        for (int i = 0; i < NT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[i][s], pf, acc[i], 0, 0, 0);
     }
-    __syncthreads();                                // As / Bs reads done: the tile reuses the LDS
-    char *T = smem;
-    constexpr int RB = COUT * 2;
+    // epilogue from registers: acc[i] register 4 gq + e = channel 32 i + 8 gq + 4 fh + e of pixel
+    // m0 + 32 wave + fr
+    const int m = m0 + wave * 32 + fr;
+    if (m < M) {
 #pragma unroll
-    for (int b = 0; b < NT; ++b) {
-        const int n = b * 32 + fr;
-        const float bv = h2f(bias[n]);
+        for (int i = 0; i < NT; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            const float v = fmaxf(h2f(f2h(h2f(f2h(acc[b][r])) + bv)), 0.f);
-            const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
-            *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
-                (uint16_t)f2h(v);
-        }
-    }
-    __syncthreads();
-    constexpr int PIECES_ROW = RB / 16;
-    for (int p = t; p < BM * PIECES_ROW; p += 256) {
-        const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
-        const int m = m0 + row;
-        if (m >= M) continue;
-        const int g = pc >> 3, pq = pc & 7;
-        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) =
-            *reinterpret_cast<const uint4 *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4));
+            for (int gq = 0; gq < 4; ++gq) {
+                const int n0 = 32 * i + 8 * gq + 4 * fh;
+                const uint2 bb = *reinterpret_cast<const uint2 *>(bias + n0);
+                const float bv[4] = {h2f(bb.x), h2f(bb.x >> 16), h2f(bb.y), h2f(bb.y >> 16)};
+                uint32_t hv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[e] = f2h(fmaxf(h2f(f2h(h2f(f2h(acc[i][4 * gq + e])) + bv[e])), 0.f));
+                *reinterpret_cast<uint2 *>(out + (size_t)m * COUT + n0) =
+                    make_uint2(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16));
+            }
     }
 }
 
@@ -316,10 +325,13 @@ int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *
     const int64_t M64 = nimg * H * W;
     if (M64 > (int64_t)0x7FFFFFFF - 1024) return MAPF_EINVAL;
     const int M = (int)M64;
-    const size_t lds = (size_t)128 * Cout * 2 > (size_t)128 * 128 + (size_t)Cout * 128 ? (size_t)128 * Cout * 2
-                                                                                       : (size_t)128 * 128 + (size_t)Cout * 128;
+    const int64_t HW = (int64_t)H * W;
+    if ((int64_t)(H + 2) * (W + 2) * Cin > 16384) return MAPF_EINVAL;
+    const int64_t nmax = 127 / HW + 2;                 // images one 128-pixel tile can touch
+    const size_t lds = (size_t)128 * 128 + (size_t)(nmax * Cin * (H + 2) * (W + 2) * 2 + 3) / 4 * 4;
+    if (lds > 64 * 1024) return MAPF_EINVAL;
     hipLaunchKernelGGL(conv::conv_first_kernel<128>, dim3((M + 127) / 128), dim3(256), lds, (hipStream_t)stream, x_nchw,
-                       w, bias, y, M, (int)Cin, (int)H, (int)W);
+                       w, bias, y, M, (int)Cin, (int)H, (int)W, (int)nimg);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

@@ -387,19 +387,22 @@ inline int grid_for(long items, int per_block) {
 // separate launches, so only the GEMM's summation order differs from lin() + the epilogue kernel;
 // the linear's fp16 output never goes to HBM.  Workgroup: 64 rows x all 512 columns, 8 waves
 // as 2 (rows) x 4 (columns), 32 x 128 per wave (4 accumulators of v_mfma_f32_32x32x16_f16).  K in
-// chunks of 64 staged by LDS-DMA (A: 64 rows x 128 B, W: 512 rows x 128 B; two buffers, 144 KiB,
-// source-side XOR swizzle as csrc/mapf_conv.hip), then the fp16 y tile goes through LDS and each
-// wave takes whole rows for the elementwise epilogue (ln_row).
+// chunks of 32 staged by LDS-DMA (A: 64 rows x 64 B, W: 512 rows x 64 B; two buffers, 72 KiB, so
+// two workgroups share a CU and one's elementwise epilogue overlaps the other's GEMM).  64-B LDS
+// rows, 16-B pieces XOR-swizzled by (row >> 2) & 3 on the source side: a ds_read_b128 16-lane group
+// reads 16 distinct rows at one piece and a 256-B bank row holds 4 rows, so every lane of a group
+// gets its own slot.  Then the fp16 y tile goes through LDS and each wave takes whole rows for the
+// elementwise epilogue (ln_row).
 typedef _Float16 gh8_t __attribute__((ext_vector_type(8)));
 typedef float gf16_t __attribute__((ext_vector_type(16)));
-constexpr int GL_BM = 64, GL_BK = 64, GL_D = 512;
+constexpr int GL_BM = 64, GL_BK = 32, GL_D = 512;
 constexpr int GL_ABYTES = GL_BM * GL_BK * 2, GL_BBYTES = GL_D * GL_BK * 2, GL_BUF = GL_ABYTES + GL_BBYTES;
 constexpr int GL_LDS = 2 * GL_BUF;
 static_assert(GL_BM * GL_D * 2 <= GL_LDS, "epilogue tile");
 
 __device__ __attribute__((aligned(16))) uint4 g_lin_zero[1];    // source of the rows past M
 
-__device__ inline int gl_swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
+__device__ inline int gl_swz(int r, int q) { return r * 64 + ((q ^ ((r >> 2) & 3)) << 4); }
 __device__ inline void gl_dma16(const void *src, void *lds) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
@@ -420,17 +423,20 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const long m0 = (long)blockIdx.x * GL_BM;
-    const int q = (lane & 7) ^ ((lane >> 3) & 7);             // logical piece this lane fetches
-    const long rowA = m0 + 8 * wave + (lane >> 3);             // wave w fills A rows 8w..8w+7
-    const uint16_t *srcA = rowA < M ? A + rowA * GL_D + q * 8 : nullptr;
+    // one DMA instruction fills 16 rows x 64 B lane-linearly: lane l -> row 16 g + (l >> 2),
+    // physical piece l & 3 = logical piece q (the same for every g)
+    const int q = (lane & 3) ^ ((lane >> 4) & 3);
+    const long rowA = m0 + 16 * wave + (lane >> 2);            // waves 0..3 fill A rows 16w..16w+15
+    const uint16_t *srcA = (wave < 4 && rowA < M) ? A + rowA * GL_D + q * 8 : nullptr;
     auto issue = [&](int c, int buf) {
         char *As = smem + buf * GL_BUF;
         char *Bs = As + GL_ABYTES;
-        gl_dma16(srcA ? (const void *)(srcA + c * GL_BK) : (const void *)g_lin_zero, As + 8 * wave * 128);
+        if (wave < 4)
+            gl_dma16(srcA ? (const void *)(srcA + c * GL_BK) : (const void *)g_lin_zero, As + 16 * wave * 64);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {                          // wave w fills W rows 64w..64w+63
-            const int n = 64 * wave + 8 * j + (lane >> 3);
-            gl_dma16(W + (size_t)n * GL_D + c * GL_BK + q * 8, Bs + (64 * wave + 8 * j) * 128);
+        for (int j = 0; j < 4; ++j) {                          // wave w fills W rows 64w..64w+63
+            const int n = 64 * wave + 16 * j + (lane >> 2);
+            gl_dma16(W + (size_t)n * GL_D + c * GL_BK + q * 8, Bs + (64 * wave + 16 * j) * 64);
         }
     };
     const int wm = wave & 1, wn = wave >> 1, fr = lane & 31, fh = lane >> 5;
@@ -443,7 +449,9 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
             issue(c + 1, (c + 1) & 1);
-            __builtin_amdgcn_s_waitcnt(0x0F70 | 9);            // vmcnt(9): chunk c's 9 copies have landed
+            // chunk c's copies have landed: the 5 (waves 0..3) or 4 copies of chunk c + 1 may not
+            if (wave < 4) __builtin_amdgcn_s_waitcnt(0x0F70 | 5);
+            else __builtin_amdgcn_s_waitcnt(0x0F70 | 4);
         } else {
             __builtin_amdgcn_s_waitcnt(0x0F70);
         }

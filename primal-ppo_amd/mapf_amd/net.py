@@ -295,7 +295,7 @@ class SCRIMPNet(nn.Module):
                 # conv1 from the fp32 NCHW observation: cast, im2col, MFMA, bias + ReLU in one launch
                 x1 = torch.empty((xin.shape[0], 128, F_, F_), dtype=torch.float16, device=dev,
                                  memory_format=torch.channels_last)
-                chk(lib.mapf_conv_first_f32(ptr(xin), ptr(h16(self.conv1.weight)), ptr(h16(self.conv1.bias)),
+                chk(lib.mapf_conv_first_f32(ptr(xin), ptr(h16(self.conv1.weight, "k64")), ptr(h16(self.conv1.bias)),
                                             ptr(x1), xin.shape[0], self.num_channel, F_, F_, 128, st))
             else:
                 x1 = conv(x.contiguous(memory_format=torch.channels_last), self.conv1)
@@ -337,6 +337,7 @@ class SCRIMPNet(nn.Module):
     _HALF_VIEWS = {"sumT": lambda t: t.sum(0).transpose(0, 1), "sum": lambda t: t.sum(0),
                    "ohwi": lambda t: t.permute(0, 2, 3, 1),        # conv weight for mapf_conv_nhwc_f16
                    "ohwi2d": lambda t: t.permute(0, 2, 3, 1).reshape(t.shape[0], -1),   # ... as a GEMM operand
+                   "k64": lambda t: F.pad(t.reshape(t.shape[0], -1), (0, 64 - t[0].numel())),   # mapf_conv_first_f32
                    "q": lambda t: t[:t.shape[0] // 3], "kv": lambda t: t[t.shape[0] // 3:]}
 
     def _half(self, t, view=None):

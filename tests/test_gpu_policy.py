@@ -223,12 +223,14 @@ def test_fp16_weight_cache_follows_in_place_updates():
 
 
 @pytest.mark.parametrize("ci,co,ks,H,B", [(128, 128, 3, 9, 37), (128, 128, 3, 11, 3), (128, 256, 2, 4, 50),
-                                         (256, 256, 2, 5, 33), (256, 256, 2, 6, 7), (128, 128, 3, 9, 1)])
+                                         (256, 256, 2, 5, 33), (256, 256, 2, 6, 7), (128, 128, 3, 9, 1),
+                                         (128, 128, 3, 9, 1001), (128, 256, 2, 4, 2111), (256, 256, 2, 6, 1003)])
 @pytest.mark.parametrize("relu", [0, 1])
 def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
     """mapf_conv_nhwc_f16 (MFMA implicit GEMM, csrc/mapf_conv.hip) == the autocast conv (fp16
     operands, fp32 accumulation, fp16 output; + fp16 bias, ReLU) to fp16 rounding -- ragged
-    pixel counts (the last workgroup's rows past M), every padding tap, 3x3 and 2x2."""
+    pixel counts (the last tile's rows past M), every padding tap, 3x3 and 2x2, and grids with
+    more tiles than CUs (a persistent workgroup's K pipeline running on into its next tile)."""
     from mapf_amd import _lib
     g = torch.Generator(device="cuda").manual_seed(ci + co + H + B)
     cl = torch.channels_last
@@ -311,6 +313,7 @@ def test_conv_first_kernel_vs_torch(C, H, B):
         y = torch.full((B, 128, H, H), float("nan"), dtype=torch.float16, device="cuda").contiguous(
             memory_format=torch.channels_last)
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        _lib.check(_lib.lib().mapf_conv_first_f32(_p(obs), _p(w.contiguous()), _p(b), _p(y), B, C, H, H, 128, st))
+        w64 = torch.nn.functional.pad(w.reshape(128, -1), (0, 64 - C * 9)).contiguous()
+        _lib.check(_lib.lib().mapf_conv_first_f32(_p(obs), _p(w64), _p(b), _p(y), B, C, H, H, 128, st))
         torch.cuda.synchronize()
         torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
