@@ -199,11 +199,20 @@ static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, 
 // the fp32 NCHW observation: K = Cin * 9 <= 63 (torch's (c, ky, kx) order, zero-padded to 64: the
 // packed weight is [Cout][64] fp16) is ONE chunk.  A workgroup of 128 output pixels copies the
 // (at most (127 / HW) + 2) images they lie in, cast to fp16 as autocast does, into an LDS image
-// with a zero border; builds its 128 im2col rows from it (each (pixel, channel) writes its 9 taps);
-// multiplies them by the weight, whose fragments every wave holds in registers (the MFMA row
-// operand, read once from L2); and writes relu(fp16(fp16(acc) + bias)) as NHWC fp16 from
-// registers (C^T accumulators: 4 consecutive channels of a pixel per 8-B store) -- the MIOpen
-// path's NHWC copy and cast, the conv and the bias / ReLU pass in one launch.
+// with a zero border, and the weight into a swizzled LDS tile; builds its 128 im2col rows from the
+// image (a thread per (row, 16-B piece of 8 k): 8 LDS reads at offsets fixed per thread, one
+// 16-B write); multiplies; and writes relu(fp16(fp16(acc) + bias)) as NHWC fp16 from registers
+// (the weight is the MFMA row operand, so the accumulators hold C^T: 4 consecutive channels of a
+// pixel per 8-B store) -- the MIOpen path's NHWC copy and cast, the conv and the bias / ReLU pass
+// in one launch.  ~100 VGPRs and ~37 KiB of LDS: four workgroups per CU overlap each other's
+// load -> build -> MFMA -> store phases.
+__device__ inline int div_small(int a, int b, float rb) {    // a / b for 0 <= a < 2^22, b > 0 (rb = 1 / b)
+    int q = (int)((float)a * rb);
+    q += (a - q * b >= b) ? 1 : 0;
+    q -= (a - q * b < 0) ? 1 : 0;
+    return q;
+}
+
 template <int COUT>
 __global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict__ in, const uint16_t *__restrict__ w,
                                                          const uint16_t *__restrict__ bias, uint16_t *__restrict__ out,
@@ -211,56 +220,63 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict
     constexpr int BM = 128, NT = COUT / 32;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char *As = smem;                                   // [128][64] fp16 im2col rows, swizzled
-    uint16_t *Img = reinterpret_cast<uint16_t *>(smem + BM * 128);   // [n][C][H + 2][W + 2] fp16
+    char *Bs = smem + BM * 128;                        // [COUT][64] fp16 weight, swizzled
+    uint16_t *Img = reinterpret_cast<uint16_t *>(smem + BM * 128 + COUT * 128);   // [n][C][H + 2][W + 2]
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int fr = lane & 31, fh = lane >> 5;
     const int m0 = (int)blockIdx.x * BM;
     const int HW = H * W, K = C * 9, PW = W + 2, PP = (H + 2) * PW;
+    const float rHW = 1.f / (float)HW, rW = 1.f / (float)W;
     const int img_lo = m0 / HW;
     int img_hi = (m0 + BM - 1) / HW;
     if (img_hi > nimg - 1) img_hi = nimg - 1;
     const int n = img_hi - img_lo + 1;
-    // the weight's fragments (row operand): channel 32 i + fr, k = 16 s + 8 fh .. + 7
-    h8_t wf[NT][4];
+    // the weight -> LDS (its loads overlap the image staging below)
+    uint4 wv[COUT * 8 / 256];
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-            wf[i][s] = *reinterpret_cast<const h8_t *>(w + (size_t)(32 * i + fr) * 64 + 16 * s + 8 * fh);
+    for (int j = 0; j < COUT * 8 / 256; ++j) {
+        const int p = t + 256 * j;
+        wv[j] = *reinterpret_cast<const uint4 *>(w + (size_t)(p >> 3) * 64 + (p & 7) * 8);
+    }
     // 1. zero the LDS images (the border stays zero), 2. copy the interior, cast to fp16
     const int img_words = (n * C * PP + 1) >> 1;
     for (int e = t; e < img_words; e += 256) reinterpret_cast<uint32_t *>(Img)[e] = 0u;
+#pragma unroll
+    for (int j = 0; j < COUT * 8 / 256; ++j) {
+        const int p = t + 256 * j;
+        *reinterpret_cast<uint4 *>(Bs + swz(p >> 3, p & 7)) = wv[j];
+    }
     __syncthreads();
     const float *src = in + (size_t)img_lo * C * HW;
     const int count = n * C * HW;
     for (int e = t; e < count; e += 256) {
-        const int ic = e / HW, rem = e - ic * HW, y = rem / W, x = rem - y * W;
+        const int ic = div_small(e, HW, rHW), rem = e - ic * HW, y = div_small(rem, W, rW), x = rem - y * W;
         Img[ic * PP + (y + 1) * PW + x + 1] = (uint16_t)f2h(src[e]);
     }
     __syncthreads();
-    // 3. im2col: thread t fills row t >> 1, channels (t & 1), (t & 1) + 2, ...; the odd thread
-    //    also zeroes k = K .. 63
+    // 3. im2col: thread t builds piece t & 7 (k = 8 (t & 7) .. + 7) of rows (t >> 3) + 32 i
     {
-        const int r = t >> 1, m = m0 + r;
-        auto put = [&](int k, uint32_t v) {
-            *reinterpret_cast<uint16_t *>(As + swz(r, k >> 3) + (k & 7) * 2) = (uint16_t)v;
-        };
-        if (m < M) {
-            const int img = m / HW, pos = m - img * HW, oy = pos / W, ox = pos - oy * W;
-            const uint16_t *base = Img + (img - img_lo) * C * PP + oy * PW + ox;
-            for (int c = t & 1; c < C; c += 2) {
-                const uint16_t *p = base + c * PP;
+        const int pc = t & 7;
+        int koff[8];
 #pragma unroll
-                for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) put(c * 9 + ky * 3 + kx, p[ky * PW + kx]);
-            }
-        } else {
-            for (int k = t & 1; k < K; k += 2) put(k, 0u);
+        for (int e = 0; e < 8; ++e) {
+            const int k = 8 * pc + e, c = (k * 57) >> 9, tap = k - 9 * c, ky = (tap * 11) >> 5, kx = tap - 3 * ky;
+            koff[e] = k < K ? c * PP + ky * PW + kx : -1;           // (k * 57) >> 9 == k / 9 for k < 64
         }
-        if (t & 1)
-            for (int k = K; k < 64; ++k) put(k, 0u);
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {
+            const int r = (t >> 3) + 32 * i, m = m0 + r;
+            uint32_t hv[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            if (m < M) {
+                const int img = m / HW, pos = m - img * HW, oy = div_small(pos, W, rW), ox = pos - oy * W;
+                const uint16_t *base = Img + (img - img_lo) * C * PP + oy * PW + ox;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) hv[e] = koff[e] >= 0 ? (uint32_t)base[koff[e]] : 0u;
+            }
+            *reinterpret_cast<uint4 *>(As + swz(r, pc)) =
+                make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+        }
     }
     __syncthreads();
     f16_t acc[NT];
@@ -271,7 +287,10 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict
     for (int s = 0; s < 4; ++s) {
         const h8_t pf = *reinterpret_cast<const h8_t *>(As + swz(wave * 32 + fr, 2 * s + fh));
 #pragma unroll
-        for (int i = 0; i < NT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[i][s], pf, acc[i], 0, 0, 0);
+        for (int i = 0; i < NT; ++i) {
+            const h8_t wf = *reinterpret_cast<const h8_t *>(Bs + swz(32 * i + fr, 2 * s + fh));
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf, pf, acc[i], 0, 0, 0);
+        }
     }
     // epilogue from registers: acc[i] register 4 gq + e = channel 32 i + 8 gq + 4 fh + e of pixel
     // m0 + 32 wave + fr
@@ -328,7 +347,7 @@ int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *
     const int64_t HW = (int64_t)H * W;
     if ((int64_t)(H + 2) * (W + 2) * Cin > 16384) return MAPF_EINVAL;
     const int64_t nmax = 127 / HW + 2;                 // images one 128-pixel tile can touch
-    const size_t lds = (size_t)128 * 128 + (size_t)(nmax * Cin * (H + 2) * (W + 2) * 2 + 3) / 4 * 4;
+    const size_t lds = (size_t)128 * 128 + (size_t)Cout * 128 + (size_t)(nmax * Cin * (H + 2) * (W + 2) * 2 + 3) / 4 * 4;
     if (lds > 64 * 1024) return MAPF_EINVAL;
     hipLaunchKernelGGL(conv::conv_first_kernel<128>, dim3((M + 127) / 128), dim3(256), lds, (hipStream_t)stream, x_nchw,
                        w, bias, y, M, (int)Cin, (int)H, (int)W, (int)nimg);

@@ -240,7 +240,7 @@ class SCRIMPNet(nn.Module):
         csrc/mapf_policy.hip -- conv bias + ReLU (+ max-pool) in one pass over each NHWC
         activation, LayerNorm written straight as the fp16 the next linear reads, dropout
         + residual add, GELU + dropout, tokeniser + positional embedding + dropout in one
-        pass.  Dropout masks come from the kernels' Philox stream (seeded from torch's
+        pass.  Dropout masks come from the kernels' counter-hash stream (seeded from torch's
         CPU generator), not from torch's."""
         from . import _lib
         lib, chk = _lib.lib(), _lib.check

@@ -50,7 +50,7 @@ def test_fused_acting_forward_is_deterministic(own_conv, fused_linear, training)
     calls and on a deep copy of the network (a kernel that reads memory it did not write, or
     races on LDS, shows up here first)"""
     import copy
-    net = _net().train(training)               # training: dropout on, masks from the seeded Philox stream
+    net = _net().train(training)               # training: dropout on, masks from the seeded hash stream
     net.own_conv, net.fused_linear = own_conv, fused_linear
     g = torch.Generator(device="cuda").manual_seed(9)
     obs = (torch.rand(300, 8, 6, 9, 9, device="cuda", generator=g) < 0.25).float()
@@ -95,6 +95,15 @@ def test_dropout_kernels_keep_rate_and_scale():
     x2 = torch.zeros(n, device="cuda")
     _lib.check(lib.mapf_dropout_residual(_p(x2), _p(y), n, 0.2, 1235, st))
     assert (x != x2).float().mean().item() > 0.2
+    # the counter hash's masks: every lane of a float4 at the keep rate, neighbours (in a float4,
+    # across float4s, a row apart) and the two seeds' masks uncorrelated
+    m = (x == 1.25).float()
+    assert all(abs(m[k::4].mean().item() - 0.8) < 5e-3 for k in range(4))
+    for lag in (1, 3, 4, 5, 512):
+        c = torch.corrcoef(torch.stack([m[:-lag], m[lag:]]))[0, 1].item()
+        assert abs(c) < 5e-3, (lag, c)
+    c = torch.corrcoef(torch.stack([m, (x2 == 1.25).float()]))[0, 1].item()
+    assert abs(c) < 5e-3, c
     # GELU + dropout: kept entries equal fp16(gelu(v) * 1.25)
     v = torch.linspace(-4, 4, n, device="cuda").half()
     h = v.clone()
