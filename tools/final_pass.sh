@@ -29,7 +29,7 @@ for st in ${STEPS:-pytest smoke bench profile rollout}; do
         python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], '%.4e'%d['value'], d['ms_per_step'], r['kernel'], r['frac'], r['traffic'], (d.get('cpu_baseline') or {}).get('value'), {k: (v['ms_per_step'], v['frac']) for k, v in d.get('paths', {}).items()})" gpurun_out/${TAG}_$f.log $f
       done ;;
     profile)
-      CONFIGS="${CONFIGS:-c2 c4 c5}" bash tools/c45_profile.sh || exit 1 ;;
+      CONFIGS="${CONFIGS:-c2 c4 c5}" STEPS=${BENCH_STEPS:-1024} bash tools/c45_profile.sh || exit 1 ;;
     rollout)   # c3: policy in the loop (4096 x 8, FOV 9) + PPO updates; c4-shaped updates (1024 x 16, 40x40)
       timeout -k 10 400 python3 tools/bench_rollout.py --train > gpurun_out/${TAG}_rollout_c3.jsonl 2>&1 \
         || { tail -5 gpurun_out/${TAG}_rollout_c3.jsonl; exit 1; }
