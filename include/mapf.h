@@ -386,6 +386,17 @@ int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, 
                        int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                        int64_t kv_seq_stride, int32_t heads, int32_t head_dim, float scale, void *stream);
 
+/* The gradient of mapf_attention_f16 (the training forward's attention, transformer.py:48-85):
+ * given q, k, v (strides as mapf_attention_f16), its fp16 output `out` and the output gradient
+ * `dout` ([B][q_rows][heads * head_dim] at out_token_stride / out_seq_stride), writes dq (q's
+ * strides) and dk, dv (k's / v's strides) as fp16: P recomputed in fp32, D = rowsum(dout * out).
+ * n <= 32, heads 16, head_dim 32; every pointer 16-B aligned, strides multiples of 8. */
+int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, const uint16_t *out,
+                           const uint16_t *dout, uint16_t *dq, uint16_t *dk, uint16_t *dv, int64_t B, int32_t n,
+                           int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
+                           int64_t kv_seq_stride, int64_t out_token_stride, int64_t out_seq_stride, int32_t heads,
+                           int32_t head_dim, float scale, void *stream);
+
 /* ---- PPO loss (model.py:115-175) ------------------------------------------
  * All loss terms of one minibatch update over R = rows x agents elements with A actions each,
  * plus d(all_loss)/d(new_ps, new_v, new_cv, policy_sig), in one launch.  Device pointers: fp32

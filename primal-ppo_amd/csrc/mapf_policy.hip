@@ -534,6 +534,156 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     }
 }
 
+// ---- attention backward (the training forward's attention, transformer.py:48-85) ---------
+// For SDPA's flash backward the 17-token sequences are all overhead (0.31 ms per layer at 2,048
+// agents x 16 heads).  One workgroup per sequence, wave w takes heads w, w + 4, ...; per head,
+// with P recomputed in fp32 from q, k (as flash does) and D = rowsum(dO o) from the forward's
+// fp16 output:
+//   row pass, lane i < rows:    S_i. = scale q_i k^T, P_i. = softmax, dP_ij = dO_i v_j,
+//                               dS_ij = P_ij (dP_ij - D_i), dq_i = scale sum_j dS_ij k_j
+//   column pass, lane j < n:    dv_j = sum_i P_ij dO_i, dk_j = scale sum_i dS_ij q_i
+// K, V, Q, dO staged as fp16 rows in LDS (every lane of a row pass reads the same K / V row:
+// broadcasts), P and dS as fp32 [i][j]; fp16 gradients out.  n <= 32, head_dim 32, 16 heads.
+constexpr int AB_ROW = 64;                                  // bytes per fp16 head row
+constexpr int AB_WAVE = 4 * 32 * AB_ROW + 2 * 32 * 32 * 4;  // Q, dO, K, V + P, dS per wave: 4 waves = 64 KiB
+// P / dS element (i, j) at i * 32 + (j ^ i): the row pass (lanes = i, one j) and the column pass
+// (lanes = j, one i) both hit 32 distinct banks.  (64 KiB: a captured graph's kernel node gets no
+// more dynamic LDS than that unless the function's attribute is raised.)
+__device__ inline int ab_pij(int i, int j) { return i * 32 + (j ^ (i & 31)); }
+static_assert(4 * AB_WAVE <= 65536, "attention_bwd_f16 LDS");
+__device__ inline void ab_row_to_f32(const char *src, float *f) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 u = reinterpret_cast<const uint4 *>(src)[c];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            f[8 * c + 2 * e] = h2f(w[e]);
+            f[8 * c + 2 * e + 1] = h2f(w[e] >> 16);
+        }
+    }
+}
+typedef _Float16 ab_h2_t __attribute__((ext_vector_type(2)));
+// a . row over 32 fp16 pairs with v_dot2_f32_f16 (fp16 products exact in fp32, fp32 sums)
+__device__ inline float ab_dot(const uint32_t *a, const char *row) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 u = reinterpret_cast<const uint4 *>(row)[c];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(ab_h2_t, a[4 * c + e]), __builtin_bit_cast(ab_h2_t, w[e]),
+                                         acc, false);
+    }
+    return acc;
+}
+__device__ inline void ab_load_h(const char *src, uint32_t *a) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 u = reinterpret_cast<const uint4 *>(src)[c];
+        a[4 * c] = u.x;
+        a[4 * c + 1] = u.y;
+        a[4 * c + 2] = u.z;
+        a[4 * c + 3] = u.w;
+    }
+}
+__device__ inline void ab_axpy(float *acc, float s, const char *row) {
+    float f[32];
+    ab_row_to_f32(row, f);
+#pragma unroll
+    for (int d = 0; d < 32; ++d) acc[d] = fmaf(s, f[d], acc[d]);
+}
+__device__ inline void ab_store(uint16_t *dst, const float *f, float scale) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        reinterpret_cast<uint4 *>(dst)[c] =
+            make_uint4(f2h(f[8 * c] * scale) | (f2h(f[8 * c + 1] * scale) << 16),
+                       f2h(f[8 * c + 2] * scale) | (f2h(f[8 * c + 3] * scale) << 16),
+                       f2h(f[8 * c + 4] * scale) | (f2h(f[8 * c + 5] * scale) << 16),
+                       f2h(f[8 * c + 6] * scale) | (f2h(f[8 * c + 7] * scale) << 16));
+}
+
+__global__ __launch_bounds__(256) void attention_bwd_f16(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
+                                                         const uint16_t *__restrict__ v, const uint16_t *__restrict__ o,
+                                                         const uint16_t *__restrict__ dout, uint16_t *__restrict__ dq,
+                                                         uint16_t *__restrict__ dk, uint16_t *__restrict__ dv, int n,
+                                                         int rows, long q_ts, long q_ss, long kv_ts, long kv_ss,
+                                                         long o_ts, long o_ss, float scale) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
+    const long b = blockIdx.x;
+    char *Qh = smem + wave * AB_WAVE, *dOh = Qh + 32 * AB_ROW, *Kh = dOh + 32 * AB_ROW, *Vh = Kh + 32 * AB_ROW;
+    float *P = reinterpret_cast<float *>(Vh + 32 * AB_ROW), *dS = P + 32 * 32;
+    for (int h = wave; h < 16; h += 4) {
+        if (lane < n) {
+            const uint4 *ks = reinterpret_cast<const uint4 *>(k + b * kv_ss + lane * kv_ts + h * 32);
+            const uint4 *vs = reinterpret_cast<const uint4 *>(v + b * kv_ss + lane * kv_ts + h * 32);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                reinterpret_cast<uint4 *>(Kh + lane * AB_ROW)[c] = ks[c];
+                reinterpret_cast<uint4 *>(Vh + lane * AB_ROW)[c] = vs[c];
+            }
+        }
+        uint32_t qh[16], gh[16];                           // this row's q and dO, fp16 pairs
+        float D = 0.f;
+        if (lane < rows) {
+            ab_load_h(reinterpret_cast<const char *>(q + b * q_ss + lane * q_ts + h * 32), qh);
+            ab_load_h(reinterpret_cast<const char *>(dout + b * o_ss + lane * o_ts + h * 32), gh);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                reinterpret_cast<uint4 *>(Qh + lane * AB_ROW)[c] = make_uint4(qh[4 * c], qh[4 * c + 1], qh[4 * c + 2], qh[4 * c + 3]);
+                reinterpret_cast<uint4 *>(dOh + lane * AB_ROW)[c] = make_uint4(gh[4 * c], gh[4 * c + 1], gh[4 * c + 2], gh[4 * c + 3]);
+            }
+            D = ab_dot(gh, reinterpret_cast<const char *>(o + b * o_ss + lane * o_ts + h * 32));
+        }
+        __syncthreads();
+        if (lane < rows) {                                 // row pass
+            float sv[32];
+            float m = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                sv[j] = j < n ? scale * ab_dot(qh, Kh + j * AB_ROW) : -INFINITY;
+                m = fmaxf(m, sv[j]);
+            }
+            float l = 0.f;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                sv[j] = j < n ? __expf(sv[j] - m) : 0.f;
+                l += sv[j];
+            }
+            const float rl = 1.f / l;
+            float gq[32];
+#pragma unroll
+            for (int d = 0; d < 32; ++d) gq[d] = 0.f;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                if (j < n) {
+                    const float pj = sv[j] * rl;
+                    const float ds = pj * (ab_dot(gh, Vh + j * AB_ROW) - D);
+                    P[ab_pij(lane, j)] = pj;
+                    dS[ab_pij(lane, j)] = ds;
+                    ab_axpy(gq, ds, Kh + j * AB_ROW);
+                }
+            }
+            ab_store(dq + b * q_ss + lane * q_ts + h * 32, gq, scale);
+        }
+        __syncthreads();
+        if (lane < n) {                                    // column pass
+            float gk[32], gv[32];
+#pragma unroll
+            for (int d = 0; d < 32; ++d) gk[d] = gv[d] = 0.f;
+            for (int i = 0; i < rows; ++i) {
+                ab_axpy(gv, P[ab_pij(i, lane)], dOh + i * AB_ROW);
+                ab_axpy(gk, dS[ab_pij(i, lane)], Qh + i * AB_ROW);
+            }
+            ab_store(dk + b * kv_ss + lane * kv_ts + h * 32, gk, scale);
+            ab_store(dv + b * kv_ss + lane * kv_ts + h * 32, gv, 1.f);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace pol
 }  // namespace mapf
 
@@ -660,6 +810,25 @@ int mapf_attention_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, 
         hipLaunchKernelGGL(pol::attention_f16<2>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, q, k, v, out,
                            (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride, (long)kv_token_stride,
                            (long)kv_seq_stride, sl2e);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t *v, const uint16_t *out,
+                           const uint16_t *dout, uint16_t *dq, uint16_t *dk, uint16_t *dv, int64_t B, int32_t n,
+                           int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
+                           int64_t kv_seq_stride, int64_t out_token_stride, int64_t out_seq_stride, int32_t heads,
+                           int32_t head_dim, float scale, void *stream) {
+    if (!q || !k || !v || !out || !dout || !dq || !dk || !dv || B < 0 || n < 1 || n > 32 || q_rows < 1 ||
+        q_rows > n || heads != 16 || head_dim != 32 ||
+        ((q_token_stride | q_seq_stride | kv_token_stride | kv_seq_stride | out_token_stride | out_seq_stride) & 7) ||
+        (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)out | (uintptr_t)dout | (uintptr_t)dq |
+          (uintptr_t)dk | (uintptr_t)dv) & 15))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::attention_bwd_f16, dim3((unsigned)B), dim3(256), 4 * pol::AB_WAVE, (hipStream_t)stream, q,
+                       k, v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride,
+                       (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride, (long)out_seq_stride,
+                       scale);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

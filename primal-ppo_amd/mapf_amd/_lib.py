@@ -112,6 +112,8 @@ SIGNATURES = {
     "mapf_conv_first_f32": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, P]),
     "mapf_conv_nhwc_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P]),
     "mapf_attention_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I32, I32, ctypes.c_float, P]),
+    "mapf_attention_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I64, I64, I32,
+                                              I32, ctypes.c_float, P]),
 }
 
 _lib = None

@@ -61,6 +61,54 @@ class _PreNorm(nn.Module):
         return self.fn.fn.forward_first(self.fn.norm(x)) + x[:, :1]
 
 
+class _HipAttention(torch.autograd.Function):
+    """softmax(q k^T * scale) v over <= 32 tokens, 16 heads of 32, for the TRAINING forward:
+    mapf_attention_f16 forward, mapf_attention_bwd_f16 backward (csrc/mapf_policy.hip) in place of
+    SDPA's flash kernels, which are tiled for long sequences.  q: `rows` tokens at column q_off of
+    qsrc [b, t, wq] (or [b, wq]); k, v at columns k_off, v_off of kvsrc [b, n, wkv]; both fp16
+    and contiguous -- qsrc may be kvsrc (the fused qkv projection), then one gradient comes back.
+    Returns [b, rows, 512] fp16."""
+
+    @staticmethod
+    def _meta(qsrc, kvsrc):
+        b, n, wkv = kvsrc.shape
+        wq = qsrc.shape[-1]
+        q_ss = wq * (qsrc.shape[1] if qsrc.dim() == 3 else 1)
+        return b, n, wq, q_ss, wkv, n * wkv
+
+    @staticmethod
+    def forward(ctx, qsrc, kvsrc, rows, q_off, k_off, v_off, scale):
+        from . import _lib
+        b, n, wq, q_ss, kv_ts, kv_ss = _HipAttention._meta(qsrc, kvsrc)
+        out = torch.empty(b, rows, 512, dtype=torch.float16, device=qsrc.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(qsrc.device).cuda_stream)
+        e = 2                                                      # bytes per fp16 element
+        _lib.check(_lib.lib().mapf_attention_f16(
+            ctypes.c_void_p(qsrc.data_ptr() + e * q_off), ctypes.c_void_p(kvsrc.data_ptr() + e * k_off),
+            ctypes.c_void_p(kvsrc.data_ptr() + e * v_off), ctypes.c_void_p(out.data_ptr()), b, n, rows, wq, q_ss,
+            kv_ts, kv_ss, 16, 32, float(scale), st))
+        ctx.save_for_backward(qsrc, kvsrc, out)
+        ctx.args = (rows, q_off, k_off, v_off, scale, qsrc.data_ptr() == kvsrc.data_ptr())
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import _lib
+        qsrc, kvsrc, out = ctx.saved_tensors
+        rows, q_off, k_off, v_off, scale, same = ctx.args
+        b, n, wq, q_ss, kv_ts, kv_ss = _HipAttention._meta(qsrc, kvsrc)
+        dout = dout.contiguous()
+        gq = torch.empty_like(qsrc)
+        gkv = gq if same else torch.empty_like(kvsrc)
+        st = ctypes.c_void_p(torch.cuda.current_stream(qsrc.device).cuda_stream)
+        e = 2
+        p = lambda t, off=0: ctypes.c_void_p(t.data_ptr() + e * off)  # noqa
+        _lib.check(_lib.lib().mapf_attention_bwd_f16(
+            p(qsrc, q_off), p(kvsrc, k_off), p(kvsrc, v_off), p(out), p(dout), p(gq, q_off), p(gkv, k_off),
+            p(gkv, v_off), b, n, rows, wq, q_ss, kv_ts, kv_ss, 512, rows * 512, 16, 32, float(scale), st))
+        return gq, (None if same else gkv), None, None, None, None, None
+
+
 class _SelfAttention(nn.Module):
     """transformer.py:48-85: fused qkv projection, softmax(q k^T / sqrt(dim)) v, output projection.
     Note the reference scales by dim ** -0.5 (the model width), not the head width.
@@ -80,10 +128,20 @@ class _SelfAttention(nn.Module):
         nn.init.zeros_(self.nn1.bias)
         self.do1 = nn.Dropout(dropout)
 
+    hip_attention = True               # the training forward's attention on _HipAttention (GPU, fp16)
+
+    def _hip(self, x, t):
+        return (self.hip_attention and x.is_cuda and t.dtype == torch.float16 and self.heads == 16 and
+                x.shape[-1] == 512 and x.shape[1] <= 32 and torch.is_grad_enabled())
+
     def forward(self, x):
         b, n, d = x.shape
         h = self.heads
-        qkv = self.to_qkv(x).view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
+        qkv = self.to_qkv(x)
+        if self._hip(x, qkv):
+            return self.do1(self.nn1(_HipAttention.apply(qkv.contiguous(), qkv.contiguous(), n, 0, d, 2 * d,
+                                                         self.scale)))
+        qkv = qkv.view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
         q, k, v = qkv[0], qkv[1], qkv[2]
         out = F.scaled_dot_product_attention(q, k, v, scale=self.scale).transpose(1, 2).reshape(b, n, d)
         return self.do1(self.nn1(out))
@@ -94,8 +152,12 @@ class _SelfAttention(nn.Module):
         h = self.heads
         w, bias = self.to_qkv.weight, self.to_qkv.bias
         # x[:, 0] is a 2-D strided view: one GEMM with lda = n*d ([b, 1, d] would run as a slow bmm)
-        q = F.linear(x[:, 0], w[:d], bias[:d]).view(b, 1, h, d // h).transpose(1, 2)           # b, h, 1, dh
-        kv = F.linear(x, w[d:], bias[d:]).view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)      # 2, b, h, n, dh
+        q = F.linear(x[:, 0], w[:d], bias[:d])
+        kv = F.linear(x, w[d:], bias[d:])
+        if self._hip(x, q):
+            return self.do1(self.nn1(_HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale)))
+        q = q.view(b, 1, h, d // h).transpose(1, 2)                                             # b, h, 1, dh
+        kv = kv.view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)                                 # 2, b, h, n, dh
         out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=self.scale).transpose(1, 2).reshape(b, 1, d)
         return self.do1(self.nn1(out))
 

@@ -326,3 +326,66 @@ def test_conv_first_kernel_vs_torch(C, H, B):
         _lib.check(_lib.lib().mapf_conv_first_f32(_p(obs), _p(w64), _p(b), _p(y), B, C, H, H, 128, st))
         torch.cuda.synchronize()
         torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,first", [(17, False), (17, True), (5, False), (32, False), (9, True)])
+def test_hip_attention_autograd_vs_sdpa(n, first):
+    """_HipAttention (mapf_attention_f16 + mapf_attention_bwd_f16) == SDPA on the same fp16 q, k, v
+    in fp32: output and dq / dk / dv, for the fused qkv tensor (one gradient) and for token 0's
+    query against separate k / v (forward_first)."""
+    from mapf_amd.net import _HipAttention
+    g = torch.Generator(device="cuda").manual_seed(n + 100 * first)
+    b, d, scale = 37, 512, 512 ** -0.5
+    gout = torch.randn(b, 1 if first else n, d, device="cuda", generator=g).half()
+    if first:
+        qsrc = (torch.randn(b, d, device="cuda", generator=g) * 2).half().requires_grad_()
+        kvsrc = (torch.randn(b, n, 2 * d, device="cuda", generator=g) * 2).half().requires_grad_()
+        out = _HipAttention.apply(qsrc, kvsrc, 1, 0, 0, d, scale)
+        out.backward(gout)
+        q32 = qsrc.detach().float().view(b, 1, 16, 32).transpose(1, 2).requires_grad_()
+        kv32 = kvsrc.detach().float().view(b, n, 2, 16, 32).permute(2, 0, 3, 1, 4)
+        k32, v32 = kv32[0].clone().requires_grad_(), kv32[1].clone().requires_grad_()
+    else:
+        qsrc = (torch.randn(b, n, 3 * d, device="cuda", generator=g) * 2).half().requires_grad_()
+        kvsrc = qsrc
+        out = _HipAttention.apply(qsrc, qsrc, n, 0, d, 2 * d, scale)
+        out.backward(gout)
+        qkv32 = qsrc.detach().float().view(b, n, 3, 16, 32).permute(2, 0, 3, 1, 4)
+        q32, k32, v32 = (t.clone().requires_grad_() for t in qkv32)
+    ref = torch.nn.functional.scaled_dot_product_attention(q32, k32, v32, scale=scale)
+    ref.backward(gout.float().view(b, -1, 16, 32).transpose(1, 2))
+    torch.testing.assert_close(out.float(), ref.transpose(1, 2).reshape(b, -1, d), rtol=2e-2, atol=2e-2)
+    gq = q32.grad.transpose(1, 2).reshape(b, -1, d)
+    gk = k32.grad.transpose(1, 2).reshape(b, n, d)
+    gv = v32.grad.transpose(1, 2).reshape(b, n, d)
+    if first:
+        got_q, got_k, got_v = qsrc.grad.view(b, 1, d), kvsrc.grad[..., :d], kvsrc.grad[..., d:]
+    else:
+        got_q, got_k, got_v = qsrc.grad[..., :d], qsrc.grad[..., d:2 * d], qsrc.grad[..., 2 * d:]
+    for name, got, want in (("dq", got_q, gq), ("dk", got_k, gk), ("dv", got_v, gv)):
+        assert torch.isfinite(got).all(), name
+        torch.testing.assert_close(got.float(), want, rtol=3e-2, atol=3e-2, msg=name)
+
+
+def test_training_forward_uses_hip_attention_and_matches_sdpa():
+    """the training forward (autograd) with _HipAttention == with SDPA: each parameter's gradient
+    within 2 % (relative norm) or 3x the spread of two SDPA runs (MIOpen's backward reduces in a
+    run-dependent order)"""
+    net = _net().eval()
+    obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.25).float()
+    vec = torch.randn(16, 8, 4, device="cuda")
+    grads = []
+    for hip in (True, False, False):
+        for m in net.modules():
+            if hasattr(m, "hip_attention"):
+                m.hip_attention = hip
+        net.zero_grad()
+        out = net(obs, vec)
+        (out[1].float().sum() + out[0].float().pow(2).sum()).backward()
+        grads.append([p.grad.detach().float().clone() for p in net.parameters() if p.grad is not None])
+    for a, b, c in zip(*grads):
+        nb = b.norm().item()
+        if nb == 0:
+            continue
+        r_hip, r_spread = (a - b).norm().item() / nb, (c - b).norm().item() / nb
+        assert r_hip <= max(2e-2, 3 * r_spread), (a.shape, r_hip, r_spread)
