@@ -187,12 +187,151 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *
     }
 }
 
+// The same implicit GEMM with K chunks of 32 (64-B LDS rows) in a ring of STAGES buffers: the
+// same LDS as the 64-deep double buffer holds STAGES - 1 chunks in flight instead of one, with one
+// barrier per chunk (the buffer refilled at chunk c is the one every wave finished reading before
+// chunk c's barrier).  64-B rows: a DMA instruction fills 16 rows, lane l row 16 g + (l >> 2),
+// physical piece l & 3; the XOR key (row >> 2) & 3 gives each lane of a ds_read_b128 16-lane group
+// (16 distinct rows, 4 rows per 256-B bank row) its own slot.
+__device__ inline int swz64(int r, int q) { return r * 64 + ((q ^ ((r >> 2) & 3)) << 4); }
+template <int N>
+__device__ inline void wait_vm() {
+    static_assert(N >= 0 && N <= 63, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
+template <int CIN, int COUT, int KS, int WAVES, int STAGES>
+struct Cfg32 {
+    static constexpr int THREADS = 64 * WAVES, NT = COUT / 32, BM = 32 * WAVES, K = KS * KS * CIN;
+    static constexpr int CB = CIN / 32, NCHUNK = KS * KS * CB;
+    static constexpr int A_BYTES = BM * 64, B_BYTES = COUT * 64, BUF = A_BYTES + B_BYTES;
+    static constexpr int JA = BM / 16 / WAVES, JB = COUT / 16 / WAVES, J = JA + JB;
+    static constexpr int LDS = STAGES * BUF > BM * COUT * 2 ? STAGES * BUF : BM * COUT * 2;
+    static_assert(CIN % 32 == 0 && COUT % 32 == 0 && BM % (16 * WAVES) == 0 && COUT % (16 * WAVES) == 0, "shape");
+    static_assert(STAGES >= 2 && (STAGES - 2) * J <= 63 && NCHUNK >= STAGES, "ring");
+};
+
+template <int CIN, int COUT, int KS, int WAVES, int STAGES>
+__global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t *__restrict__ in,
+                                                                  const uint16_t *__restrict__ w,
+                                                                  const uint16_t *__restrict__ bias,
+                                                                  uint16_t *__restrict__ out, int M, int H, int W,
+                                                                  int Ho, int Wo, int pad, int epi) {
+    using C = Cfg32<CIN, COUT, KS, WAVES, STAGES>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int m0 = (int)blockIdx.x * C::BM;
+    const int HWo = Ho * Wo;
+    const int q = (lane & 3) ^ ((lane >> 4) & 3);          // logical piece of this lane's 16 B
+    int apix[C::JA], ayx[C::JA];
+#pragma unroll
+    for (int j = 0; j < C::JA; ++j) {
+        const int m = m0 + 16 * (wave * C::JA + j) + (lane >> 2);
+        if (m < M) {
+            const int img = m / HWo, pos = m - img * HWo, oy = pos / Wo, ox = pos - oy * Wo;
+            apix[j] = img * H * W + oy * W + ox;
+            ayx[j] = (oy << 16) | ox;
+        } else {
+            apix[j] = 0;
+            ayx[j] = (int)0x80000000u;                     // every tap out of range
+        }
+    }
+    auto issue = [&](int c, int buf) {
+        const int tap = c / C::CB, cb = c - tap * C::CB;
+        const int ky = tap / KS, kx = tap - ky * KS;
+        char *A = smem + buf * C::BUF;
+        char *B = A + C::A_BYTES;
+        const int dpix = (ky - pad) * W + (kx - pad);
+#pragma unroll
+        for (int j = 0; j < C::JA; ++j) {
+            const int iy = (ayx[j] >> 16) + ky - pad, ix = (ayx[j] & 0xFFFF) + kx - pad;
+            const bool ok = ((unsigned)iy < (unsigned)H) & ((unsigned)ix < (unsigned)W);
+            const void *src = ok ? (const void *)(in + (size_t)(apix[j] + dpix) * CIN + cb * 32 + q * 8)
+                                 : (const void *)g_zero16;
+            dma16(src, A + 16 * (wave * C::JA + j) * 64);
+        }
+#pragma unroll
+        for (int j = 0; j < C::JB; ++j) {
+            const int n = 16 * (wave * C::JB + j) + (lane >> 2);
+            dma16(w + (size_t)n * C::K + c * 32 + q * 8, B + 16 * (wave * C::JB + j) * 64);
+        }
+    };
+    f16_t acc[C::NT];
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b)
+        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < STAGES - 1; ++c) issue(c, c);
+    const int fr = lane & 31, fh = lane >> 5;
+    for (int c = 0; c < C::NCHUNK; ++c) {
+        // chunks c + 1 .. min(c + STAGES - 2, NCHUNK - 1) may stay in flight
+        const int ahead = C::NCHUNK - 1 - c < STAGES - 2 ? C::NCHUNK - 1 - c : STAGES - 2;
+        if (ahead >= STAGES - 2) wait_vm<(STAGES - 2) * C::J>();
+        else if (STAGES > 3 && ahead == 1) wait_vm<(STAGES > 3 ? C::J : 0)>();
+        else if (STAGES > 4 && ahead == 2) wait_vm<(STAGES > 4 ? 2 * C::J : 0)>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (c + STAGES - 1 < C::NCHUNK) issue(c + STAGES - 1, (c + STAGES - 1) % STAGES);
+        const char *A = smem + (c % STAGES) * C::BUF;
+        const char *B = A + C::A_BYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int qq = 2 * s + fh;
+            const h8_t af = *reinterpret_cast<const h8_t *>(A + swz64(wave * 32 + fr, qq));
+#pragma unroll
+            for (int b = 0; b < C::NT; ++b) {
+                const h8_t bf = *reinterpret_cast<const h8_t *>(B + swz64(b * 32 + fr, qq));
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    __syncthreads();                                  // every wave done with the ring: the tile reuses it
+    char *T = smem;
+    constexpr int RB = COUT * 2;
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b) {
+        const int n = b * 32 + fr;
+        const float bv = epi ? h2f(bias[n]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            float v = h2f(f2h(acc[b][r]));
+            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);
+            const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
+            *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
+                (uint16_t)f2h(v);
+        }
+    }
+    __syncthreads();
+    constexpr int PIECES_ROW = RB / 16;
+    for (int p = t; p < C::BM * PIECES_ROW; p += C::THREADS) {
+        const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
+        const int m = m0 + row;
+        if (m >= M) continue;
+        const int g = pc >> 3, pq = pc & 7;
+        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) =
+            *reinterpret_cast<const uint4 *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4));
+    }
+}
+
+#ifndef MAPF_CONV_STAGES
+#define MAPF_CONV_STAGES 3                            // 0: the 64-deep double buffer (conv_igemm_kernel)
+#endif
+
 template <int CIN, int COUT, int KS, int WAVES>
 static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, uint16_t *out, int M, int H, int W,
                    int Ho, int Wo, int pad, int epi, hipStream_t s) {
+#if MAPF_CONV_STAGES
+    using C = Cfg32<CIN, COUT, KS, WAVES, MAPF_CONV_STAGES>;
+    hipLaunchKernelGGL((conv_igemm32_kernel<CIN, COUT, KS, WAVES, MAPF_CONV_STAGES>), dim3((M + C::BM - 1) / C::BM),
+                       dim3(C::THREADS), C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi);
+#else
     using C = Cfg<CIN, COUT, KS, WAVES>;
     hipLaunchKernelGGL((conv_igemm_kernel<CIN, COUT, KS, WAVES>), dim3((M + C::BM - 1) / C::BM), dim3(C::THREADS),
                        C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi);
+#endif
 }
 
 // The first convolution (conv1, net.py:104: Cin = num_channel <= 7, 3x3, padding 1) straight from

@@ -1,9 +1,15 @@
 """The PPO update on the device (Model._train_device, model.py:78-199 of the reference): the
 whole AMP update -- HIP normalisation, forward, fused loss, backward, unscale + found-inf,
-clip, fused Adam, loss-scale update -- captured once per minibatch shape and replayed.  The
-replays must apply the same updates as the eager body (same kernels; MIOpen's backward may
-reduce in another order, so to fp16-backward tolerance), change the weights, keep the AMP
-state on the device, and leave the acting path on the new weights."""
+clip, fused Adam, loss-scale update -- captured once per minibatch shape and replayed.  With
+MIOpen's deterministic algorithms the replays must apply the same updates as the eager body (same
+kernels: bitwise in practice), change the weights, keep the AMP state on the device, and leave the
+acting path on the new weights.
+
+The graphed model trains first and its eager twins after it, not interleaved: a SECOND model's
+eager update (backward + fused Adam) run between two replays of the first model's captured update
+makes a later replay non-finite (tools/diag_graph3.py; acting forwards, foreach ops, a fused Adam
+step or pinned-memory traffic in between do not).  One training model per process -- the driver's
+layout -- never interleaves that way."""
 import copy
 
 import numpy as np
@@ -52,12 +58,10 @@ def test_graphed_updates_equal_eager_updates(deterministic_convs, hip_attention,
     batches = [_batch(g) for _ in range(6)]
     w0 = m1.network.conv1.weight.detach().clone()
     init = [p.detach().clone() for p in m1.network.parameters()]
-    for k, (obs, vec, ret, cret, v, cv, act, ps, tv) in enumerate(batches):
-        s1 = m1.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-        s2 = m2.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-        s4 = m4.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-        print("update", k, "graph - eager", [round(float(a) - float(b), 6) for a, b in zip(s1, s2)],
-              "eager - eager", [round(float(a) - float(b), 6) for a, b in zip(s4, s2)])
+    runs = {id(m): [m.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
+                    for (obs, vec, ret, cret, v, cv, act, ps, tv) in batches] for m in (m1, m2, m4)}
+    for k in range(len(batches)):
+        s1, s2, s4 = runs[id(m1)][k], runs[id(m2)][k], runs[id(m4)][k]
         # (grad_norm, stats[8], is inf when the fp16 backward overflowed: the AMP step is then
         # skipped on the device and the scale halved -- in both models alike)
         assert all(np.isfinite(float(x)) for i, x in enumerate(s1) if i != 8), (k, s1)
@@ -66,27 +70,19 @@ def test_graphed_updates_equal_eager_updates(deterministic_convs, hip_attention,
             if i == 8 and not (np.isfinite(a) and np.isfinite(b)):
                 assert np.isinf(a) == np.isinf(b), (k, a, b)
                 continue
-            # from the second update on the weights differ by the backward's run-to-run drift (see
-            # below; fp16 stats then move by an ulp): 1 % (the gradient norm, the most sensitive,
-            # 2 %) or the eager twins' own spread at this update
-            tol = 2e-3 * max(1.0, abs(b))
-            if k > 0:
-                tol = max(tol, (2e-2 if i == 8 else 1e-2) * max(1.0, abs(b)), 3 * abs(float(s4[i]) - b))
-            assert abs(a - b) <= tol, (k, i, a, b, float(s4[i]))
-        assert len(m1.network._h16) == 0        # the acting path's fp16 weights are re-read
+            assert abs(a - b) <= max(1e-5 * max(1.0, abs(b)), 3 * abs(float(s4[i]) - b)), (k, i, a, b, float(s4[i]))
+    assert len(m1.network._h16) == 0            # the acting path's fp16 weights are re-read
     upd = next(iter(m1._updates.values()))
     assert upd.graph is not None and upd.eager_runs == upd.WARMUP   # updates 3..6 were replays
     assert not torch.equal(m1.network.conv1.weight, w0)            # ... which moved the weights
-    # the weights after six updates: Adam's steps are ~lr * m / sqrt(v), and the first layers'
-    # fp16 gradients differ by ~2 % between runs of the same eager update (MIOpen's backward
-    # reduction order), which Adam's early steps amplify -- so the graphed deltas are held to the
-    # spread of two eager twins, not to zero
+    # the weights after six updates: equal to the eager twins' (or within their own spread, should
+    # MIOpen's deterministic algorithms still differ between runs)
     delta = lambda m: torch.cat([(p.detach() - p0).flatten() for p, p0 in zip(m.network.parameters(), init)])  # noqa
     d1, d2, d4 = delta(m1), delta(m2), delta(m4)
     r_ge = ((d1 - d2).norm() / d2.norm()).item()
     r_ee = ((d4 - d2).norm() / d2.norm()).item()
     print(f"relative delta difference: graph vs eager {r_ge:.4f}, eager vs eager {r_ee:.4f}")
-    assert d2.norm() > 0 and r_ge <= max(2.5 * r_ee, 0.02), (r_ge, r_ee)
+    assert d2.norm() > 0 and r_ge <= max(2.5 * r_ee, 1e-4), (r_ge, r_ee)
     torch.testing.assert_close(m1._updates[next(iter(m1._updates))].scale,
                                m2._updates[next(iter(m2._updates))].scale)
     # acting after graphed updates == acting of a model holding the same weights
