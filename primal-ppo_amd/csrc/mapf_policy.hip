@@ -566,17 +566,17 @@ __device__ inline void ab_row_to_f32(const char *src, float *f) {
 typedef _Float16 ab_h2_t __attribute__((ext_vector_type(2)));
 // a . row over 32 fp16 pairs with v_dot2_f32_f16 (fp16 products exact in fp32, fp32 sums)
 __device__ inline float ab_dot(const uint32_t *a, const char *row) {
-    float acc = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};               // four independent chains (latency, not issue, bound)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const uint4 u = reinterpret_cast<const uint4 *>(row)[c];
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(ab_h2_t, a[4 * c + e]), __builtin_bit_cast(ab_h2_t, w[e]),
-                                         acc, false);
+            acc[e] = __builtin_amdgcn_fdot2(__builtin_bit_cast(ab_h2_t, a[4 * c + e]), __builtin_bit_cast(ab_h2_t, w[e]),
+                                            acc[e], false);
     }
-    return acc;
+    return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 __device__ inline void ab_load_h(const char *src, uint32_t *a) {
 #pragma unroll
