@@ -363,7 +363,8 @@ int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *
 int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B, int32_t L,
                 int32_t D, float p, uint64_t seed, void *stream);
 /* mapf_tokens (D = 512) and z = LayerNorm(x) as fp16 (gamma, beta, eps) in one pass; bit-identical
- * to mapf_tokens then mapf_layernorm_f16. */
+ * to mapf_tokens then mapf_layernorm_f16.  x may be NULL (the tokens not written: see
+ * mapf_linear512_tokens_residual_layernorm). */
 int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
                           int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
                           float eps, uint16_t *z, void *stream);
@@ -378,6 +379,17 @@ int mapf_linear512_gelu_dropout(const uint16_t *a, const uint16_t *w, const uint
 int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
                                       const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
                                       float p, uint64_t seed, void *stream);
+
+/* mapf_linear512_residual_layernorm on the first block's residual stream without it in HBM: the
+ * input rows x (B sequences x (L + 1) tokens) are the tokens of mapf_tokens (A, VV, cls, pos,
+ * tok_p, tok_seed: same values and mask bits) recomputed in the epilogue; x is written with
+ * tokens + dropout(linear(a)), z = LayerNorm of it.  With mapf_tokens_layernorm(x = NULL, ...)
+ * before it, the tokens' fp32 copy is never written nor read back. */
+int mapf_linear512_tokens_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                             const float *gamma, const float *beta, uint16_t *z, int64_t B, int32_t L,
+                                             float eps, float p, uint64_t seed, const float *tok_A,
+                                             const uint16_t *tok_VV, const float *tok_cls, const float *tok_pos,
+                                             float tok_p, uint64_t tok_seed, void *stream);
 /* out[B][q_rows][512] = softmax(q k^T * scale) v per head (heads = 16, head_dim = 32, n <= 32 tokens;
  * fp16 in/out, fp32 scores and softmax, P rounded to fp16 for P.V like flash SDPA) --
  * transformer.py:48-85's attention for the first q_rows queries.  Strides in fp16 elements between

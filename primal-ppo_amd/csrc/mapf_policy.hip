@@ -268,9 +268,11 @@ __global__ __launch_bounds__(256) void tokens_layernorm(float *__restrict__ x, c
     const int t = (int)(row - b * (L + 1));
     const float4 a = token4(A, VV, cls, pos, b, t, lane, L, 512, row * 128 + lane, thr, scale, seed);
     const float4 c = token4(A, VV, cls, pos, b, t, 64 + lane, L, 512, row * 128 + 64 + lane, thr, scale, seed);
-    float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
-    xr[lane] = a;
-    xr[64 + lane] = c;
+    if (x) {                                        // (null: the next fused linear recomputes the tokens)
+        float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
+        xr[lane] = a;
+        xr[64 + lane] = c;
+    }
     ln_row(a, c, lane, gamma, beta, eps, z + row * 512);
 }
 
@@ -426,13 +428,25 @@ __device__ inline int gl_tile(int r, int n) {
     return r * 1024 + (byte >> 7) * 128 + ((((byte >> 4) & 7) ^ (r & 7)) << 4) + (byte & 15);
 }
 
+// EPI 1 with tok.VV set: the residual stream's input rows are the tokens (mapf_tokens' token4,
+// same mask bits) recomputed here instead of read back from x -- x is only written
+struct TokSrc {
+    const float *A;
+    const uint16_t *VV;
+    const float *cls, *pos;
+    int L;
+    uint32_t thr;
+    float scale;
+    uint64_t seed;
+};
+
 template <int EPI>
 __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
                                                         const uint16_t *__restrict__ bias, long M,
                                                         uint16_t *__restrict__ out, float *__restrict__ x,
                                                         const float *__restrict__ gamma, const float *__restrict__ beta,
                                                         uint16_t *__restrict__ z, float eps, uint32_t thr, float scale,
-                                                        uint64_t seed) {
+                                                        uint64_t seed, TokSrc tok) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -525,8 +539,19 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
             reinterpret_cast<uint2 *>(out)[i1] = o[1];
         } else {
             float4 *xr = reinterpret_cast<float4 *>(x);
-            const float4 a = add_dropped(xr[i0], y0, k0, scale);
-            const float4 c = add_dropped(xr[i1], y1, k1, scale);
+            float4 x0, x1;
+            if (tok.VV) {
+                const long tb = g / (tok.L + 1);
+                const int tt = (int)(g - tb * (tok.L + 1));
+                x0 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, lane, tok.L, 512, i0, tok.thr, tok.scale, tok.seed);
+                x1 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, 64 + lane, tok.L, 512, i1, tok.thr, tok.scale,
+                            tok.seed);
+            } else {
+                x0 = xr[i0];
+                x1 = xr[i1];
+            }
+            const float4 a = add_dropped(x0, y0, k0, scale);
+            const float4 c = add_dropped(x1, y1, k1, scale);
             xr[i0] = a;
             xr[i1] = c;
             ln_row(a, c, lane, gamma, beta, eps, z + g * 512);
@@ -752,7 +777,7 @@ int mapf_linear512_gelu_dropout(const uint16_t *a, const uint16_t *w, const uint
     if (rows == 0) return MAPF_OK;
     hipLaunchKernelGGL(pol::linear512_kernel<0>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
                        pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, out, nullptr, nullptr, nullptr,
-                       nullptr, 0.f, pol::drop_threshold(p), 1.f / (1.f - p), seed);
+                       nullptr, 0.f, pol::drop_threshold(p), 1.f / (1.f - p), seed, pol::TokSrc{});
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
@@ -763,7 +788,25 @@ int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, cons
     if (rows == 0) return MAPF_OK;
     hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
                        pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
-                       pol::drop_threshold(p), 1.f / (1.f - p), seed);
+                       pol::drop_threshold(p), 1.f / (1.f - p), seed, pol::TokSrc{});
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_linear512_tokens_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                             const float *gamma, const float *beta, uint16_t *z, int64_t B, int32_t L,
+                                             float eps, float p, uint64_t seed, const float *tok_A,
+                                             const uint16_t *tok_VV, const float *tok_cls, const float *tok_pos,
+                                             float tok_p, uint64_t tok_seed, void *stream) {
+    if (!a || !w || !bias || !x || !gamma || !beta || !z || !tok_A || !tok_VV || !tok_cls || !tok_pos || B < 0 ||
+        L < 1 || !(p >= 0.f && p < 1.f) || !(tok_p >= 0.f && tok_p < 1.f))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const long rows = (long)B * (L + 1);
+    const pol::TokSrc tok{tok_A, tok_VV, tok_cls, tok_pos, (int)L, pol::drop_threshold(tok_p), 1.f / (1.f - tok_p),
+                          tok_seed};
+    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
+                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, rows, nullptr, x, gamma, beta, z, eps,
+                       pol::drop_threshold(p), 1.f / (1.f - p), seed, tok);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
@@ -781,8 +824,7 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
 int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
                           int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
                           float eps, uint16_t *z, void *stream) {
-    if (!x || !A || !VV || !cls || !pos || !gamma || !beta || !z || B < 0 || L < 1 || D != 512 ||
-        !(p >= 0.f && p < 1.f))
+    if (!A || !VV || !cls || !pos || !gamma || !beta || !z || B < 0 || L < 1 || D != 512 || !(p >= 0.f && p < 1.f))
         return MAPF_EINVAL;
     if (B == 0) return MAPF_OK;
     const long rows = (long)B * (L + 1);

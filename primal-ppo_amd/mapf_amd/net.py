@@ -375,17 +375,25 @@ class SCRIMPNet(nn.Module):
             VV = torch.matmul(hf, h16(self.token_wV, "sum")).contiguous()      # [b, 512] fp16
             xt = torch.empty(b, self.L + 1, self.cT, dtype=torch.float32, device=dev)
             cls, pos = self.cls_token.detach().contiguous(), self.pos_embedding.detach().contiguous()
-            y0 = None
+            y0 = tok = None
             if self.fused_residual_ln:                     # tokens + the first LayerNorm in one pass
                 norm = self.transformer.layers[0][0].fn.norm
                 y0 = torch.empty(xt.shape, dtype=torch.float16, device=dev)
-                chk(lib.mapf_tokens_layernorm(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
-                                              drop(self.dropout), next(seeds), ptr(norm.weight), ptr(norm.bias),
+                # the first block's fused out-projection recomputes the tokens (same mask bits): their
+                # fp32 copy is then never written nor read back (mapf_linear512_tokens_residual_layernorm)
+                layers = self.transformer.layers
+                recompute = (self.fused_linear and self.cT == 512 and len(layers) >= 2 and
+                             layers[0][0].fn.fn.nn1.weight.shape == (512, 512))
+                p_tok, seed_tok = drop(self.dropout), next(seeds)
+                chk(lib.mapf_tokens_layernorm(None if recompute else ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b,
+                                              self.L, self.cT, p_tok, seed_tok, ptr(norm.weight), ptr(norm.bias),
                                               float(norm.eps), ptr(y0), st))
+                if recompute:
+                    tok = (A, VV, cls, pos, p_tok, seed_tok)
             else:
                 chk(lib.mapf_tokens(ptr(xt), ptr(A), ptr(VV), ptr(cls), ptr(pos), b, self.L, self.cT,
                                     drop(self.dropout), next(seeds), st))
-            x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop, y0)[:, 0]
+            x = self._encoder_fused(xt, lib, chk, st, ptr, seeds, drop, y0, tok)[:, 0]
             x = lin(self.nn_same, lin(self.nn_same, x))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)
@@ -418,10 +426,11 @@ class SCRIMPNet(nn.Module):
     def _lin16(self, m, x):
         return F.linear(x, self._half(m.weight), None if m.bias is None else self._half(m.bias))
 
-    def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop, y0=None):
+    def _encoder_fused(self, x, lib, chk, st, ptr, seeds, drop, y0=None, tok=None):
         """self.transformer(x, first_only=True) on the fused epilogues; x fp32 [b, n, d] is
         updated in place (the residual stream) and token 0 after the last block returned; y0 is
-        the first block's LayerNorm of x when the caller already computed it."""
+        the first block's LayerNorm of x when the caller already computed it; tok = (A, VV, cls,
+        pos, p, seed) when x was NOT written and the first fused out-projection recomputes it."""
         layers = self.transformer.layers
         b, n, d = x.shape
         h16, lin = self._half, self._lin16
@@ -444,11 +453,19 @@ class SCRIMPNet(nn.Module):
 
         fused_lin = self.fused_linear and d == 512 and self.fused_residual_ln
 
-        def lin_residual(m, inp, x, drop_m, norm):     # x += dropout(m(inp)); LayerNorm(x) -> fp16, one launch
+        def lin_residual(m, inp, x, drop_m, norm, tok=None):   # x += dropout(m(inp)); LayerNorm(x) -> fp16
             if not fused_lin or norm is None or m.weight.shape != (512, 512):
+                assert tok is None
                 return residual(x, lin(m, inp), drop_m, norm)
             inp = inp.contiguous()
             z = torch.empty(x.shape, dtype=torch.float16, device=x.device)
+            if tok is not None:                         # x = tokens (recomputed) + dropout(m(inp))
+                A, VV, cls, pos, p_tok, seed_tok = tok
+                chk(lib.mapf_linear512_tokens_residual_layernorm(
+                    ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x), ptr(norm.weight), ptr(norm.bias), ptr(z),
+                    x.shape[0], x.shape[1] - 1, float(norm.eps), drop(drop_m), next(seeds), ptr(A), ptr(VV), ptr(cls),
+                    ptr(pos), p_tok, seed_tok, st))
+                return z
             chk(lib.mapf_linear512_residual_layernorm(ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x),
                                                       ptr(norm.weight), ptr(norm.bias), ptr(z), x.numel() // d,
                                                       float(norm.eps), drop(drop_m), next(seeds), st))
@@ -486,7 +503,7 @@ class SCRIMPNet(nn.Module):
                     qkv = qkv.view(b, n, 3, hh, d // hh).permute(2, 0, 3, 1, 4)
                     out = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], scale=a.scale)
                     out = out.transpose(1, 2).reshape(b, n, d)
-                yf = lin_residual(a.nn1, out, x, a.do1, ff.fn.norm)
+                yf = lin_residual(a.nn1, out, x, a.do1, ff.fn.norm, tok if li == 0 else None)
             else:                               # the last block: token 0's query only (see _Encoder)
                 w, bias = a.to_qkv.weight, a.to_qkv.bias
                 q = F.linear(y[:, 0], h16(w, "q"), h16(bias, "q"))

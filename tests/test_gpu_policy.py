@@ -215,6 +215,42 @@ def test_tokens_layernorm_equals_two_launches():
             torch.testing.assert_close(x1, ref, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("B", [1, 7, 333])
+def test_linear512_tokens_variant_equals_tokens_then_linear512(B):
+    """mapf_tokens_layernorm(x = NULL) + mapf_linear512_tokens_residual_layernorm (the tokens
+    recomputed in the epilogue) == mapf_tokens_layernorm(x) + mapf_linear512_residual_layernorm:
+    bit-identical LayerNorm input, residual stream and LayerNorm output, dropout on and off."""
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L, D = 16, 512
+    gen = torch.Generator(device="cuda").manual_seed(B)
+    A = torch.rand(B, L, device="cuda", generator=gen)
+    VV = torch.randn(B, D, device="cuda", generator=gen).half()
+    cls, pos = torch.randn(D, device="cuda", generator=gen), torch.randn(L + 1, D, device="cuda", generator=gen)
+    g0, e0 = torch.rand(D, device="cuda", generator=gen) + 0.5, torch.randn(D, device="cuda", generator=gen)
+    g1, e1 = torch.rand(D, device="cuda", generator=gen) + 0.5, torch.randn(D, device="cuda", generator=gen)
+    a = torch.randn(B * (L + 1), D, device="cuda", generator=gen).half()
+    w = (torch.randn(D, D, device="cuda", generator=gen) / D ** 0.5).half()
+    bias = (torch.randn(D, device="cuda", generator=gen) * 0.1).half()
+    for p_tok, p in ((0.0, 0.0), (0.1, 0.2)):
+        x1 = torch.empty(B, L + 1, D, device="cuda")
+        y1, y2 = (torch.empty(B, L + 1, D, dtype=torch.float16, device="cuda") for _ in range(2))
+        _lib.check(lib.mapf_tokens_layernorm(_p(x1), _p(A), _p(VV), _p(cls), _p(pos), B, L, D, p_tok, 11, _p(g0),
+                                             _p(e0), 1e-5, _p(y1), st))
+        _lib.check(lib.mapf_tokens_layernorm(None, _p(A), _p(VV), _p(cls), _p(pos), B, L, D, p_tok, 11, _p(g0), _p(e0),
+                                             1e-5, _p(y2), st))
+        z1, z2 = (torch.empty(B, L + 1, D, dtype=torch.float16, device="cuda") for _ in range(2))
+        x2 = torch.full_like(x1, float("nan"))
+        _lib.check(lib.mapf_linear512_residual_layernorm(_p(a), _p(w), _p(bias), _p(x1), _p(g1), _p(e1), _p(z1),
+                                                         B * (L + 1), 1e-5, p, 22, st))
+        _lib.check(lib.mapf_linear512_tokens_residual_layernorm(_p(a), _p(w), _p(bias), _p(x2), _p(g1), _p(e1), _p(z2),
+                                                                B, L, 1e-5, p, 22, _p(A), _p(VV), _p(cls), _p(pos),
+                                                                p_tok, 11, st))
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2) and torch.equal(x1, x2) and torch.equal(z1, z2), (p_tok, p)
+
+
 def test_fp16_weight_cache_follows_in_place_updates():
     net = _net().eval()
     obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.25).float()
