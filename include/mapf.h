@@ -380,6 +380,13 @@ int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, cons
                                       const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
                                       float p, uint64_t seed, void *stream);
 
+/* mapf_linear512_residual_layernorm that writes the updated residual rows back only for rows
+ * g % x_every == 0 (z for every row): before a block that keeps only token 0 of the stream
+ * (the encoder's last block), the other tokens' fp32 rows are never needed again. */
+int mapf_linear512_residual_layernorm_rows(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                           const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
+                                           float p, uint64_t seed, int32_t x_every, void *stream);
+
 /* mapf_linear512_residual_layernorm on the first block's residual stream without it in HBM: the
  * input rows x (B sequences x (L + 1) tokens) are the tokens of mapf_tokens (A, VV, cls, pos,
  * tok_p, tok_seed: same values and mask bits) recomputed in the epilogue; x is written with

@@ -438,6 +438,7 @@ struct TokSrc {
     uint32_t thr;
     float scale;
     uint64_t seed;
+    int x_every;        // > 1: write back only rows g with g % x_every == 0 (token 0 of each sequence)
 };
 
 template <int EPI>
@@ -552,8 +553,10 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
             }
             const float4 a = add_dropped(x0, y0, k0, scale);
             const float4 c = add_dropped(x1, y1, k1, scale);
-            xr[i0] = a;
-            xr[i1] = c;
+            if (tok.x_every <= 1 || g % tok.x_every == 0) {
+                xr[i0] = a;
+                xr[i1] = c;
+            }
             ln_row(a, c, lane, gamma, beta, eps, z + g * 512);
         }
     }
@@ -792,6 +795,20 @@ int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, cons
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
+int mapf_linear512_residual_layernorm_rows(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
+                                           const float *gamma, const float *beta, uint16_t *z, int64_t rows, float eps,
+                                           float p, uint64_t seed, int32_t x_every, void *stream) {
+    if (!a || !w || !bias || !x || !gamma || !beta || !z || rows < 0 || x_every < 1 || !(p >= 0.f && p < 1.f))
+        return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    pol::TokSrc tok{};
+    tok.x_every = x_every;
+    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
+                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
+                       pol::drop_threshold(p), 1.f / (1.f - p), seed, tok);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
 int mapf_linear512_tokens_residual_layernorm(const uint16_t *a, const uint16_t *w, const uint16_t *bias, float *x,
                                              const float *gamma, const float *beta, uint16_t *z, int64_t B, int32_t L,
                                              float eps, float p, uint64_t seed, const float *tok_A,
@@ -803,7 +820,7 @@ int mapf_linear512_tokens_residual_layernorm(const uint16_t *a, const uint16_t *
     if (B == 0) return MAPF_OK;
     const long rows = (long)B * (L + 1);
     const pol::TokSrc tok{tok_A, tok_VV, tok_cls, tok_pos, (int)L, pol::drop_threshold(tok_p), 1.f / (1.f - tok_p),
-                          tok_seed};
+                          tok_seed, 1};
     hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
                        pol::GL_LDS, (hipStream_t)stream, a, w, bias, rows, nullptr, x, gamma, beta, z, eps,
                        pol::drop_threshold(p), 1.f / (1.f - p), seed, tok);

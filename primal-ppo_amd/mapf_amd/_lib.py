@@ -109,6 +109,8 @@ SIGNATURES = {
     "mapf_linear512_gelu_dropout": (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_linear512_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float, ctypes.c_float,
                                                           ctypes.c_uint64, P]),
+    "mapf_linear512_residual_layernorm_rows": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float,
+                                                              ctypes.c_float, ctypes.c_uint64, I32, P]),
     "mapf_linear512_tokens_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, P, P, I64, I32, ctypes.c_float,
                                                                 ctypes.c_float, ctypes.c_uint64, P, P, P, P,
                                                                 ctypes.c_float, ctypes.c_uint64, P]),

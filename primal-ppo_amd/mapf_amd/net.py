@@ -453,7 +453,7 @@ class SCRIMPNet(nn.Module):
 
         fused_lin = self.fused_linear and d == 512 and self.fused_residual_ln
 
-        def lin_residual(m, inp, x, drop_m, norm, tok=None):   # x += dropout(m(inp)); LayerNorm(x) -> fp16
+        def lin_residual(m, inp, x, drop_m, norm, tok=None, x_every=1):   # x += dropout(m(inp)); LayerNorm(x)
             if not fused_lin or norm is None or m.weight.shape != (512, 512):
                 assert tok is None
                 return residual(x, lin(m, inp), drop_m, norm)
@@ -465,6 +465,11 @@ class SCRIMPNet(nn.Module):
                     ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x), ptr(norm.weight), ptr(norm.bias), ptr(z),
                     x.shape[0], x.shape[1] - 1, float(norm.eps), drop(drop_m), next(seeds), ptr(A), ptr(VV), ptr(cls),
                     ptr(pos), p_tok, seed_tok, st))
+                return z
+            if x_every > 1:                             # only token 0's residual rows are read again
+                chk(lib.mapf_linear512_residual_layernorm_rows(
+                    ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x), ptr(norm.weight), ptr(norm.bias), ptr(z),
+                    x.numel() // d, float(norm.eps), drop(drop_m), next(seeds), x_every, st))
                 return z
             chk(lib.mapf_linear512_residual_layernorm(ptr(inp), ptr(h16(m.weight)), ptr(h16(m.bias)), ptr(x),
                                                       ptr(norm.weight), ptr(norm.bias), ptr(z), x.numel() // d,
@@ -519,5 +524,7 @@ class SCRIMPNet(nn.Module):
                 x = x[:, :1].contiguous()
                 yf = lin_residual(a.nn1, out, x, a.do1, ff.fn.norm)
             hid = lin_gelu(f.nn1, yf, f.do1)
-            y = lin_residual(f.nn2, hid, x, f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None)
+            # before the last block only token 0 of the stream is carried on (x[:, :1] below)
+            y = lin_residual(f.nn2, hid, x, f.do2, layers[li + 1][0].fn.norm if li + 1 < len(layers) else None,
+                             x_every=n if li + 2 == len(layers) and x.shape[1] == n else 1)
         return x

@@ -251,6 +251,30 @@ def test_linear512_tokens_variant_equals_tokens_then_linear512(B):
         assert torch.equal(y1, y2) and torch.equal(x1, x2) and torch.equal(z1, z2), (p_tok, p)
 
 
+def test_linear512_rows_variant_writes_back_every_kth_row():
+    """mapf_linear512_residual_layernorm_rows(x_every = 17): z as the full launch for every row, the
+    residual written back for rows 0, 17, 34, ... only (the rest untouched)"""
+    from mapf_amd import _lib
+    lib = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    rows, k = 17 * 41, 17
+    a = torch.randn(rows, 512, device="cuda", generator=gen).half()
+    w = (torch.randn(512, 512, device="cuda", generator=gen) / 512 ** 0.5).half()
+    bias = (torch.randn(512, device="cuda", generator=gen) * 0.1).half()
+    g1, e1 = torch.rand(512, device="cuda", generator=gen) + 0.5, torch.randn(512, device="cuda", generator=gen)
+    x0 = torch.randn(rows, 512, device="cuda", generator=gen)
+    x1, x2 = x0.clone(), x0.clone()
+    z1, z2 = (torch.empty(rows, 512, dtype=torch.float16, device="cuda") for _ in range(2))
+    _lib.check(lib.mapf_linear512_residual_layernorm(_p(a), _p(w), _p(bias), _p(x1), _p(g1), _p(e1), _p(z1), rows,
+                                                     1e-5, 0.1, 3, st))
+    _lib.check(lib.mapf_linear512_residual_layernorm_rows(_p(a), _p(w), _p(bias), _p(x2), _p(g1), _p(e1), _p(z2), rows,
+                                                          1e-5, 0.1, 3, k, st))
+    torch.cuda.synchronize()
+    keep = torch.arange(rows, device="cuda") % k == 0
+    assert torch.equal(z1, z2) and torch.equal(x2[keep], x1[keep]) and torch.equal(x2[~keep], x0[~keep])
+
+
 def test_fp16_weight_cache_follows_in_place_updates():
     net = _net().eval()
     obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.25).float()
