@@ -141,6 +141,54 @@ __device__ inline void ln_row(float4 a, float4 c, int lane, const float *__restr
     yr[64 + lane] = pack4(o[4], o[5], o[6], o[7]);
 }
 
+// ln_row for R rows a wave holds at once: every row's sums in ln_row's order, the R
+// cross-lane reductions interleaved step by step (independent shuffles in flight together
+// instead of one dependent chain per row); bit-identical to R ln_row calls.  Rows with
+// live[r] false are computed but not stored.
+template <int R>
+__device__ inline void ln_rows(const float4 *a, const float4 *c, const bool *live, int lane,
+                               const float *__restrict__ gamma, const float *__restrict__ beta, float eps,
+                               uint16_t *const *y) {
+    constexpr int D = 512;
+    float sm[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) sm[r] = a[r].x + a[r].y + a[r].z + a[r].w + c[r].x + c[r].y + c[r].z + c[r].w;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1)
+#pragma unroll
+        for (int r = 0; r < R; ++r) sm[r] += __shfl_xor(sm[r], st, 64);
+    float d[R][8], ss[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float mean = sm[r] * (1.f / D);
+        d[r][0] = a[r].x - mean; d[r][1] = a[r].y - mean; d[r][2] = a[r].z - mean; d[r][3] = a[r].w - mean;
+        d[r][4] = c[r].x - mean; d[r][5] = c[r].y - mean; d[r][6] = c[r].z - mean; d[r][7] = c[r].w - mean;
+        ss[r] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ss[r] += d[r][k] * d[r][k];
+    }
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1)
+#pragma unroll
+        for (int r = 0; r < R; ++r) ss[r] += __shfl_xor(ss[r], st, 64);
+    const float4 g0 = reinterpret_cast<const float4 *>(gamma)[lane], g1 = reinterpret_cast<const float4 *>(gamma)[64 + lane];
+    const float4 e0 = reinterpret_cast<const float4 *>(beta)[lane], e1 = reinterpret_cast<const float4 *>(beta)[64 + lane];
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float rstd = 1.f / sqrtf(ss[r] * (1.f / D) + eps);
+        uint32_t o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = f2h(d[r][k] * rstd * g[k] + e[k]);
+        if (live[r]) {
+            uint2 *yr = reinterpret_cast<uint2 *>(y[r]);
+            yr[lane] = pack4(o[0], o[1], o[2], o[3]);
+            yr[64 + lane] = pack4(o[4], o[5], o[6], o[7]);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x, long xstride,
                                                      const float *__restrict__ gamma, const float *__restrict__ beta,
                                                      uint16_t *__restrict__ y, long rows, float eps) {
@@ -512,7 +560,53 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
         }
     }
     __syncthreads();
-    // elementwise epilogue: wave w takes rows w, w + 8, ...; lane holds columns 4l..4l+3 and 256+4l..
+    if (EPI == 1) {
+        // wave w takes rows w, w + 8, ..., four at a time (ln_rows: their reductions interleaved)
+        constexpr int R = 4;
+        for (int row0 = wave; row0 < GL_BM; row0 += 8 * R) {
+            float4 av[R], cv[R];
+            bool live[R];
+            uint16_t *zr[R];
+            float4 *xr = reinterpret_cast<float4 *>(x);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int row = row0 + 8 * r;
+                const long g = m0 + row;
+                live[r] = row < GL_BM && g < M;
+                zr[r] = z + (live[r] ? g : 0) * 512;
+                if (!live[r]) {
+                    av[r] = cv[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    continue;
+                }
+                const uint2 y0 = *reinterpret_cast<const uint2 *>(smem + gl_tile(row, 4 * lane));
+                const uint2 y1 = *reinterpret_cast<const uint2 *>(smem + gl_tile(row, 256 + 4 * lane));
+                const long i0 = g * 128 + lane, i1 = i0 + 64;
+                const unsigned k0 = thr ? keep4(seed, (uint64_t)i0, thr) : 15u;
+                const unsigned k1 = thr ? keep4(seed, (uint64_t)i1, thr) : 15u;
+                float4 x0, x1;
+                if (tok.VV) {
+                    const long tb = g / (tok.L + 1);
+                    const int tt = (int)(g - tb * (tok.L + 1));
+                    x0 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, lane, tok.L, 512, i0, tok.thr, tok.scale,
+                                tok.seed);
+                    x1 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, 64 + lane, tok.L, 512, i1, tok.thr,
+                                tok.scale, tok.seed);
+                } else {
+                    x0 = xr[i0];
+                    x1 = xr[i1];
+                }
+                av[r] = add_dropped(x0, y0, k0, scale);
+                cv[r] = add_dropped(x1, y1, k1, scale);
+                if (tok.x_every <= 1 || g % tok.x_every == 0) {
+                    xr[i0] = av[r];
+                    xr[i1] = cv[r];
+                }
+            }
+            ln_rows<R>(av, cv, live, lane, gamma, beta, eps, zr);
+        }
+        return;
+    }
+    // EPI 0 (GELU + dropout): wave w takes rows w, w + 8, ...; lane holds columns 4l..4l+3 and 256+4l..
     for (int row = wave; row < GL_BM; row += 8) {
         const long g = m0 + row;
         if (g >= M) break;
@@ -538,26 +632,6 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
             }
             reinterpret_cast<uint2 *>(out)[i0] = o[0];
             reinterpret_cast<uint2 *>(out)[i1] = o[1];
-        } else {
-            float4 *xr = reinterpret_cast<float4 *>(x);
-            float4 x0, x1;
-            if (tok.VV) {
-                const long tb = g / (tok.L + 1);
-                const int tt = (int)(g - tb * (tok.L + 1));
-                x0 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, lane, tok.L, 512, i0, tok.thr, tok.scale, tok.seed);
-                x1 = token4(tok.A, tok.VV, tok.cls, tok.pos, tb, tt, 64 + lane, tok.L, 512, i1, tok.thr, tok.scale,
-                            tok.seed);
-            } else {
-                x0 = xr[i0];
-                x1 = xr[i1];
-            }
-            const float4 a = add_dropped(x0, y0, k0, scale);
-            const float4 c = add_dropped(x1, y1, k1, scale);
-            if (tok.x_every <= 1 || g % tok.x_every == 0) {
-                xr[i0] = a;
-                xr[i1] = c;
-            }
-            ln_row(a, c, lane, gamma, beta, eps, z + g * 512);
         }
     }
 }
