@@ -309,19 +309,35 @@ __global__ __launch_bounds__(256) void tokens_layernorm(float *__restrict__ x, c
                                                         float scale, uint64_t seed, const float *__restrict__ gamma,
                                                         const float *__restrict__ beta, float eps,
                                                         uint16_t *__restrict__ z) {
+    // four rows per wave (ln_rows: their reductions interleaved), 16 per block
+    constexpr int R = 4;
     const int lane = (int)(threadIdx.x & 63);
-    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= B * (L + 1)) return;
-    const long b = row / (L + 1);
-    const int t = (int)(row - b * (L + 1));
-    const float4 a = token4(A, VV, cls, pos, b, t, lane, L, 512, row * 128 + lane, thr, scale, seed);
-    const float4 c = token4(A, VV, cls, pos, b, t, 64 + lane, L, 512, row * 128 + 64 + lane, thr, scale, seed);
-    if (x) {                                        // (null: the next fused linear recomputes the tokens)
-        float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
-        xr[lane] = a;
-        xr[64 + lane] = c;
+    const long rows = B * (L + 1);
+    const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+    if (row0 >= rows) return;
+    float4 av[R], cv[R];
+    bool live[R];
+    uint16_t *zr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const long row = row0 + r;
+        live[r] = row < rows;
+        zr[r] = z + (live[r] ? row : 0) * 512;
+        if (!live[r]) {
+            av[r] = cv[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            continue;
+        }
+        const long b = row / (L + 1);
+        const int t = (int)(row - b * (L + 1));
+        av[r] = token4(A, VV, cls, pos, b, t, lane, L, 512, row * 128 + lane, thr, scale, seed);
+        cv[r] = token4(A, VV, cls, pos, b, t, 64 + lane, L, 512, row * 128 + 64 + lane, thr, scale, seed);
+        if (x) {                                    // (null: the next fused linear recomputes the tokens)
+            float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
+            xr[lane] = av[r];
+            xr[64 + lane] = cv[r];
+        }
     }
-    ln_row(a, c, lane, gamma, beta, eps, z + row * 512);
+    ln_rows<R>(av, cv, live, lane, gamma, beta, eps, zr);
 }
 
 // ---- attention over a short token axis (transformer.py:48-85; n <= 32 tokens) -----
@@ -919,7 +935,7 @@ int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const fl
         return MAPF_EINVAL;
     if (B == 0) return MAPF_OK;
     const long rows = (long)B * (L + 1);
-    hipLaunchKernelGGL(pol::tokens_layernorm, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, A,
+    hipLaunchKernelGGL(pol::tokens_layernorm, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, (hipStream_t)stream, x, A,
                        VV, cls, pos, (long)B, (int)L, pol::drop_threshold(p), 1.f / (1.f - p), seed, gamma, beta, eps,
                        z);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
