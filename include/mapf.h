@@ -442,6 +442,13 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
                        int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, int32_t relu,
                        void *stream);
 
+/* mapf_conv_nhwc_f16 + bias + ReLU + 2x2 max-pool (net.py:106-107 / 110-111: relu(conv) then
+ * MaxPool2d(2), floor), y fp16 NHWC [nimg][Ho / 2][Wo / 2][Cout]: the conv's output never goes to
+ * HBM (tiles of whole images; 128 -> 128 3x3 and 256 -> 256 2x2 with Ho * Wo <= the tile).
+ * Same values as mapf_conv_nhwc_f16(relu = 0) then mapf_nhwc_bias_relu_pool2. */
+int mapf_conv_nhwc_pool_f16(const uint16_t *x, const uint16_t *w_packed, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                            int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, void *stream);
+
 /* conv1 (net.py:104, 3x3, padding 1, Cin = num_channel <= 7, Cout = 128) from the fp32 NCHW observation
  * x_nchw [nimg][Cin][H][W] (cast to fp16 as autocast does); w fp16 [Cout][64]: torch's [Cout][Cin][3][3]
  * flattened per output channel (K = Cin * 9 in (c, ky, kx) order) and zero-padded to 64;

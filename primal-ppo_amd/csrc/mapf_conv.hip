@@ -216,19 +216,22 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
                                                                   const uint16_t *__restrict__ w,
                                                                   const uint16_t *__restrict__ bias,
                                                                   uint16_t *__restrict__ out, int M, int H, int W,
-                                                                  int Ho, int Wo, int pad, int epi) {
+                                                                  int Ho, int Wo, int pad, int epi, int ipt) {
+    // ipt > 0: tiles of ipt whole images (ipt * Ho * Wo <= BM rows, the rest padding) and a pooled
+    // epilogue: out = relu(fp16(max2x2(conv) + bias)), [img][Ho / 2][Wo / 2][COUT] (nhwc_bias_relu_pool2)
     using C = Cfg32<CIN, COUT, KS, WAVES, STAGES>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int m0 = (int)blockIdx.x * C::BM;
     const int HWo = Ho * Wo;
+    const int rows_here = ipt ? ipt * HWo : C::BM;     // tile rows that are output pixels
+    const int m0 = (int)blockIdx.x * rows_here;
     const int q = (lane & 3) ^ ((lane >> 4) & 3);          // logical piece of this lane's 16 B
     int apix[C::JA], ayx[C::JA];
 #pragma unroll
     for (int j = 0; j < C::JA; ++j) {
-        const int m = m0 + 16 * (wave * C::JA + j) + (lane >> 2);
-        if (m < M) {
+        const int r = 16 * (wave * C::JA + j) + (lane >> 2), m = m0 + r;
+        if (r < rows_here && m < M) {
             const int img = m / HWo, pos = m - img * HWo, oy = pos / Wo, ox = pos - oy * Wo;
             apix[j] = img * H * W + oy * W + ox;
             ayx[j] = (oy << 16) | ox;
@@ -306,13 +309,43 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
     }
     __syncthreads();
     constexpr int PIECES_ROW = RB / 16;
+    auto piece = [&](int row, int pc) {
+        return *reinterpret_cast<const uint4 *>(T + row * RB + (pc >> 3) * 128 + (((pc & 7) ^ (row & 7)) << 4));
+    };
+    if (ipt) {                                        // 2x2 max-pool + bias + ReLU of whole images
+        const int Hp = Ho >> 1, Wp = Wo >> 1, img0 = (int)blockIdx.x * ipt;
+        const int nimg_here = min(ipt, M / HWo - img0);
+        const int items = nimg_here * Hp * Wp * PIECES_ROW;
+        for (int p = t; p < items; p += C::THREADS) {
+            const int pc = p % PIECES_ROW, cell = p / PIECES_ROW;
+            const int il = cell / (Hp * Wp), rem = cell - il * (Hp * Wp), pi = rem / Wp, pj = rem - pi * Wp;
+            const int r00 = il * HWo + 2 * pi * Wo + 2 * pj;
+            const uint4 v[4] = {piece(r00, pc), piece(r00 + 1, pc), piece(r00 + Wo, pc), piece(r00 + Wo + 1, pc)};
+            const uint4 bb = *reinterpret_cast<const uint4 *>(bias + pc * 8);
+            const uint32_t bw[4] = {bb.x, bb.y, bb.z, bb.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {                  // 2 channels per dword
+                const uint32_t w0 = (&v[0].x)[e], w1 = (&v[1].x)[e], w2 = (&v[2].x)[e], w3 = (&v[3].x)[e];
+                uint32_t h2[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int sh = 16 * hh;
+                    const float m = fmaxf(fmaxf(h2f(w0 >> sh), h2f(w1 >> sh)), fmaxf(h2f(w2 >> sh), h2f(w3 >> sh)));
+                    h2[hh] = f2h(fmaxf(h2f(f2h(m + h2f(bw[e] >> sh))), 0.f));
+                }
+                o[e] = h2[0] | (h2[1] << 16);
+            }
+            *reinterpret_cast<uint4 *>(out + ((size_t)(img0 + il) * Hp * Wp + pi * Wp + pj) * COUT + pc * 8) =
+                make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        return;
+    }
     for (int p = t; p < C::BM * PIECES_ROW; p += C::THREADS) {
         const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
         const int m = m0 + row;
         if (m >= M) continue;
-        const int g = pc >> 3, pq = pc & 7;
-        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) =
-            *reinterpret_cast<const uint4 *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4));
+        *reinterpret_cast<uint4 *>(out + (size_t)m * COUT + pc * 8) = piece(row, pc);
     }
 }
 
@@ -322,11 +355,17 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
 
 template <int CIN, int COUT, int KS, int WAVES>
 static void launch(const uint16_t *in, const uint16_t *w, const uint16_t *bias, uint16_t *out, int M, int H, int W,
-                   int Ho, int Wo, int pad, int epi, hipStream_t s) {
+                   int Ho, int Wo, int pad, int epi, hipStream_t s, bool pool = false) {
 #if MAPF_CONV_STAGES
     using C = Cfg32<CIN, COUT, KS, WAVES, MAPF_CONV_STAGES>;
+    if (pool) {                                   // whole images per tile (the caller checked Ho * Wo <= BM)
+        const int ipt = C::BM / (Ho * Wo), nimg = M / (Ho * Wo);
+        hipLaunchKernelGGL((conv_igemm32_kernel<CIN, COUT, KS, WAVES, MAPF_CONV_STAGES>), dim3((nimg + ipt - 1) / ipt),
+                           dim3(C::THREADS), C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, 0, ipt);
+        return;
+    }
     hipLaunchKernelGGL((conv_igemm32_kernel<CIN, COUT, KS, WAVES, MAPF_CONV_STAGES>), dim3((M + C::BM - 1) / C::BM),
-                       dim3(C::THREADS), C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi);
+                       dim3(C::THREADS), C::LDS, s, in, w, bias, out, M, H, W, Ho, Wo, pad, epi, 0);
 #else
     using C = Cfg<CIN, COUT, KS, WAVES>;
     hipLaunchKernelGGL((conv_igemm_kernel<CIN, COUT, KS, WAVES>), dim3((M + C::BM - 1) / C::BM), dim3(C::THREADS),
@@ -474,6 +513,29 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
     else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else return MAPF_EINVAL;
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_conv_nhwc_pool_f16(const uint16_t *x, const uint16_t *w_packed, const uint16_t *bias, uint16_t *y, int64_t nimg,
+                            int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, void *stream) {
+#if MAPF_CONV_STAGES
+    if (!x || !w_packed || !bias || !y) return MAPF_EINVAL;
+    if (nimg < 1 || H < 1 || W < 1 || pad < 0 || pad >= ks) return MAPF_EINVAL;
+    const int Ho = H + 2 * pad - ks + 1, Wo = W + 2 * pad - ks + 1;
+    if (Ho < 2 || Wo < 2) return MAPF_EINVAL;
+    const int64_t M64 = nimg * Ho * Wo;
+    if (M64 > (int64_t)0x7FFFFFFF - 1024 || nimg * H * W > (int64_t)0x7FFFFFFF / 512) return MAPF_EINVAL;
+    const int M = (int)M64;
+    hipStream_t s = (hipStream_t)stream;
+    // (8 waves for the 128-channel form too: 256-row tiles hold 3 whole 9 x 9 images, 5 % padding)
+    if (Cin == 128 && Cout == 128 && ks == 3 && Ho * Wo <= conv::Cfg32<128, 128, 3, 8, MAPF_CONV_STAGES>::BM)
+        conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, 0, s, true);
+    else if (Cin == 256 && Cout == 256 && ks == 2 && Ho * Wo <= conv::Cfg32<256, 256, 2, 8, MAPF_CONV_STAGES>::BM)
+        conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, 0, s, true);
+    else return MAPF_EINVAL;
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+#else
+    return MAPF_EINVAL;
+#endif
 }
 
 int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *bias, uint16_t *y, int64_t nimg,

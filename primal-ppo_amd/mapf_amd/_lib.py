@@ -114,6 +114,7 @@ SIGNATURES = {
     "mapf_linear512_tokens_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, P, P, I64, I32, ctypes.c_float,
                                                                 ctypes.c_float, ctypes.c_uint64, P, P, P, P,
                                                                 ctypes.c_float, ctypes.c_uint64, P]),
+    "mapf_conv_nhwc_pool_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P]),
     "mapf_conv_first_f32": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, P]),
     "mapf_conv_nhwc_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P]),
     "mapf_attention_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I32, I32, ctypes.c_float, P]),

@@ -321,6 +321,19 @@ class SCRIMPNet(nn.Module):
             def conv(x, m, pool=False):        # F.relu(conv(x)) (+ pool): bias and ReLU in the epilogue kernel
                 b = h16(m.bias)
                 co, ci, ks, _ = m.weight.shape
+                if (pool and self.own_conv and (ci, co, ks) in ((128, 128, 3), (256, 256, 2)) and
+                        x.is_contiguous(memory_format=torch.channels_last)):
+                    # conv + bias + ReLU + 2x2 max-pool in one launch (mapf_conv_nhwc_pool_f16): the
+                    # conv's output never reaches HBM
+                    p = m.padding[0]
+                    B_, _, H_, W_ = x.shape
+                    Ho_, Wo_ = H_ + 2 * p - ks + 1, W_ + 2 * p - ks + 1
+                    yp = torch.empty((B_, co, Ho_ // 2, Wo_ // 2), dtype=torch.float16, device=dev,
+                                     memory_format=torch.channels_last)
+                    rc = lib.mapf_conv_nhwc_pool_f16(ptr(x), ptr(h16(m.weight, "ohwi")), ptr(b), ptr(yp), B_, H_, W_,
+                                                     ci, co, ks, p, st)
+                    if rc == 0:
+                        return yp
                 if self.own_conv and (ci, co, ks) in self._OWN_CONV and x.is_contiguous(memory_format=torch.channels_last):
                     # the MFMA implicit GEMM (csrc/mapf_conv.hip); bias + ReLU in its epilogue unless pooled
                     p = m.padding[0]

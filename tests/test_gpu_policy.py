@@ -319,6 +319,36 @@ def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
     torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("ci,co,ks,H,B", [(128, 128, 3, 9, 37), (128, 128, 3, 9, 1), (128, 128, 3, 11, 5),
+                                         (256, 256, 2, 6, 1003), (256, 256, 2, 6, 7)])
+def test_conv_pool_kernel_equals_conv_then_pool(ci, co, ks, H, B):
+    """mapf_conv_nhwc_pool_f16 (whole-image tiles, pooled epilogue) == mapf_conv_nhwc_f16(relu=0) then
+    mapf_nhwc_bias_relu_pool2, bit-identical; and == torch's relu(conv + b) then MaxPool2d(2) to
+    fp16 rounding"""
+    from mapf_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(ci + co + H + B)
+    cl = torch.channels_last
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    x = torch.randn(B, ci, H, H, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    w = (torch.randn(co, ci, ks, ks, device="cuda", generator=g) / (ci * ks * ks) ** 0.5).half()
+    b = torch.randn(co, device="cuda", generator=g).half()
+    wp = w.permute(0, 2, 3, 1).contiguous()
+    Ho = H + 2 - ks + 1
+    raw = torch.empty(B, co, Ho, Ho, dtype=torch.float16, device="cuda").contiguous(memory_format=cl)
+    _lib.check(L.mapf_conv_nhwc_f16(_p(x), _p(wp), _p(b), _p(raw), B, H, H, ci, co, ks, 1, 0, st))
+    want = torch.empty(B, co, Ho // 2, Ho // 2, dtype=torch.float16, device="cuda").contiguous(memory_format=cl)
+    _lib.check(L.mapf_nhwc_bias_relu_pool2(_p(raw), _p(b), _p(want), B, Ho, Ho, co, st))
+    got = torch.full_like(want, float("nan"))
+    _lib.check(L.mapf_conv_nhwc_pool_f16(_p(x), _p(wp), _p(b), _p(got), B, H, H, ci, co, ks, 1, st))
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    ref = torch.nn.functional.max_pool2d(torch.relu(
+        (torch.nn.functional.conv2d(x.float(), w.float(), None, 1, 1).half().float() + b.float().view(1, -1, 1, 1))
+        .half().float()), 2)
+    torch.testing.assert_close(got.float(), ref, rtol=1e-2, atol=1e-2)
+
+
 def test_conv_kernel_rejects_other_shapes():
     from mapf_amd import _lib
     x = torch.zeros(1, dtype=torch.float16, device="cuda")
