@@ -508,7 +508,7 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
     if (M64 > (int64_t)0x7FFFFFFF - 1024 || nimg * H * W > (int64_t)0x7FFFFFFF / 512) return MAPF_EINVAL;
     const int M = (int)M64, epi = relu ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 4>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 128 && Cout == 256 && ks == 2) conv::launch<128, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else return MAPF_EINVAL;
