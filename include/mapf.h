@@ -262,6 +262,12 @@ int mapf_rollout_plan(const mapf_env *env, int32_t slots, char *buf, int32_t n);
  * on work recorded before its capture began). */
 int mapf_flush(mapf_env *env, void *stream);
 
+/* Return every argument slot that captured persistent launches of this handle took (16 per
+ * handle; a capture past them fails with MAPF_ESTATE and launches nothing).  Call only once every
+ * hipGraph holding such a launch of this handle has been destroyed: their replays would read
+ * slots that later captures overwrite. */
+int mapf_release_captures(mapf_env *env);
+
 /* Uniform random policy (Philox, counter = env clock): DEVICE int32 [B][N]. */
 int mapf_random_actions(mapf_env *env, int32_t *actions, void *stream);
 
@@ -326,6 +332,12 @@ int mapf_advantage_moments(const float *ret, const float *v, const float *cret, 
 int mapf_normalize_advantages_stats(const float *ret, const float *v, const float *cret, const float *cv,
                                     const double *stats, float *adv_out, float *cadv_out, int32_t M, double lagrange,
                                     int32_t mix, void *stream);
+/* mapf_normalize_advantages_stats with the multiplier in DEVICE memory, lam_dev[2] as in
+ * mapf_normalize_advantages_dlam: the distributed form of Model.train's device update (the
+ * multiplier stays where the captured single-rank form keeps it). */
+int mapf_normalize_advantages_stats_dlam(const float *ret, const float *v, const float *cret, const float *cv,
+                                         const double *stats, float *adv_out, float *cadv_out, int32_t M,
+                                         const float *lam_dev, int32_t mix, void *stream);
 
 /* OneEpPerformance.episodeReward / episodeCostReward of every env (runner.py:95-96:
  * `perf.episodeReward += np.sum(rewards)` once per step): x DEVICE float [T][B][N] (one

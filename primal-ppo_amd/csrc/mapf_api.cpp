@@ -639,10 +639,12 @@ int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_
     if (T == 0) return MAPF_OK;
     if (rollout_random_fused(e)) {
         if (int rc = flush_search(e, s)) return rc;     // the kernel searches inline from here on
-        if (!launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s) &&
-            launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s) != MAPF_OK)
+        int rc = launch_rollout_random(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s);
+        if (rc == ROLLOUT_NOT_COVERED)
+            rc = launch_rollout_wide(e->d, T, actions_out, o, obs, vec, slots ? 1 : 0, e->tune, e->args, s);
+        if (rc != MAPF_OK)
             return fail(MAPF_ESTATE, "every argument slot for captured persistent launches of this handle is taken "
-                                     "(16 per handle, ArgRing)");
+                                     "(16 per handle, ArgRing; mapf_release_captures frees them)");
         HIPCHK(hipGetLastError());
         return MAPF_OK;
     }
@@ -663,6 +665,12 @@ int mapf_rollout_random(mapf_env *e, int32_t T, int32_t slots, int32_t *actions_
                                        vec + k * BN * 4, stream))
             return rc;
     }
+    return MAPF_OK;
+}
+
+int mapf_release_captures(mapf_env *e) {
+    if (!e) return fail(MAPF_EINVAL, "null argument");
+    e->args.release_captures();
     return MAPF_OK;
 }
 
@@ -957,7 +965,19 @@ int mapf_normalize_advantages_stats(const float *ret, const float *v, const floa
     if (M < 0) return fail(MAPF_EINVAL, "M must be >= 0");
     if (M == 0) return MAPF_OK;
     launch_normalize_stats(ret, v, cret, cv, stats, adv_out, cadv_out, M, (float)lagrange, (float)(lagrange + 1.0), mix,
-                           (hipStream_t)stream);
+                           nullptr, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return MAPF_OK;
+}
+
+int mapf_normalize_advantages_stats_dlam(const float *ret, const float *v, const float *cret, const float *cv,
+                                         const double *stats, float *adv_out, float *cadv_out, int32_t M,
+                                         const float *lam_dev, int32_t mix, void *stream) {
+    if (!ret || !v || !cret || !cv || !stats || !adv_out || !cadv_out || !lam_dev)
+        return fail(MAPF_EINVAL, "null argument");
+    if (M < 0) return fail(MAPF_EINVAL, "M must be >= 0");
+    if (M == 0) return MAPF_OK;
+    launch_normalize_stats(ret, v, cret, cv, stats, adv_out, cadv_out, M, 0.f, 1.f, mix, lam_dev, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return MAPF_OK;
 }

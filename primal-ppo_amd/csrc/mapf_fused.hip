@@ -308,30 +308,25 @@ void describe_rollout_random(const DevEnv &e, int slots, const mapf_tuning &tu, 
                   p.subs > 1 ? p.slack : -1, p.remap);
 }
 
-bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
-                           int slots, const mapf_tuning &tu, ArgRing &ring, hipStream_t s) {
+int launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+                          int slots, const mapf_tuning &tu, ArgRing &ring, hipStream_t s) {
     RolloutPlan p;
-    if (!plan_rollout_random(e, slots, tu, p)) return false;
+    if (!plan_rollout_random(e, slots, tu, p)) return ROLLOUT_NOT_COVERED;
     const RolloutOut ro{actions, out, obs, vec, slots, p.remap, p.sub_lds, p.slack, p.fair};
-    auto launch = [&](auto kern) {
+    auto launch = [&](auto kern) -> int {
         const dim3 gd(p.grid), bd(256 * p.subs);
 #if MAPF_ARGS_PTR
         const RolloutArgs *args = push_args(ring, RolloutArgs{e, ro}, s);
-        if (!args) return;
+        if (!args) return MAPF_ESTATE;      // a capture found no free argument slot: nothing launched
         hipLaunchKernelGGL(kern, gd, bd, p.lds, s, args, T);
 #else
         hipLaunchKernelGGL(kern, gd, bd, p.lds, s, e, T, ro);
 #endif
+        return MAPF_OK;
     };
     (void)ring;
-    if (p.subs == 4) {
-        if (slots) launch(rollout_random_kernel<true, 4>);
-        else launch(rollout_random_kernel<false, 4>);
-    } else {
-        if (slots) launch(rollout_random_kernel<true, 1>);
-        else launch(rollout_random_kernel<false, 1>);
-    }
-    return true;
+    if (p.subs == 4) return slots ? launch(rollout_random_kernel<true, 4>) : launch(rollout_random_kernel<false, 4>);
+    return slots ? launch(rollout_random_kernel<true, 1>) : launch(rollout_random_kernel<false, 1>);
 }
 
 bool step_observe_fusable(const DevEnv &e) {

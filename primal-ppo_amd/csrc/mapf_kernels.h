@@ -83,12 +83,14 @@ void launch_bfs_fixup(const DevEnv &e, int parity, float *obs, hipStream_t s);
 bool step_observe_fusable(const DevEnv &e);
 void launch_step_observe(const DevEnv &e, int32_t *actions, const StepOut &out, uint32_t flags, int slot,
                          float *obs, float *vec, int nsearch, int sslot, hipStream_t s);
-// T committed random-policy steps + observations in one launch (mapf_fused.hip);
-// false (nothing launched) if the configuration is not covered
+// T committed random-policy steps + observations in one launch (mapf_fused.hip): MAPF_OK;
+// ROLLOUT_NOT_COVERED (nothing launched) if the configuration is not covered; MAPF_ESTATE
+// (nothing launched) if a captured launch found no free argument slot (ArgRing)
 // (the kernel's form from the handle's tuning, mapf.h: mapf_tuning); describe_* write the
 // form launch_* would take as text (mapf_rollout_plan)
+constexpr int ROLLOUT_NOT_COVERED = 1;
 bool rollout_random_fusable(const DevEnv &e);
-bool launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
+int launch_rollout_random(const DevEnv &e, int T, int32_t *actions, const StepOut &out, float *obs, float *vec,
                            int slots, const mapf_tuning &tu, struct ArgRing &ring, hipStream_t s);
 void describe_rollout_random(const DevEnv &e, int slots, const mapf_tuning &tu, char *buf, size_t n);
 // the same for up to 64 agents / per-env maps / the BFS channel: one wave per env
@@ -115,6 +117,7 @@ struct ArgRing {
     char *base = nullptr;     // (ARG_SLOTS + ARG_CAPTURE_SLOTS) * ARG_SLOT_BYTES of device memory (the handle's)
     unsigned next = 0;        // ring position
     unsigned captured = 0;    // capture slots handed out
+    void release_captures() { captured = 0; }
     template <class A>
     A *slot(bool capturing) {
         static_assert(sizeof(A) <= ARG_SLOT_BYTES, "argument block larger than a slot");
@@ -170,7 +173,8 @@ void launch_normalize(const float *ret, const float *v, const float *cret, const
 void launch_moments(const float *ret, const float *v, const float *cret, const float *cv, int M, const double *mean,
                     double *out, hipStream_t s);
 void launch_normalize_stats(const float *ret, const float *v, const float *cret, const float *cv, const double *stats,
-                            float *adv, float *cadv, int M, float lam, float lam1, int mix, hipStream_t s);
+                            float *adv, float *cadv, int M, float lam, float lam1, int mix, const float *lamd,
+                            hipStream_t s);
 void launch_episode_sum(const float *x, int T, int B, int N, float *out, hipStream_t s);
 void launch_sample(const float *ps, int stride, int32_t *a32, int64_t *a64, int M, uint64_t seed, uint32_t step,
                    hipStream_t s);

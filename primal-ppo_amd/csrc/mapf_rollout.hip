@@ -130,9 +130,10 @@ __global__ __launch_bounds__(256) void normalize_stats_kernel(const float *__res
                                                               const float *__restrict__ cv,
                                                               const double *__restrict__ stats, float *__restrict__ adv,
                                                               float *__restrict__ cadv, int M, float lam, float lam1,
-                                                              int mix) {
+                                                              int mix, const float *__restrict__ lamd) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= M) return;
+    if (lamd) { lam = lamd[0]; lam1 = lamd[1]; }     // {lam, f32(lam + 1)} in device memory
     const float mean0 = (float)stats[0], mean1 = (float)stats[1];
     const float den0 = __fadd_rn((float)sqrt(stats[2]), 1e-6f), den1 = __fadd_rn((float)sqrt(stats[3]), 1e-6f);
     float a = __fdiv_rn(__fsub_rn(__fsub_rn(ret[k], v[k]), mean0), den0);
@@ -182,9 +183,10 @@ void launch_moments(const float *ret, const float *v, const float *cret, const f
 }
 
 void launch_normalize_stats(const float *ret, const float *v, const float *cret, const float *cv, const double *stats,
-                            float *adv, float *cadv, int M, float lam, float lam1, int mix, hipStream_t s) {
+                            float *adv, float *cadv, int M, float lam, float lam1, int mix, const float *lamd,
+                            hipStream_t s) {
     hipLaunchKernelGGL(normalize_stats_kernel, dim3((M + 255) / 256), dim3(256), 0, s, ret, v, cret, cv, stats, adv,
-                       cadv, M, lam, lam1, mix);
+                       cadv, M, lam, lam1, mix, lamd);
 }
 
 void launch_episode_sum(const float *x, int T, int B, int N, float *out, hipStream_t s) {

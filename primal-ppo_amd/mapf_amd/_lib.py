@@ -75,6 +75,7 @@ SIGNATURES = {
     "mapf_set_tuning": (ctypes.c_int, [P, ctypes.POINTER(Tuning)]),
     "mapf_rollout_plan": (ctypes.c_int, [P, I32, ctypes.c_char_p, I32]),
     "mapf_flush": (ctypes.c_int, [P, P]),
+    "mapf_release_captures": (ctypes.c_int, [P]),
     "mapf_random_actions": (ctypes.c_int, [P, P, P]),
     "mapf_bfs": (ctypes.c_int, [P, P, P]),
     "mapf_render": (ctypes.c_int, [P, P, I32, I32, P, P]),
@@ -89,6 +90,7 @@ SIGNATURES = {
     "mapf_sample_actions": (ctypes.c_int, [P, I32, P, P, I32, ctypes.c_uint64, U32, P]),
     "mapf_advantage_moments": (ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     "mapf_normalize_advantages_stats": (ctypes.c_int, [P, P, P, P, P, P, P, I32, ctypes.c_double, I32, P]),
+    "mapf_normalize_advantages_stats_dlam": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I32, P]),
     "mapf_episode_sum": (ctypes.c_int, [P, I32, I32, I32, P, P]),
     # policy acting forward epilogues (csrc/mapf_policy.hip)
     "mapf_nhwc_bias_relu": (ctypes.c_int, [P, P, I64, I32, P]),

@@ -370,6 +370,11 @@ class BatchedMapfGym:
         """Run pending search work (BFS maps, next human paths) now, in its own launch."""
         _lib.check(_lib.lib().mapf_flush(self.h, _stream(self.device)))
 
+    def release_captures(self):
+        """Free the argument slots captured rollouts of this env took (mapf_release_captures):
+        only after every hipGraph holding one has been destroyed."""
+        _lib.check(_lib.lib().mapf_release_captures(self.h))
+
     def random_actions(self, out=None):
         out = self.actions if out is None else out
         _check(out, torch.int32, self.B * self.N, self.device, "actions")
@@ -492,12 +497,15 @@ def normalize_advantages_dlam(returns, values, cost_returns, cost_values, lam2, 
     return adv, cadv
 
 
-def normalize_advantages_distributed(returns, values, cost_returns, cost_values, lagrange=0.0, mix=False, group=None):
+def normalize_advantages_distributed(returns, values, cost_returns, cost_values, lagrange=0.0, mix=False, group=None,
+                                     lam2=None):
     """normalize_advantages over a minibatch split across the ranks of torch.distributed: this
     rank's rows in, this rank's rows out, normalised with the GLOBAL mean and unbiased std
     (model.py:106-113 on the whole minibatch).  Two-pass fp64 moments on the device
     (mapf_advantage_moments), each pass all-reduced (2 small all-reduces), then
-    mapf_normalize_advantages_stats."""
+    mapf_normalize_advantages_stats.  lam2: the multiplier in device memory instead of
+    `lagrange` (float32 [2] = {f32(lagrange), f32(lagrange + 1)}, as normalize_advantages_dlam;
+    mapf_normalize_advantages_stats_dlam) -- Model.train's distributed device update."""
     import torch.distributed as dist
     dev, M = returns.device, returns.numel()
     if dev.type != "cuda":
@@ -505,6 +513,8 @@ def normalize_advantages_distributed(returns, values, cost_returns, cost_values,
     for name, t in (("returns", returns), ("values", values), ("cost_returns", cost_returns),
                     ("cost_values", cost_values)):
         _check(t, torch.float32, M, dev, name)
+    if lam2 is not None:
+        _check(lam2, torch.float32, 2, dev, "lam2")
     st, L = _stream(dev), _lib.lib()
     ptrs = [_ptr(t) for t in (returns, values, cost_returns, cost_values)]
     buf = torch.zeros(3, dtype=torch.float64, device=dev)          # sum x, sum c, rows
@@ -518,8 +528,12 @@ def normalize_advantages_distributed(returns, values, cost_returns, cost_values,
     stats = torch.cat([mean, q / (buf[2] - 1).clamp_min(1)]).contiguous()
     adv = torch.empty_like(returns)
     cadv = torch.empty_like(returns)
-    _lib.check(L.mapf_normalize_advantages_stats(*ptrs, _ptr(stats), _ptr(adv), _ptr(cadv), M, float(lagrange),
-                                                 int(mix), st))
+    if lam2 is None:
+        _lib.check(L.mapf_normalize_advantages_stats(*ptrs, _ptr(stats), _ptr(adv), _ptr(cadv), M, float(lagrange),
+                                                     int(mix), st))
+    else:
+        _lib.check(L.mapf_normalize_advantages_stats_dlam(*ptrs, _ptr(stats), _ptr(adv), _ptr(cadv), M, _ptr(lam2),
+                                                          int(mix), st))
     return adv, cadv
 
 

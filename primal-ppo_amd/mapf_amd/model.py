@@ -4,12 +4,14 @@ Mirrors the reference's Model (model.py:13-231) and Lagrangian multipliers
 (lagrange.py:26-88), with the device-resident pieces of the hot path:
   * step(): the policy forward + on-device categorical sampling (mapf_sample_actions
     in place of np.random.choice, model.py:38-40);
-  * train(): advantage normalisation by the HIP kernels (mapf_normalize_advantages,
+  * train(): advantage normalisation by the HIP kernels (mapf_normalize_advantages_dlam,
     model.py:106-113) -- statistics over the GLOBAL minibatch when distributed (two-pass
-    fp64 moments all-reduced, mapf_normalize_advantages_stats) --
+    fp64 moments all-reduced, mapf_normalize_advantages_stats_dlam; _DeviceUpdate.body) --
     then the reference's loss (:115-170), AMP GradScaler, and between backward and
     unscale the RCCL all-reduce of the flattened gradient bucket (SURVEY.md §3.4:
-    the only exchange step of the path).
+    the only exchange step of the path).  Every rank then holds the same gradient, so
+    found-inf, clipping, Adam and the loss scale agree across ranks; the returned stats are
+    averaged over the ranks (the global minibatch's means when the shards are equal).
 """
 import ctypes
 
@@ -274,17 +276,26 @@ class Model:
         One rank: after two eager updates of a minibatch shape the same body is captured into a
         hipGraph and every later update of that shape is one replay (the host launched ~1,500
         small ops per update).  Distributed: eager (the all-reduce sits between backward and
-        unscale, model.py:177-185)."""
-        key = (tuple(observation.shape), tuple(vector.shape), tuple(old_ps.shape), tuple(train_valid.shape),
-               input_state is None)
+        unscale, model.py:177-185), the advantages normalised with the global minibatch's
+        statistics.  input_state is ignored, as the network ignores it (net.py:102-155 never
+        reads it): driver.py passes the rollout's zero hiddenState rows, never None.
+        The loss scale and its growth tracker are net_scaler's own tensors (one AMP state per
+        model, as the reference's one GradScaler, shared by every minibatch shape and by the
+        eager path)."""
+        key = (tuple(observation.shape), tuple(vector.shape), tuple(old_ps.shape), tuple(train_valid.shape))
+        sc = self.net_scaler
+        if sc._scale is None:
+            sc._lazy_init_scale_growth_tracker(self.device)
         upd = self._updates.get(key)
+        if upd is not None and not upd.uses(sc):
+            upd = None                        # net_scaler replaced or reconfigured: re-capture
         if upd is None:
             upd = self._updates[key] = _DeviceUpdate(self, observation, vector, returns, old_ps, train_valid, action)
         T = TrainingParameters
         upd.load(observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, train_valid,
                  coef=(T.CLIP_RANGE, T.ENTROPY_COEF, T.VALUE_COEF, T.VALID_COEF, T.COST_VALUE_COEF, T.COST_COEF * lam),
                  lam=lam)
-        upd.run(graph=self.graph_update and not distributed and input_state is None, allreduce=distributed)
+        upd.run(graph=self.graph_update and not distributed, allreduce=distributed)
         # the Lagrangian step (host, model.py:180) depends only on the episode cost
         if distributed:   # every rank must update the multiplier with the same episode cost
             c = torch.tensor([float(episode_cost)], dtype=torch.float64, device=self.device)
@@ -330,14 +341,23 @@ class _DeviceUpdate:
         self.action = e(action, torch.int64)
         self.old_ps, self.tv = e(old_ps), e(train_valid)
         self.dyn = torch.zeros(8, dtype=torch.float32, device=dev)     # coef[6], lam, f32(lam + 1)
-        sc = model.net_scaler                  # its settings (torch.amp.GradScaler: 2^16, x2 / 2000, x0.5)
-        self.scale = torch.full((), float(sc._init_scale), dtype=torch.float32, device=dev)   # 0-dim, as GradScaler's
-        self.growth = torch.zeros((), dtype=torch.int32, device=dev)
-        self.amp = (float(sc._growth_factor), float(sc._backoff_factor), int(sc._growth_interval))
+        sc = model.net_scaler                  # its live state and settings (GradScaler: 2^16, x2 / 2000, x0.5)
+        self.scaler = sc
+        self.scale, self.growth = sc._scale, sc._growth_tracker        # 0-dim device tensors, updated in place
+        self.amp = self._amp_settings(sc)
         self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
         self.stats = torch.zeros(11, dtype=torch.float32, device=dev)
         self.graph = None
         self.eager_runs = 0
+
+    @staticmethod
+    def _amp_settings(sc):
+        return float(sc._growth_factor), float(sc._backoff_factor), int(sc._growth_interval)
+
+    def uses(self, sc):
+        """True while this update's captured AMP state is `sc`'s (same tensors, same settings)."""
+        return (self.scaler is sc and self.scale is sc._scale and self.growth is sc._growth_tracker
+                and self.amp == self._amp_settings(sc))
 
     def load(self, observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, train_valid, coef, lam):
         for dst, src in ((self.obs, observation), (self.vec, vector), (self.ret, returns), (self.cret, cost_returns),
@@ -352,9 +372,12 @@ class _DeviceUpdate:
         m, net, opt = self.model, self.model.network, self.model.net_optimizer
         T = TrainingParameters
         opt.zero_grad(set_to_none=True)
-        from .env import normalize_advantages_dlam
-        adv, cadv = normalize_advantages_dlam(self.ret.reshape(-1), self.v.reshape(-1), self.cret.reshape(-1),
-                                              self.cv.reshape(-1), self.dyn[6:8], T.MINUS_ADV_WITH_CADV)
+        from .env import normalize_advantages_distributed, normalize_advantages_dlam
+        ins = (self.ret.reshape(-1), self.v.reshape(-1), self.cret.reshape(-1), self.cv.reshape(-1))
+        if allreduce:    # model.py:106-113 over the GLOBAL minibatch: moments all-reduced
+            adv, cadv = normalize_advantages_distributed(*ins, mix=T.MINUS_ADV_WITH_CADV, lam2=self.dyn[6:8])
+        else:
+            adv, cadv = normalize_advantages_dlam(*ins, self.dyn[6:8], T.MINUS_ADV_WITH_CADV)
         adv, cadv = adv.view(self.ret.shape), cadv.view(self.ret.shape)
         with torch.autocast(device_type="cuda", cache_enabled=False):
             new_ps, new_v, block, policy_sig, _, _, new_cv = net(self.obs, self.vec, None)
@@ -375,6 +398,9 @@ class _DeviceUpdate:
         self.stats.copy_(torch.stack([t.detach().float().reshape(()) for t in (
             all_loss, terms[0], terms[1], terms[2], terms[3], terms[4], terms[5], terms[6], grad_norm,
             torch.mean(adv), torch.mean(cadv))]))
+        if allreduce:    # the loss terms' and advantages' means over the global minibatch (equal shards)
+            dist.all_reduce(self.stats)
+            self.stats.div_(dist.get_world_size())
 
     def run(self, graph=True, allreduce=False):
         if not graph or self.eager_runs < self.WARMUP:

@@ -64,3 +64,39 @@ def test_threaded_batches_match_single_thread():
     for i, b in enumerate(batches):
         assert got[i] == want[0]
         assert (b.obs == want[1]).all() and (b.vec == want[2]).all()
+
+
+def test_all_cores_figure_is_labelled():
+    """`value` is this GPU's CPU share, labelled as such; the all-host-cores
+    figure is reported beside it (per-thread rate x nproc, named an extrapolation)."""
+    import bench
+    from mapf_amd.maps import generate_warehouse
+    line = bench.cpu_baseline(generate_warehouse(10, 10), 10, 10, 4, 11, 6, 0.5)
+    assert line["value_label"].startswith(f"{line['cores']} of {line['host_cores']} host cores")
+    assert abs(line["all_host_cores_value"] - line["per_core_value"] * line["host_cores"]) <= 1.0 + 1e-6 * line["value"]
+    assert "extrapolated" in line["all_host_cores_basis"]
+
+
+def test_gpus_flag_launches_that_many_ranks(monkeypatch):
+    """`bench.py --gpus N` with no launcher around it starts N ranks of the same
+    command under torch.distributed.run (a child process; 127.0.0.1 rendezvous) and exits with its
+    code -- before anything touches the GPU."""
+    import subprocess
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    try:
+        bench.main()
+        raise AssertionError("main() returned")
+    except SystemExit as e:
+        assert e.code == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")

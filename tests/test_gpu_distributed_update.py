@@ -1,0 +1,149 @@
+"""Model.train's DEFAULT GPU update (fused loss, _DeviceUpdate) on two ranks vs one process --
+SURVEY.md §8(e): the minibatch split over the ranks, the advantages normalised with the GLOBAL
+minibatch's statistics (two all-reduced moment passes, model.py:106-113), the gradient bucket
+all-reduced between backward and unscale (model.py:177-185).
+
+Two gloo ranks share this GPU (RCCL refuses two ranks on one device; the update's collectives are
+the same calls either way).  Each rank trains on its half of the same minibatches (the reference's
+g5 minibatch, then two seeded ones) with MIOpen's deterministic algorithms and dropout off.
+Checked per update: every rank's advantages equal the one-process advantages' rows (1e-5); both
+ranks hold bit-identical weights; the two-rank weights equal the one-process weights within the
+spread of the update itself under a change of summation order (the same one-process update on a
+row-permuted minibatch)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import load
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ["observation", "vector", "returns", "cost_returns", "old_v", "old_cv", "action", "old_ps", "train_valid"]
+
+
+def _batches():
+    z = load("g5_net")
+    out = [{k: z["train_" + k] for k in FIELDS}]
+    g = np.random.default_rng(7)
+    R, N = z["train_returns"].shape
+    for _ in range(2):
+        ps = g.random((R, N, 5)).astype(np.float32) + 0.05
+        out.append({"observation": (g.random((R, N, 6, 9, 9)) < 0.3).astype(np.float32),
+                    "vector": g.normal(size=(R, N, 4)).astype(np.float32),
+                    "returns": g.normal(size=(R, N)).astype(np.float32),
+                    "cost_returns": g.normal(size=(R, N)).astype(np.float32) * 0.3,
+                    "old_v": g.normal(size=(R, N)).astype(np.float32),
+                    "old_cv": g.normal(size=(R, N)).astype(np.float32) * 0.3,
+                    "action": g.integers(0, 5, (R, N)).astype(np.int64),
+                    "old_ps": (ps / ps.sum(-1, keepdims=True)).astype(np.float32),
+                    "train_valid": (g.random((R, N, 5)) < 0.7).astype(np.float32)})
+    return out
+
+
+def _train(batches, world=1, rank=0, perm=None):
+    """Model.train (default device path) over `batches`, this rank's rows; returns the weights
+    after each update and the advantages the normalisation produced."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd"), os.path.join(ROOT, "tests")]
+    from mapf_amd import env as E
+    from mapf_amd.config import EnvParameters
+    flags, n_agents = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark), EnvParameters.N_AGENTS
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    EnvParameters.N_AGENTS = 2
+    seen, saved = [], {}
+    for name in ("normalize_advantages_dlam", "normalize_advantages_distributed"):
+        fn = saved[name] = getattr(E, name)
+        setattr(E, name, lambda *a, _fn=fn, **k: seen.append(_fn(*a, **k)) or seen[-1])
+    try:
+        return _train_recorded(batches, world, rank, perm, seen)
+    finally:
+        for name, fn in saved.items():
+            setattr(E, name, fn)
+        (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark), EnvParameters.N_AGENTS = flags, n_agents
+
+
+def _train_recorded(batches, world, rank, perm, seen):
+    from mapf_amd.model import Model
+    from test_net import det_weights
+    m = Model(0, "cuda", global_model=True, numChannel=6, num_agents=2, fov=9)
+    m.network.load_state_dict(det_weights(m.network.state_dict()))
+    m.network.eval()
+    m.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    assert m.fused_loss
+    flat = lambda: torch.cat([p.detach().flatten() for p in m.network.parameters()]).cpu().numpy()  # noqa: E731
+    weights, advs, stats = [flat()], [], []
+    for b in batches:
+        rows = np.arange(len(b["returns"]))
+        if perm is not None:
+            rows = perm(rows)
+        sl = rows[rank * len(rows) // world:(rank + 1) * len(rows) // world]
+        g = lambda k: b[k][sl]  # noqa: E731
+        s = m.train(g("observation"), g("vector"), g("returns"), g("cost_returns"), g("old_v"), g("old_cv"),
+                    g("action"), g("old_ps"), np.zeros((len(sl), 2, 2, 512), np.float32), g("train_valid"), 3.0)
+        stats.append(np.array([float(np.asarray(x)) for x in s]))
+        weights.append(flat())
+        adv, cadv = seen[-1]
+        advs.append((adv.detach().cpu().numpy().reshape(len(sl), -1), cadv.detach().cpu().numpy().reshape(len(sl), -1),
+                     sl))
+    return weights, advs, stats
+
+
+def _worker(rank, world, port, batches, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        w, a, s = _train(batches, world, rank)
+        q.put((rank, w, [(x, y) for x, y, _ in a], s))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_model_train_two_ranks_equals_one_process():
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    batches = _batches()
+    w1, a1, s1 = _train(batches)
+    # the update's own spread under a change of summation order: the same rows, permuted
+    wp, _, _ = _train(batches, perm=lambda r: r[::-1].copy())
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, batches, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, w_r0, a_r0, s_r0), (_, w_r1, a_r1, s_r1) = res
+    for k in range(len(batches)):
+        R = len(batches[k]["returns"])
+        adv1, cadv1, _ = a1[k]
+        # every rank's rows: the one-process normalisation of the whole minibatch (global statistics)
+        for r, (adv, cadv) in enumerate((a_r0[k], a_r1[k])):
+            rows = slice(r * R // 2, (r + 1) * R // 2)
+            np.testing.assert_allclose(adv, adv1[rows], rtol=1e-5, atol=1e-5, err_msg=f"update {k} rank {r} adv")
+            np.testing.assert_allclose(cadv, cadv1[rows], rtol=1e-5, atol=1e-5, err_msg=f"update {k} rank {r} cadv")
+        # both ranks hold the same weights (the all-reduced gradient, the same Adam step)
+        np.testing.assert_array_equal(w_r0[k + 1], w_r1[k + 1], err_msg=f"update {k}")
+        # the averaged stats agree across ranks and with one process (global means)
+        np.testing.assert_array_equal(s_r0[k], s_r1[k])
+        np.testing.assert_allclose(s_r0[k][[9, 10]], s1[k][[9, 10]], atol=1e-5)
+        # the weights' total change: two ranks vs one process, within the update's own spread
+        moved = np.linalg.norm(w1[k + 1] - w1[0])
+        assert moved > 0
+        r_dist = np.linalg.norm(w_r0[k + 1] - w1[k + 1]) / moved
+        r_perm = np.linalg.norm(wp[k + 1] - w1[k + 1]) / moved
+        print(f"update {k}: two ranks vs one process {r_dist:.3e}, permuted rows vs one process {r_perm:.3e}")
+        assert r_dist <= max(3 * r_perm, 1e-3), (k, r_dist, r_perm)

@@ -100,3 +100,46 @@ def test_capture_after_deferred_search_needs_flush():
     assert torch.equal(env.obs, twin.obs) and torch.equal(env.vec, twin.vec)
     assert torch.equal(env.actions, twin.actions)
     assert_same_env(env, twin, "after the replays")
+
+
+def test_capture_slots_run_out_loudly_and_can_be_released():
+    """16 captured persistent launches per handle (ArgRing): the 17th capture fails with
+    MAPF_ESTATE and records nothing (the env is unchanged, no other kernel form is launched in
+    its place); after the graphs are destroyed, mapf_release_captures hands the slots back."""
+    import gc
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    env, twin = c4_env(), c4_env()
+    env.rollout_random(2)
+    twin.rollout_random(2)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+
+    def capture():
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                env.rollout_random(1)
+        torch.cuda.synchronize()
+        return g
+
+    graphs = [capture() for _ in range(16)]
+    with pytest.raises(RuntimeError, match="argument slot"):
+        capture()
+    torch.cuda.synchronize()
+    assert_same_env(env, twin, "after the refused capture")     # nothing ran
+    graphs[3].replay()                                          # a held slot still replays
+    twin.rollout_random(1)
+    torch.cuda.synchronize()
+    assert_same_env(env, twin, "after a replay")
+    del graphs
+    gc.collect()
+    env.release_captures()
+    g = capture()
+    for _ in range(2):
+        g.replay()
+        twin.rollout_random(1)
+    torch.cuda.synchronize()
+    assert torch.equal(env.obs, twin.obs)
+    assert_same_env(env, twin, "after the released slots were captured again")
