@@ -380,6 +380,12 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
 int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
                           int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
                           float eps, uint16_t *z, void *stream);
+/* Row tiles per workgroup of the mapf_linear512_* kernels (process-wide; bit-identical results
+ * either way, for A/B timing): 2 (128 rows share each staged 512 x 32 weight chunk), 1 (64 rows),
+ * or 0 (default) the faster as measured per kernel: 2 for the residual + LayerNorm forms, 1 for
+ * GELU.  MAPF_EINVAL on another value. */
+int mapf_linear512_select(int32_t row_tiles);
+
 /* 512 x 512 Linear (w: fp16 [512 out][512 in], torch's layout; bias fp16 [512]) on `rows` contiguous fp16
  * rows a[rows][512] with its epilogue, one launch (MFMA GEMM; the linear's fp16 output stays on chip):
  *   mapf_linear512_gelu_dropout        out = dropout(gelu(a w^T + b)) fp16    = lin + mapf_gelu_dropout_f16
@@ -460,6 +466,14 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
  * Same values as mapf_conv_nhwc_f16(relu = 0) then mapf_nhwc_bias_relu_pool2. */
 int mapf_conv_nhwc_pool_f16(const uint16_t *x, const uint16_t *w_packed, const uint16_t *bias, uint16_t *y, int64_t nimg,
                             int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks, int32_t pad, void *stream);
+
+/* Which implicit-GEMM form mapf_conv_nhwc_f16 / mapf_conv_nhwc_pool_f16 launch (process-wide; values
+ * to fp16 rounding of a different summation order, for A/B timing): 2 the image-resident form
+ * wherever its geometry applies (whole images per workgroup, each input channel slice DMA'd into
+ * LDS once and read by every tap), 0 the per-tap staged form, 1 (default) the faster of the two
+ * as measured per layer (image-resident for the 3x3 and the pooled layers).  MAPF_EINVAL on
+ * another value. */
+int mapf_conv_select(int32_t impl);
 
 /* conv1 (net.py:104, 3x3, padding 1, Cin = num_channel <= 7, Cout = 128) from the fp32 NCHW observation
  * x_nchw [nimg][Cin][H][W] (cast to fp16 as autocast does); w fp16 [Cout][64]: torch's [Cout][Cin][3][3]

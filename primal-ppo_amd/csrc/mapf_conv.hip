@@ -349,6 +349,244 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
     }
 }
 
+// ---- Image-resident implicit GEMM (round 5) ---------------------------------------------
+// conv_igemm32 stages one A row per (output pixel, tap): every input pixel crosses L2 -> LDS KS^2
+// times (9x for the 3x3 layers), 24 KiB of DMA per 32-deep K-chunk at 128 channels -- the kernel
+// ran at ~37 GB/s per CU of LDS-DMA, about half what the CU can take in from L2, latency-bound on
+// those copies.  Here a workgroup owns `ipt` WHOLE images (ipt * Ho * Wo <= 32 * WAVES rows) and
+// each 32-channel slice of their input pixels is DMA'd into LDS once; every tap's A fragment is
+// read from that image at a shifted pixel index.  K order (channel chunk cc, tap, 32 channels):
+// per chunk only the weight slice (COUT x 32) streams, through a ring of S buffers; the next image
+// chunk is DMA'd into the other image buffer while the current one is in use (issued at the
+// current chunk's first tap, waited for T taps later).  For the 3x3 / 128-channel layers the
+// L2 -> LDS bytes per tile fall from 864 to ~390 KiB.
+//
+// LDS image of one channel chunk: slot s (64 B = 32 fp16 channels of one pixel) at s * 64, the 16-B
+// pieces XOR-swizzled by (s >> 2) & 3.  Input pixel (img, iy, ix) sits at slot
+//     MARGIN + img * IS + (iy + pad) * Wo + ix          (rows of Wo slots, ix < W <= Wo)
+// with zero slots for the pad rows; columns past W and the horizontal padding are never stored --
+// the A fragment of a tap whose ix = ox + kx - pad falls outside [0, W) is zeroed in registers.
+// The output row r = img * Ho * Wo + oy * Wo + ox of tap (ky, kx) reads slot
+//     MARGIN + r + img * (IS - Ho * Wo) + ky * Wo + kx - pad,
+// and IS = Ho * Wo + 16 k makes that r + const mod 16: the 16 rows a ds_read_b128 lane group
+// reads ({0-3,12-15,20-27} / {4-11,16-19,28-31} of a wave's 32) are 16 distinct residues, i.e. 16
+// distinct (s & 3, piece) bank slots -- conflict-free for every tap.  A DMA instruction fills 16
+// consecutive slots lane-linearly (lane l: slot 16 g + (l >> 2), physical piece l & 3), the source
+// pre-swizzled; slots that hold no input pixel (pad rows, gaps, the margin) fetch zeros.
+constexpr int IMG_MARGIN = 16;
+
+template <int CIN, int COUT, int KS, int WAVES, int S, int JI>
+struct CfgImg {
+    static constexpr int THREADS = 64 * WAVES, NT = COUT / 32, BM = 32 * WAVES, T = KS * KS, K = T * CIN;
+    static constexpr int NCC = CIN / 32, NCH = NCC * T;
+    static constexpr int IMG_SLOTS = 16 * JI * WAVES, IMG_BYTES = IMG_SLOTS * 64;
+    static constexpr int B_BYTES = COUT * 64, JB = COUT / 16 / WAVES;
+    static constexpr int RING = 2 * IMG_BYTES + S * B_BYTES;
+    static constexpr int LDS = RING > BM * COUT * 2 ? RING : BM * COUT * 2;
+    static_assert(CIN % 32 == 0 && COUT % 32 == 0 && COUT % (16 * WAVES) == 0, "shape");
+    static_assert(S == 3 && T >= S && JB + JI <= 15, "ring / vmcnt");
+};
+
+__device__ inline int img_slot(int s, int q) { return s * 64 + ((q ^ ((s >> 2) & 3)) << 4); }
+
+template <int CIN, int COUT, int KS, int WAVES, int S, int JI>
+__global__ __launch_bounds__(64 * WAVES) void conv_img_kernel(const uint16_t *__restrict__ in,
+                                                              const uint16_t *__restrict__ w,
+                                                              const uint16_t *__restrict__ bias,
+                                                              uint16_t *__restrict__ out, int nimg, int H, int W,
+                                                              int pad, int ipt, int IS, int epi, int pool) {
+    using C = CfgImg<CIN, COUT, KS, WAVES, S, JI>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int Ho = H + 2 * pad - KS + 1, Wo = W + 2 * pad - KS + 1, HWo = Ho * Wo;
+    const int img0 = (int)blockIdx.x * ipt;
+    const int nimg_here = min(ipt, nimg - img0);
+    const int rows_here = nimg_here * HWo;
+    char *IMG = smem;                                         // two image-chunk buffers
+    char *BR = smem + 2 * C::IMG_BYTES;                       // the weight ring
+    // image-chunk DMA: this lane's source (element offset of channel 0 of its pixel, or -1: zeros)
+    // and logical piece, per instruction j (the same for every channel chunk)
+    int isrc[JI];
+#pragma unroll
+    for (int j = 0; j < JI; ++j) {
+        const int slot = 16 * (wave * JI + j) + (lane >> 2);
+        const int u = slot - IMG_MARGIN;
+        int src = -1;
+        if (u >= 0 && u < nimg_here * IS) {
+            const int il = u / IS, rem = u - il * IS, rr = rem / Wo, ix = rem - rr * Wo, iy = rr - pad;
+            if ((unsigned)iy < (unsigned)H && ix < W) src = (((img0 + il) * H + iy) * W + ix) * CIN;
+        }
+        const int q = (lane & 3) ^ ((slot >> 2) & 3);
+        isrc[j] = src < 0 ? -1 : src + q * 8;
+    }
+    auto issue_img = [&](int cc, int buf) {
+        char *D = IMG + buf * C::IMG_BYTES;
+#pragma unroll
+        for (int j = 0; j < JI; ++j)
+            dma16(isrc[j] >= 0 ? (const void *)(in + isrc[j] + cc * 32) : (const void *)g_zero16,
+                  D + 16 * (wave * JI + j) * 64);
+    };
+    const int qw = (lane & 3) ^ ((lane >> 4) & 3);            // weight rows: key (n >> 2) & 3, n = 16 g + (l >> 2)
+    auto issue_b = [&](int c, int slot) {
+        const int cc = c / C::T, tap = c - cc * C::T;
+        char *D = BR + slot * C::B_BYTES;
+#pragma unroll
+        for (int j = 0; j < C::JB; ++j) {
+            const int n = 16 * (wave * C::JB + j) + (lane >> 2);
+            dma16(w + (size_t)n * C::K + tap * CIN + cc * 32 + qw * 8, D + 16 * (wave * C::JB + j) * 64);
+        }
+    };
+    // this lane's A row: slot of tap (0, 0) and its output column (for the horizontal padding mask)
+    const int fr = lane & 31, fh = lane >> 5;
+    const int r = wave * 32 + fr;
+    int sbase, ox;
+    if (r < rows_here) {
+        const int il = r / HWo, p = r - il * HWo, oy = p / Wo;
+        ox = p - oy * Wo;
+        sbase = IMG_MARGIN + il * IS + oy * Wo + ox - pad;
+    } else {                                                  // padding row: any slot of the same residue
+        ox = 0x4000;                                          // every tap masked
+        sbase = IMG_MARGIN + (r & 15);
+    }
+    f16_t acc[C::NT];
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b)
+        for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+    issue_img(0, 0);
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c) issue_b(c, c);
+    for (int c = 0; c < C::NCH; ++c) {
+        const int cc = c / C::T, tap = c - cc * C::T;
+        // weights of chunk c (and image chunk cc, DMA'd >= T >= S chunks earlier) have landed;
+        // younger copies may stay in flight: the next weight slice, and the next image chunk if one
+        // was issued in the last S - 1 chunks (at a chunk's tap 0)
+        if (c + S - 2 >= C::NCH) wait_vm<0>();
+        else if ((tap >= 1 && tap <= S - 1) && cc + 1 < C::NCC) wait_vm<(S - 2) * C::JB + JI>();
+        else wait_vm<(S - 2) * C::JB>();
+        __builtin_amdgcn_s_barrier();
+        if (c + S - 1 < C::NCH) issue_b(c + S - 1, (c + S - 1) % S);
+        if (tap == 0 && cc + 1 < C::NCC) issue_img(cc + 1, (cc + 1) & 1);   // its buffer was read in cc - 1
+        const char *A = IMG + (cc & 1) * C::IMG_BYTES;
+        const char *B = BR + (c % S) * C::B_BYTES;
+        const int ky = tap / KS, kx = tap - ky * KS;
+        const int sl = sbase + ky * Wo + kx;
+        const bool ok = (unsigned)(ox + kx - pad) < (unsigned)W;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int qq = 2 * s2 + fh;
+            h8_t af = *reinterpret_cast<const h8_t *>(A + img_slot(sl, qq));
+            if (!ok) af = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < C::NT; ++b) {
+                const h8_t bf = *reinterpret_cast<const h8_t *>(B + swz64(b * 32 + fr, qq));
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    __syncthreads();                                  // every wave done with the images and the ring
+    char *Tt = smem;
+    constexpr int RB = COUT * 2;
+#pragma unroll
+    for (int b = 0; b < C::NT; ++b) {
+        const int n = b * 32 + fr;
+        const float bv = epi ? h2f(bias[n]) : 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+            float v = h2f(f2h(acc[b][e]));
+            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);
+            const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
+            *reinterpret_cast<uint16_t *>(Tt + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
+                (uint16_t)f2h(v);
+        }
+    }
+    __syncthreads();
+    constexpr int PIECES_ROW = RB / 16;
+    auto piece = [&](int row, int pc) {
+        return *reinterpret_cast<const uint4 *>(Tt + row * RB + (pc >> 3) * 128 + (((pc & 7) ^ (row & 7)) << 4));
+    };
+    if (pool) {                                       // 2x2 max-pool + bias + ReLU of whole images
+        const int Hp = Ho >> 1, Wp = Wo >> 1;
+        const int items = nimg_here * Hp * Wp * PIECES_ROW;
+        for (int p = t; p < items; p += C::THREADS) {
+            const int pc = p % PIECES_ROW, cell = p / PIECES_ROW;
+            const int il = cell / (Hp * Wp), rem = cell - il * (Hp * Wp), pi = rem / Wp, pj = rem - pi * Wp;
+            const int r00 = il * HWo + 2 * pi * Wo + 2 * pj;
+            const uint4 v[4] = {piece(r00, pc), piece(r00 + 1, pc), piece(r00 + Wo, pc), piece(r00 + Wo + 1, pc)};
+            const uint4 bb = *reinterpret_cast<const uint4 *>(bias + pc * 8);
+            const uint32_t bw[4] = {bb.x, bb.y, bb.z, bb.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t w0 = (&v[0].x)[e], w1 = (&v[1].x)[e], w2 = (&v[2].x)[e], w3 = (&v[3].x)[e];
+                uint32_t h2[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int sh = 16 * hh;
+                    const float m = fmaxf(fmaxf(h2f(w0 >> sh), h2f(w1 >> sh)), fmaxf(h2f(w2 >> sh), h2f(w3 >> sh)));
+                    h2[hh] = f2h(fmaxf(h2f(f2h(m + h2f(bw[e] >> sh))), 0.f));
+                }
+                o[e] = h2[0] | (h2[1] << 16);
+            }
+            *reinterpret_cast<uint4 *>(out + ((size_t)(img0 + il) * Hp * Wp + pi * Wp + pj) * COUT + pc * 8) =
+                make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        return;
+    }
+    const size_t m0 = (size_t)img0 * HWo;
+    for (int p = t; p < rows_here * PIECES_ROW; p += C::THREADS) {
+        const int row = p / PIECES_ROW, pc = p - row * PIECES_ROW;
+        *reinterpret_cast<uint4 *>(out + (m0 + row) * COUT + pc * 8) = piece(row, pc);
+    }
+}
+
+// the image-resident form's geometry for one layer, or false when it does not apply
+struct ImgPlan {
+    int ipt, IS, ji;
+};
+template <int WAVES>
+static bool plan_img(int H, int W, int pad, int KS, ImgPlan &p) {
+    const int Ho = H + 2 * pad - KS + 1, Wo = W + 2 * pad - KS + 1, HWo = Ho * Wo;
+    if (Ho < 1 || Wo < W || HWo > 32 * WAVES || pad > 15) return false;
+    const int need = (Ho + KS - 1) * Wo + KS;        // slots an image's taps can reach (+ slack)
+    int IS = HWo;
+    while (IS < need) IS += 16;
+    p.ipt = (32 * WAVES) / HWo;
+    const int slots = IMG_MARGIN + p.ipt * IS;
+    // padding rows read slot MARGIN + (r & 15) + tap offset: keep every read inside the buffer
+    const int reach = IMG_MARGIN + 32 * WAVES + (KS - 1) * Wo + KS;
+    const int need_slots = slots > reach ? slots : reach;
+    p.ji = (need_slots + 16 * WAVES - 1) / (16 * WAVES);
+    p.IS = IS;
+    return p.ji <= 4;
+}
+
+// 1 (default): the form measured faster per layer (tools/bench_conv_impl.py, profiles/r05_conv_ab.jsonl):
+//   image-resident for the 3x3 layers and the pooled 2x2 layer, per-tap staged for the plain 2x2 layers;
+// 2: image-resident wherever its geometry applies; 0: per-tap staged everywhere
+static int g_conv_impl = 1;
+
+template <int CIN, int COUT, int KS, int WAVES, int JI>
+static void launch_img_ji(const uint16_t *in, const uint16_t *w, const uint16_t *bias, uint16_t *out, int nimg, int H,
+                          int W, int pad, const ImgPlan &p, int epi, int pool, hipStream_t s) {
+    using C = CfgImg<CIN, COUT, KS, WAVES, 3, JI>;
+    hipLaunchKernelGGL((conv_img_kernel<CIN, COUT, KS, WAVES, 3, JI>), dim3((nimg + p.ipt - 1) / p.ipt), dim3(C::THREADS),
+                       C::LDS, s, in, w, bias, out, nimg, H, W, pad, p.ipt, p.IS, epi, pool);
+}
+template <int CIN, int COUT, int KS, int WAVES>
+static bool launch_img(const uint16_t *in, const uint16_t *w, const uint16_t *bias, uint16_t *out, int nimg, int H,
+                       int W, int pad, int epi, int pool, hipStream_t s) {
+    ImgPlan p;
+    if (g_conv_impl == 0 || (g_conv_impl == 1 && KS == 2 && !pool) || !plan_img<WAVES>(H, W, pad, KS, p))
+        return false;
+    if (pool && ((H + 2 * pad - KS + 1) < 2 || (W + 2 * pad - KS + 1) < 2)) return false;
+    if (p.ji <= 3) launch_img_ji<CIN, COUT, KS, WAVES, 3>(in, w, bias, out, nimg, H, W, pad, p, epi, pool, s);
+    else launch_img_ji<CIN, COUT, KS, WAVES, 4>(in, w, bias, out, nimg, H, W, pad, p, epi, pool, s);
+    return true;
+}
+
 #ifndef MAPF_CONV_STAGES
 #define MAPF_CONV_STAGES 3                            // 0: the 64-deep double buffer (conv_igemm_kernel)
 #endif
@@ -508,7 +746,10 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
     if (M64 > (int64_t)0x7FFFFFFF - 1024 || nimg * H * W > (int64_t)0x7FFFFFFF / 512) return MAPF_EINVAL;
     const int M = (int)M64, epi = relu ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    if (Cin == 128 && Cout == 128 && ks == 3 && conv::launch_img<128, 128, 3, 8>(x, w_packed, bias, y, (int)nimg, H, W, pad, epi, 0, s));
+    else if (Cin == 128 && Cout == 256 && ks == 2 && conv::launch_img<128, 256, 2, 8>(x, w_packed, bias, y, (int)nimg, H, W, pad, epi, 0, s));
+    else if (Cin == 256 && Cout == 256 && ks == 2 && conv::launch_img<256, 256, 2, 8>(x, w_packed, bias, y, (int)nimg, H, W, pad, epi, 0, s));
+    else if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 128 && Cout == 256 && ks == 2) conv::launch<128, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else return MAPF_EINVAL;
@@ -527,7 +768,9 @@ int mapf_conv_nhwc_pool_f16(const uint16_t *x, const uint16_t *w_packed, const u
     const int M = (int)M64;
     hipStream_t s = (hipStream_t)stream;
     // (8 waves for the 128-channel form too: 256-row tiles hold 3 whole 9 x 9 images, 5 % padding)
-    if (Cin == 128 && Cout == 128 && ks == 3 && Ho * Wo <= conv::Cfg32<128, 128, 3, 8, MAPF_CONV_STAGES>::BM)
+    if (Cin == 128 && Cout == 128 && ks == 3 && conv::launch_img<128, 128, 3, 8>(x, w_packed, bias, y, (int)nimg, H, W, pad, 0, 1, s));
+    else if (Cin == 256 && Cout == 256 && ks == 2 && conv::launch_img<256, 256, 2, 8>(x, w_packed, bias, y, (int)nimg, H, W, pad, 0, 1, s));
+    else if (Cin == 128 && Cout == 128 && ks == 3 && Ho * Wo <= conv::Cfg32<128, 128, 3, 8, MAPF_CONV_STAGES>::BM)
         conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, 0, s, true);
     else if (Cin == 256 && Cout == 256 && ks == 2 && Ho * Wo <= conv::Cfg32<256, 256, 2, 8, MAPF_CONV_STAGES>::BM)
         conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, 0, s, true);
@@ -536,6 +779,12 @@ int mapf_conv_nhwc_pool_f16(const uint16_t *x, const uint16_t *w_packed, const u
 #else
     return MAPF_EINVAL;
 #endif
+}
+
+int mapf_conv_select(int32_t impl) {
+    if (impl < 0 || impl > 2) return MAPF_EINVAL;
+    conv::g_conv_impl = impl;
+    return MAPF_OK;
 }
 
 int mapf_conv_first_f32(const float *x_nchw, const uint16_t *w, const uint16_t *bias, uint16_t *y, int64_t nimg,

@@ -476,9 +476,15 @@ inline int grid_for(long items, int per_block) {
 typedef _Float16 gh8_t __attribute__((ext_vector_type(8)));
 typedef float gf16_t __attribute__((ext_vector_type(16)));
 constexpr int GL_BM = 64, GL_BK = 32, GL_D = 512;
-constexpr int GL_ABYTES = GL_BM * GL_BK * 2, GL_BBYTES = GL_D * GL_BK * 2, GL_BUF = GL_ABYTES + GL_BBYTES;
-constexpr int GL_LDS = 2 * GL_BUF;
-static_assert(GL_BM * GL_D * 2 <= GL_LDS, "epilogue tile");
+// MT = 64-row tiles per workgroup sharing each staged W chunk (round 5: MT = 2 halves the W bytes
+// per row -- 32 KiB of W per 32-deep chunk were 8 of every 9 bytes the kernel DMA'd at MT = 1)
+template <int MT>
+struct GL {
+    static constexpr int ABYTES = MT * GL_BM * GL_BK * 2, BBYTES = GL_D * GL_BK * 2, BUF = ABYTES + BBYTES;
+    static constexpr int LDS = 2 * BUF;
+    static_assert(GL_BM * GL_D * 2 <= LDS, "epilogue tile");
+};
+constexpr int GL_LDS = GL<1>::LDS;
 
 __device__ __attribute__((aligned(16))) uint4 g_lin_zero[1];    // source of the rows past M
 
@@ -505,7 +511,7 @@ struct TokSrc {
     int x_every;        // > 1: write back only rows g with g % x_every == 0 (token 0 of each sequence)
 };
 
-template <int EPI>
+template <int EPI, int MT>
 __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
                                                         const uint16_t *__restrict__ bias, long M,
                                                         uint16_t *__restrict__ out, float *__restrict__ x,
@@ -515,16 +521,18 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const long m0 = (long)blockIdx.x * GL_BM;
+    using G = GL<MT>;
+    constexpr int AW = 4 * MT;                                 // waves that fill A (16 rows each)
+    const long mt0 = (long)blockIdx.x * GL_BM * MT;
     // one DMA instruction fills 16 rows x 64 B lane-linearly: lane l -> row 16 g + (l >> 2),
     // physical piece l & 3 = logical piece q (the same for every g)
     const int q = (lane & 3) ^ ((lane >> 4) & 3);
-    const long rowA = m0 + 16 * wave + (lane >> 2);            // waves 0..3 fill A rows 16w..16w+15
-    const uint16_t *srcA = (wave < 4 && rowA < M) ? A + rowA * GL_D + q * 8 : nullptr;
+    const long rowA = mt0 + 16 * wave + (lane >> 2);           // waves 0..AW-1 fill A rows 16w..16w+15
+    const uint16_t *srcA = (wave < AW && rowA < M) ? A + rowA * GL_D + q * 8 : nullptr;
     auto issue = [&](int c, int buf) {
-        char *As = smem + buf * GL_BUF;
-        char *Bs = As + GL_ABYTES;
-        if (wave < 4)
+        char *As = smem + buf * G::BUF;
+        char *Bs = As + G::ABYTES;
+        if (wave < AW)
             gl_dma16(srcA ? (const void *)(srcA + c * GL_BK) : (const void *)g_lin_zero, As + 16 * wave * 64);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {                          // wave w fills W rows 64w..64w+63
@@ -533,37 +541,47 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
         }
     };
     const int wm = wave & 1, wn = wave >> 1, fr = lane & 31, fh = lane >> 5;
-    gf16_t acc[4];
+    gf16_t acc[MT][4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
-        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            for (int r = 0; r < 16; ++r) acc[i][b][r] = 0.f;
     constexpr int NCH = GL_D / GL_BK;
     issue(0, 0);
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
             issue(c + 1, (c + 1) & 1);
-            // chunk c's copies have landed: the 5 (waves 0..3) or 4 copies of chunk c + 1 may not
-            if (wave < 4) __builtin_amdgcn_s_waitcnt(0x0F70 | 5);
+            // chunk c's copies have landed: the 5 (A-filling waves) or 4 copies of chunk c + 1 may not
+            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0F70 | 5);
             else __builtin_amdgcn_s_waitcnt(0x0F70 | 4);
         } else {
             __builtin_amdgcn_s_waitcnt(0x0F70);
         }
         __builtin_amdgcn_s_barrier();
-        const char *As = smem + (c & 1) * GL_BUF;
-        const char *Bs = As + GL_ABYTES;
+        const char *As = smem + (c & 1) * G::BUF;
+        const char *Bs = As + G::ABYTES;
 #pragma unroll
         for (int s = 0; s < GL_BK / 16; ++s) {
             const int qq = 2 * s + fh;
-            const gh8_t af = *reinterpret_cast<const gh8_t *>(As + gl_swz(32 * wm + fr, qq));
+            gh8_t af[MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i] = *reinterpret_cast<const gh8_t *>(As + gl_swz(64 * i + 32 * wm + fr, qq));
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const gh8_t bf = *reinterpret_cast<const gh8_t *>(Bs + gl_swz(128 * wn + 32 * b + fr, qq));
-                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[b], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < MT; ++i) acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf, acc[i][b], 0, 0, 0);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
     }
+    // the 64-row tiles one after the other through one LDS tile
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+    const long m0 = mt0 + (long)GL_BM * i;
+    if (i > 0) __syncthreads();                                 // the previous tile's epilogue is done with it
     // y = fp16(acc + bias) -> LDS tile
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -572,7 +590,7 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            *reinterpret_cast<uint16_t *>(smem + gl_tile(row, n)) = (uint16_t)f2h(acc[b][r] + bv);
+            *reinterpret_cast<uint16_t *>(smem + gl_tile(row, n)) = (uint16_t)f2h(acc[i][b][r] + bv);
         }
     }
     __syncthreads();
@@ -620,7 +638,7 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
             }
             ln_rows<R>(av, cv, live, lane, gamma, beta, eps, zr);
         }
-        return;
+        continue;
     }
     // EPI 0 (GELU + dropout): wave w takes rows w, w + 8, ...; lane holds columns 4l..4l+3 and 256+4l..
     for (int row = wave; row < GL_BM; row += 8) {
@@ -650,6 +668,21 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
             reinterpret_cast<uint2 *>(out)[i1] = o[1];
         }
     }
+    }
+}
+
+// MT row tiles per workgroup (mapf_linear512_select): 2 (80 KiB of LDS, two workgroups per CU), 1, or
+// 0 (default): per kernel as measured (tools/bench_lin_impl.py: residual + LayerNorm 940 -> 917 us
+// at 128 rows, GELU 685 -> 795 us -- slower)
+static int g_lin_mt = 0;
+template <int EPI, class... Args>
+static void launch_linear512(long rows, hipStream_t s, Args... args) {
+    if (g_lin_mt == 2 || (g_lin_mt == 0 && EPI == 1))
+        hipLaunchKernelGGL((linear512_kernel<EPI, 2>), dim3((unsigned)((rows + 2 * GL_BM - 1) / (2 * GL_BM))), dim3(512),
+                           GL<2>::LDS, s, args...);
+    else
+        hipLaunchKernelGGL((linear512_kernel<EPI, 1>), dim3((unsigned)((rows + GL_BM - 1) / GL_BM)), dim3(512),
+                           GL<1>::LDS, s, args...);
 }
 
 // ---- attention backward (the training forward's attention, transformer.py:48-85) ---------
@@ -864,12 +897,17 @@ int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
+int mapf_linear512_select(int32_t row_tiles) {
+    if (row_tiles < 0 || row_tiles > 2) return MAPF_EINVAL;
+    pol::g_lin_mt = row_tiles;
+    return MAPF_OK;
+}
+
 int mapf_linear512_gelu_dropout(const uint16_t *a, const uint16_t *w, const uint16_t *bias, uint16_t *out, int64_t rows,
                                 float p, uint64_t seed, void *stream) {
     if (!a || !w || !bias || !out || rows < 0 || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
     if (rows == 0) return MAPF_OK;
-    hipLaunchKernelGGL(pol::linear512_kernel<0>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
-                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, out, nullptr, nullptr, nullptr,
+    pol::launch_linear512<0>((long)rows, (hipStream_t)stream, a, w, bias, (long)rows, out, nullptr, nullptr, nullptr,
                        nullptr, 0.f, pol::drop_threshold(p), 1.f / (1.f - p), seed, pol::TokSrc{});
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
@@ -879,8 +917,7 @@ int mapf_linear512_residual_layernorm(const uint16_t *a, const uint16_t *w, cons
                                       float p, uint64_t seed, void *stream) {
     if (!a || !w || !bias || !x || !gamma || !beta || !z || rows < 0 || !(p >= 0.f && p < 1.f)) return MAPF_EINVAL;
     if (rows == 0) return MAPF_OK;
-    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
-                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
+    pol::launch_linear512<1>((long)rows, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
                        pol::drop_threshold(p), 1.f / (1.f - p), seed, pol::TokSrc{});
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
@@ -893,8 +930,7 @@ int mapf_linear512_residual_layernorm_rows(const uint16_t *a, const uint16_t *w,
     if (rows == 0) return MAPF_OK;
     pol::TokSrc tok{};
     tok.x_every = x_every;
-    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
-                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
+    pol::launch_linear512<1>((long)rows, (hipStream_t)stream, a, w, bias, (long)rows, nullptr, x, gamma, beta, z, eps,
                        pol::drop_threshold(p), 1.f / (1.f - p), seed, tok);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
@@ -911,8 +947,7 @@ int mapf_linear512_tokens_residual_layernorm(const uint16_t *a, const uint16_t *
     const long rows = (long)B * (L + 1);
     const pol::TokSrc tok{tok_A, tok_VV, tok_cls, tok_pos, (int)L, pol::drop_threshold(tok_p), 1.f / (1.f - tok_p),
                           tok_seed, 1};
-    hipLaunchKernelGGL(pol::linear512_kernel<1>, dim3((unsigned)((rows + pol::GL_BM - 1) / pol::GL_BM)), dim3(512),
-                       pol::GL_LDS, (hipStream_t)stream, a, w, bias, rows, nullptr, x, gamma, beta, z, eps,
+    pol::launch_linear512<1>((long)rows, (hipStream_t)stream, a, w, bias, rows, nullptr, x, gamma, beta, z, eps,
                        pol::drop_threshold(p), 1.f / (1.f - p), seed, tok);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }

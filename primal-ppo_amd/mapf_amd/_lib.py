@@ -109,6 +109,7 @@ SIGNATURES = {
                                            P]),
     "mapf_normalize_advantages_dlam": (ctypes.c_int, [P, P, P, P, P, P, I32, P, I32, P]),
     "mapf_linear512_gelu_dropout": (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
+    "mapf_linear512_select": (ctypes.c_int, [I32]),
     "mapf_linear512_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float, ctypes.c_float,
                                                           ctypes.c_uint64, P]),
     "mapf_linear512_residual_layernorm_rows": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float,
@@ -118,6 +119,7 @@ SIGNATURES = {
                                                                 ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_conv_nhwc_pool_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P]),
     "mapf_conv_first_f32": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, P]),
+    "mapf_conv_select": (ctypes.c_int, [I32]),
     "mapf_conv_nhwc_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P]),
     "mapf_attention_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I32, I32, ctypes.c_float, P]),
     "mapf_attention_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I64, I64, I32,

@@ -8,8 +8,9 @@ the same calls either way).  Each rank trains on its half of the same minibatche
 g5 minibatch, then two seeded ones) with MIOpen's deterministic algorithms and dropout off.
 Checked per update: every rank's advantages equal the one-process advantages' rows (1e-5); both
 ranks hold bit-identical weights; the two-rank weights equal the one-process weights within the
-spread of the update itself under a change of summation order (the same one-process update on a
-row-permuted minibatch)."""
+fp16 autocast backward's rounding: the all-reduced (unscaled, clipped) gradient within 2e-2 (relative L2) of the
+one-process gradient, the weights within the sum of both runs' largest per-step moves (Adam moves tiny-gradient
+elements as far as large ones)."""
 import os
 import socket
 import sys
@@ -67,6 +68,10 @@ def _train(batches, world=1, rank=0, perm=None):
 
 
 def _train_recorded(batches, world, rank, perm, seen):
+    return _train_model(batches, world, rank, perm, seen, [])
+
+
+def _train_model(batches, world, rank, perm, seen, grads):
     from mapf_amd.model import Model
     from test_net import det_weights
     m = Model(0, "cuda", global_model=True, numChannel=6, num_agents=2, fov=9)
@@ -85,11 +90,14 @@ def _train_recorded(batches, world, rank, perm, seen):
         s = m.train(g("observation"), g("vector"), g("returns"), g("cost_returns"), g("old_v"), g("old_cv"),
                     g("action"), g("old_ps"), np.zeros((len(sl), 2, 2, 512), np.float32), g("train_valid"), 3.0)
         stats.append(np.array([float(np.asarray(x)) for x in s]))
+        # the update's gradient (all-reduced, unscaled, clipped) as the parameters hold it after the step
+        grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.network.parameters()
+                                if p.grad is not None]).cpu().numpy())
         weights.append(flat())
         adv, cadv = seen[-1]
         advs.append((adv.detach().cpu().numpy().reshape(len(sl), -1), cadv.detach().cpu().numpy().reshape(len(sl), -1),
                      sl))
-    return weights, advs, stats
+    return weights, advs, stats, grads
 
 
 def _worker(rank, world, port, batches, q):
@@ -99,8 +107,8 @@ def _worker(rank, world, port, batches, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        w, a, s = _train(batches, world, rank)
-        q.put((rank, w, [(x, y) for x, y, _ in a], s))
+        w, a, s, g = _train(batches, world, rank)
+        q.put((rank, w, [(x, y) for x, y, _ in a], s, g))
     finally:
         dist.destroy_process_group()
 
@@ -110,9 +118,7 @@ def test_model_train_two_ranks_equals_one_process():
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
     batches = _batches()
-    w1, a1, s1 = _train(batches)
-    # the update's own spread under a change of summation order: the same rows, permuted
-    wp, _, _ = _train(batches, perm=lambda r: r[::-1].copy())
+    w1, a1, s1, g1 = _train(batches)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -126,7 +132,8 @@ def test_model_train_two_ranks_equals_one_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, w_r0, a_r0, s_r0), (_, w_r1, a_r1, s_r1) = res
+    (_, w_r0, a_r0, s_r0, g_r0), (_, w_r1, a_r1, s_r1, g_r1) = res
+    lr = 1e-5                                   # TrainingParameters.lr (alg_parameters.py:52)
     for k in range(len(batches)):
         R = len(batches[k]["returns"])
         adv1, cadv1, _ = a1[k]
@@ -135,15 +142,24 @@ def test_model_train_two_ranks_equals_one_process():
             rows = slice(r * R // 2, (r + 1) * R // 2)
             np.testing.assert_allclose(adv, adv1[rows], rtol=1e-5, atol=1e-5, err_msg=f"update {k} rank {r} adv")
             np.testing.assert_allclose(cadv, cadv1[rows], rtol=1e-5, atol=1e-5, err_msg=f"update {k} rank {r} cadv")
-        # both ranks hold the same weights (the all-reduced gradient, the same Adam step)
+        # both ranks hold the same gradient (all-reduced) and the same weights (the same Adam step)
+        np.testing.assert_array_equal(g_r0[k], g_r1[k], err_msg=f"update {k}")
         np.testing.assert_array_equal(w_r0[k + 1], w_r1[k + 1], err_msg=f"update {k}")
+        # the all-reduced gradient is the whole minibatch's, to the fp16 autocast backward's rounding
+        # (each rank's backward runs on other rows, so its fp16 intermediates round differently)
+        r_grad = np.linalg.norm(g_r0[k] - g1[k]) / np.linalg.norm(g1[k])
+        print(f"update {k}: gradient two ranks vs one process, relative {r_grad:.3e}")
+        assert r_grad < 2e-2, (k, r_grad)
         # the averaged stats agree across ranks and with one process (global means)
         np.testing.assert_array_equal(s_r0[k], s_r1[k])
         np.testing.assert_allclose(s_r0[k][[9, 10]], s1[k][[9, 10]], atol=1e-5)
-        # the weights' total change: two ranks vs one process, within the update's own spread
+        # the weights: Adam moves an element by at most ~lr per step whatever its gradient's size, so
+        # gradients that differ in their last bits can differ by up to 2 lr per update where they are
+        # tiny (|g| ~ eps = 1e-8, fp16 subnormals under the loss scale); the total change agrees
         moved = np.linalg.norm(w1[k + 1] - w1[0])
-        assert moved > 0
         r_dist = np.linalg.norm(w_r0[k + 1] - w1[k + 1]) / moved
-        r_perm = np.linalg.norm(wp[k + 1] - w1[k + 1]) / moved
-        print(f"update {k}: two ranks vs one process {r_dist:.3e}, permuted rows vs one process {r_perm:.3e}")
-        assert r_dist <= max(3 * r_perm, 1e-3), (k, r_dist, r_perm)
+        print(f"update {k}: weights two ranks vs one process, relative to their change {r_dist:.3e}")
+        assert moved > 0 and r_dist < 5e-2, (k, r_dist)
+        steps = sum(max(np.abs(wa - wb).max(), np.abs(ra - rb).max())
+                    for wa, wb, ra, rb in zip(w1[1:k + 2], w1[:k + 1], w_r0[1:k + 2], w_r0[:k + 1]))
+        assert np.abs(w_r0[k + 1] - w1[k + 1]).max() <= steps * 1.001 and steps < 50 * lr * (k + 1)

@@ -291,11 +291,21 @@ def test_fp16_weight_cache_follows_in_place_updates():
     torch.testing.assert_close(got[5].float(), ref[5].float(), rtol=3e-2, atol=3e-2)
 
 
+@pytest.fixture(params=[2, 0], ids=["image_resident", "per_tap"])
+def conv_impl(request):
+    """Both implicit-GEMM forms (mapf_conv_select: 2 image-resident, 0 per-tap staged; the default 1
+    picks one of them per layer)."""
+    from mapf_amd import _lib
+    _lib.check(_lib.lib().mapf_conv_select(request.param))
+    yield request.param
+    _lib.check(_lib.lib().mapf_conv_select(1))
+
+
 @pytest.mark.parametrize("ci,co,ks,H,B", [(128, 128, 3, 9, 37), (128, 128, 3, 11, 3), (128, 256, 2, 4, 50),
                                          (256, 256, 2, 5, 33), (256, 256, 2, 6, 7), (128, 128, 3, 9, 1),
                                          (128, 128, 3, 9, 1001), (128, 256, 2, 4, 2111), (256, 256, 2, 6, 1003)])
 @pytest.mark.parametrize("relu", [0, 1])
-def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
+def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu, conv_impl):
     """mapf_conv_nhwc_f16 (MFMA implicit GEMM, csrc/mapf_conv.hip) == the autocast conv (fp16
     operands, fp32 accumulation, fp16 output; + fp16 bias, ReLU) to fp16 rounding -- ragged
     pixel counts (the last tile's rows past M), every padding tap, 3x3 and 2x2, and grids with
@@ -321,7 +331,7 @@ def test_conv_kernel_vs_torch(ci, co, ks, H, B, relu):
 
 @pytest.mark.parametrize("ci,co,ks,H,B", [(128, 128, 3, 9, 37), (128, 128, 3, 9, 1), (128, 128, 3, 11, 5),
                                          (256, 256, 2, 6, 1003), (256, 256, 2, 6, 7)])
-def test_conv_pool_kernel_equals_conv_then_pool(ci, co, ks, H, B):
+def test_conv_pool_kernel_equals_conv_then_pool(ci, co, ks, H, B, conv_impl):
     """mapf_conv_nhwc_pool_f16 (whole-image tiles, pooled epilogue) == mapf_conv_nhwc_f16(relu=0) then
     mapf_nhwc_bias_relu_pool2, bit-identical; and == torch's relu(conv + b) then MaxPool2d(2) to
     fp16 rounding"""
@@ -479,3 +489,54 @@ def test_training_forward_uses_hip_attention_and_matches_sdpa():
             continue
         r_hip, r_spread = (a - b).norm().item() / nb, (c - b).norm().item() / nb
         assert r_hip <= max(2e-2, 3 * r_spread), (a.shape, r_hip, r_spread)
+
+
+@pytest.mark.parametrize("rows", [1, 64, 127, 129, 1000, 17 * 97])
+def test_linear512_row_tiles_are_bit_identical(rows):
+    """mapf_linear512_select: 128-row workgroups (two 64-row tiles sharing each staged weight chunk,
+    the default) give bit-identical outputs to 64-row workgroups -- the same MFMA sequence per
+    element, the same epilogues -- for the GELU, residual + LayerNorm, rows and tokens variants,
+    ragged row counts included (the last workgroup's second tile partly or wholly past M)."""
+    from mapf_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a = torch.randn(rows, 512, device="cuda", generator=g).half()
+    w = (torch.randn(512, 512, device="cuda", generator=g) / 512 ** 0.5).half()
+    b = (torch.randn(512, device="cuda", generator=g) * 0.1).half()
+    gamma = 1 + 0.1 * torch.randn(512, device="cuda", generator=g)
+    beta = 0.1 * torch.randn(512, device="cuda", generator=g)
+    x0 = torch.randn(rows, 512, device="cuda", generator=g)
+    Bt = max(1, rows // 17)
+    A = torch.rand(Bt, 16, device="cuda", generator=g)
+    VV = torch.randn(Bt, 512, device="cuda", generator=g).half()
+    cls, pos = torch.randn(512, device="cuda", generator=g), torch.randn(17, 512, device="cuda", generator=g)
+    at = torch.randn(Bt * 17, 512, device="cuda", generator=g).half()
+
+    def run():
+        out = torch.full((rows, 512), float("nan"), dtype=torch.float16, device="cuda")
+        _lib.check(L.mapf_linear512_gelu_dropout(_p(a), _p(w), _p(b), _p(out), rows, 0.2, 7, st))
+        x1, z1 = x0.clone(), torch.full((rows, 512), float("nan"), dtype=torch.float16, device="cuda")
+        _lib.check(L.mapf_linear512_residual_layernorm(_p(a), _p(w), _p(b), _p(x1), _p(gamma), _p(beta), _p(z1), rows,
+                                                       1e-5, 0.2, 8, st))
+        x2, z2 = x0.clone(), torch.full((rows, 512), float("nan"), dtype=torch.float16, device="cuda")
+        _lib.check(L.mapf_linear512_residual_layernorm_rows(_p(a), _p(w), _p(b), _p(x2), _p(gamma), _p(beta), _p(z2),
+                                                            rows, 1e-5, 0.2, 9, 17, st))
+        x3 = torch.full((Bt * 17, 512), float("nan"), device="cuda")
+        z3 = torch.full((Bt * 17, 512), float("nan"), dtype=torch.float16, device="cuda")
+        _lib.check(L.mapf_linear512_tokens_residual_layernorm(_p(at), _p(w), _p(b), _p(x3), _p(gamma), _p(beta), _p(z3),
+                                                              Bt, 16, 1e-5, 0.2, 10, _p(A), _p(VV), _p(cls), _p(pos),
+                                                              0.1, 11, st))
+        torch.cuda.synchronize()
+        return out, x1, z1, x2, z2, x3, z3
+
+    try:
+        _lib.check(L.mapf_linear512_select(2))
+        two = run()
+        _lib.check(L.mapf_linear512_select(1))
+        one = run()
+    finally:
+        _lib.check(L.mapf_linear512_select(0))
+    for k, (u, v) in enumerate(zip(two, one)):
+        assert torch.isfinite(u.float()).all(), k
+        assert torch.equal(u, v), k
