@@ -446,6 +446,9 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
     } else if (!G.wave && L.lut && !skip_band && ((E * N * CFF) & 3) == 0 && (nt & 7) == 0) {
         // the same table-driven expansion for a workgroup's stream: thread t's float4s
         // q = t + nt*k keep the bit field 4(t & 7) of words (t >> 3) + (nt / 8) k
+        int tid = G.tid;
+        asm volatile("" : "+v"(tid));      // opaque here: its pointers are not hoisted into the
+                                           // persistent kernels' loop prologue (VGPR spills there)
         const int sh = (tid & 7) * 4;
         const uint32_t *swp = stream + (tid >> 3);
         float4 *dp = reinterpret_cast<float4 *>(dst) + tid;
@@ -457,6 +460,8 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         for (size_t q = ((total >> 2) << 2) + tid; q < total; q += nt)
             dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
     } else if (((E * N * CFF) & 3) == 0) {
+        int tid = G.tid;
+        asm volatile("" : "+v"(tid));      // (as above)
         const size_t n4 = total >> 2;
         float4 *d4 = reinterpret_cast<float4 *>(dst);
         int z0 = 0, z1 = 0;
@@ -477,6 +482,8 @@ __device__ inline void obs_emit(const DevEnv &e, const ObsLds &L, float *__restr
         for (size_t q = (n4 << 2) + tid; q < total; q += nt)
             dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
     } else {
+        int tid = G.tid;
+        asm volatile("" : "+v"(tid));      // (as above)
         for (size_t q = tid; q < total; q += nt) dst[q] = (float)((stream[q >> 5] >> (q & 31)) & 1u);
     }
 }

@@ -444,6 +444,12 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void r
     rollout_wide_body<T, RW, NT>(args->e, T_steps, args->ro);
 }
 
+// The three-wave form is not built for 128-bit rows spread over two lanes (maps over 64 x 64 cells on
+// both axes): at 168 VGPRs that instantiation spilled 136-188 B per lane to scratch, and
+// such maps carry the BFS channel in the BASELINE configs (c5), which the three-wave form excludes.
+template <class T, int RW>
+constexpr bool wide3_form() { return !(std::is_same<T, srch::Row2>::value && RW == 2); }
+
 template <class T, int RW>
 static bool wide_fits(const DevEnv &e) { return wide_lds_bytes<T, RW>(e) <= 64 * 1024; }
 
@@ -470,8 +476,10 @@ static WidePlan plan_wide_t(const DevEnv &e, int slots, const mapf_tuning &tu) {
     p.nt = tu.wide_nt >= 0 ? tu.wide_nt != 0 : (slots || (size_t)e.B * e.N * e.C * e.F * e.F * 4 > ((size_t)128 << 20));
     const void *kern = p.nt ? reinterpret_cast<const void *>(rollout_wide_kernel<T, RW, true>)
                             : reinterpret_cast<const void *>(rollout_wide_kernel<T, RW, false>);
-    const void *kern3 = p.nt ? reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, true>)
-                             : reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, false>);
+    const void *kern3 = nullptr;
+    if constexpr (wide3_form<T, RW>())
+        kern3 = p.nt ? reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, true>)
+                     : reinterpret_cast<const void *>(rollout_wide3_kernel<T, RW, false>);
     // two waves per env where every env's pair fits at once: the VGPR budget of a SIMD
     // (512 per lane) over the waves it must hold, 4 SIMDs per CU
     const int fit = 512 / ((kernel_vgprs(kern) + 7) & ~7);
@@ -501,9 +509,9 @@ static WidePlan plan_wide_t(const DevEnv &e, int slots, const mapf_tuning &tu) {
     // on its SIMDs -- a SIMD asked for a fourth wave (4 x 152 VGPRs > 512) and part of the grid
     // ran in a second round (c4: 6.2 or 8.3 us per step by launch); one workgroup per CU is
     // spread evenly
-    const int fit3 = 512 / ((kernel_vgprs(kern3) + 7) & ~7);
+    const int fit3 = kern3 ? 512 / ((kernel_vgprs(kern3) + 7) & ~7) : 0;
     const size_t lds3 = wide_a16(lds + wide_scratch_bytes<T, RW>(e));
-    if (r.overlap && (3 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit3 && lds3 <= (occ > 1 ? cap : (size_t)64 * 1024) &&
+    if (kern3 && r.overlap && (3 * e.B + 4 * ncu - 1) / (4 * ncu) <= fit3 && lds3 <= (occ > 1 ? cap : (size_t)64 * 1024) &&
         e.B % occ == 0 && 3 * occ <= 12 && (size_t)occ * lds3 + 32 <= (size_t)device_max_group_lds() &&
         tu.wide_obs >= 2) {
         r.wpe = 3;
@@ -546,12 +554,14 @@ static int launch_wide_t(const DevEnv &e, int steps, const WideOut &ro, const ma
     r.out = ro.out;
     r.obs = ro.obs;
     r.vec = ro.vec;
-    if (r.wpe == 3) {
-        const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
-        if (!args) return MAPF_ESTATE;
-        auto kern3 = p.nt ? rollout_wide3_kernel<T, RW, true> : rollout_wide3_kernel<T, RW, false>;
-        hipLaunchKernelGGL(kern3, dim3(p.grid), dim3(p.block), p.lds, s, args, steps);
-        return MAPF_OK;
+    if constexpr (wide3_form<T, RW>()) {
+        if (r.wpe == 3) {
+            const WideArgs *args = push_args(ring, WideArgs{e, r}, s);
+            if (!args) return MAPF_ESTATE;
+            auto kern3 = p.nt ? rollout_wide3_kernel<T, RW, true> : rollout_wide3_kernel<T, RW, false>;
+            hipLaunchKernelGGL(kern3, dim3(p.grid), dim3(p.block), p.lds, s, args, steps);
+            return MAPF_OK;
+        }
     }
     auto kern = p.nt ? rollout_wide_kernel<T, RW, true> : rollout_wide_kernel<T, RW, false>;
 #if MAPF_ARGS_PTR

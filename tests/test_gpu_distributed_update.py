@@ -160,6 +160,6 @@ def test_model_train_two_ranks_equals_one_process():
         r_dist = np.linalg.norm(w_r0[k + 1] - w1[k + 1]) / moved
         print(f"update {k}: weights two ranks vs one process, relative to their change {r_dist:.3e}")
         assert moved > 0 and r_dist < 5e-2, (k, r_dist)
-        steps = sum(max(np.abs(wa - wb).max(), np.abs(ra - rb).max())
+        steps = sum(np.abs(wa - wb).max() + np.abs(ra - rb).max()
                     for wa, wb, ra, rb in zip(w1[1:k + 2], w1[:k + 1], w_r0[1:k + 2], w_r0[:k + 1]))
         assert np.abs(w_r0[k + 1] - w1[k + 1]).max() <= steps * 1.001 and steps < 50 * lr * (k + 1)
