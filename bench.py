@@ -207,7 +207,11 @@ def pmc_traffic_per_step(B, N, H, W, F, C, kernel, slots=False):
         return None
     with open(path) as f:
         rep = json.load(f)
-    return rep["traffic_bytes"] / rep.get("steps_per_launch", 1) / 1e6
+    # WRITE + 2 x FETCH: FETCH_SIZE counts 64 B per 128-B line read, for these kernels' narrow reads as
+    # for wide streams (round-5 calibration, profiles/r05_fetch_calibration.json); reports written
+    # before it stored WRITE + FETCH as traffic_bytes
+    t = rep["write_bytes"] + rep["fetch_bytes_x2"] if "fetch_bytes_x2" in rep else rep["traffic_bytes"]
+    return t / rep.get("steps_per_launch", 1) / 1e6
 
 
 def launch_ranks(n):
@@ -546,7 +550,7 @@ def main():
                          "peak": None if ic_resident else HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": None if ic_resident else round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic * steps_pl, 3) if traffic is not None else None,
-                         "traffic_unit": "MB/launch (PMC)", "steps_per_launch": steps_pl,
+                         "traffic_unit": "MB/launch (PMC: WRITE_SIZE + 2 x FETCH_SIZE)", "steps_per_launch": steps_pl,
                          "algorithmic_mb": round(bpa * B * N * steps_pl / 1e6, 3), "bytes_per_agent_step": bpa,
                          "agents_per_step": B * N,
                          "residency": ("--inplace: the re-written [B] observation buffer (%.0f MB) stays in the 256 MiB "

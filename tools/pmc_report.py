@@ -6,10 +6,11 @@ HBM traffic of the roofline kernel, written as JSON under profiles/.
 
 Units and corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM /
 rocprofv3 section): both counters are in KiB; WRITE_SIZE is exact for the
-16 B/lane streaming stores the observe kernel issues; FETCH_SIZE reads half the
-bytes of WIDE (16 B/lane) streaming reads and is uncalibrated for narrower
-widths -- the observe kernel's reads are 1-8 B/lane, so the raw figure is kept
-and the x2 figure reported beside it as an upper bound.
+16 B/lane streaming stores the observe kernel issues; FETCH_SIZE counts 64 B per
+128-B line fetched -- half the bytes of wide (16 B/lane) streaming reads (the
+guide) and half the distinct 128-B lines of the kernels' narrow dword reads too
+(calibrated in round 5 on the BFS-window pattern: tools/fetch_calib.hip,
+profiles/r05_fetch_calibration.json) -- so traffic = WRITE + 2 x FETCH.
 """
 import argparse
 import csv
@@ -47,14 +48,15 @@ def main():
     rep = {
         "kernel": a.kernel, "launches": {"WRITE_SIZE": nw, "FETCH_SIZE": nf},
         "write_bytes": w, "fetch_bytes_raw": f, "fetch_bytes_x2": 2 * f,
-        "traffic_bytes": w + f,
+        "traffic_bytes": w + 2 * f,
         "steps_per_launch": a.steps_per_launch,
         "note": "per launch; counters in KiB x1024; WRITE_SIZE exact for 16 B/lane stores; "
-                "FETCH_SIZE raw (narrow reads, uncalibrated), x2 = wide-read correction upper bound",
+                "FETCH_SIZE = 64 B per 128-B line read (calibrated: profiles/r05_fetch_calibration.json): "
+                "traffic = WRITE + 2 x FETCH",
     }
     if a.algorithmic_bytes:
         rep["algorithmic_bytes"] = a.algorithmic_bytes
-        rep["traffic_over_algorithmic"] = (w + f) / a.algorithmic_bytes
+        rep["traffic_over_algorithmic"] = (w + 2 * f) / a.algorithmic_bytes
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(rep, open(a.out, "w"), indent=1)
     print(json.dumps(rep))
