@@ -39,6 +39,7 @@ for p in (ROOT, os.path.join(ROOT, "primal-ppo_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+import mapf_amd  # noqa: E402,F401  (sets the HIP graph-capture mode before the runtime starts)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -4,7 +4,24 @@ Host-side mirror of the reference's env/runner API (Nielsencu/primal-ppo
 mapf_gym.py / runner.py) over the HIP C ABI in ../lib/libmapf.so
 (include/mapf.h).  The GPU path is the only path: if libmapf.so is missing
 or no GPU is visible, calls fail loudly -- there is no CPU fallback.
-"""
-from .config import EnvParameters, TrainingParameters, NetParameters, make_config  # noqa: F401
 
-__all__ = ["EnvParameters", "TrainingParameters", "NetParameters", "make_config"]
+Graph capture mode.  ROCm 7's HIP runtime records a hipGraph capture as
+prebuilt AQL packets by default (DEBUG_CLR_GRAPH_PACKET_CAPTURE=1).  In that
+mode a captured hipMemsetAsync takes effect on the first replay only
+(tools/diag_graph20.py: memset(0) + add(1) replays to 1, then to garbage), so
+every captured multi-block torch reduction -- its semaphores are zeroed by a
+captured memset -- returns stale partial sums from the second replay on: the
+captured PPO update's bias gradients, grad norm and loss means.
+The runtime reads the flag at its first HIP call, so it is switched off here,
+before torch or libmapf touch the GPU; an explicit setting in the environment
+is kept, and Model checks captured reductions before it captures an update
+(model.captured_reductions_ok).
+"""
+import os as _os
+
+GRAPH_CAPTURE_FLAG = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+_os.environ.setdefault(GRAPH_CAPTURE_FLAG, "0")
+
+from .config import EnvParameters, TrainingParameters, NetParameters, make_config  # noqa: F401,E402
+
+__all__ = ["EnvParameters", "TrainingParameters", "NetParameters", "make_config", "GRAPH_CAPTURE_FLAG"]

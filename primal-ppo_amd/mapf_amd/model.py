@@ -327,6 +327,39 @@ class Model:
         return [np.asarray(v) for v in stats] + [self.lagrange.get_lagrangian_param()]
 
 
+_REDUCTIONS_OK = {}
+
+
+def captured_reductions_ok(device):
+    """Whether a captured multi-block torch reduction gives the right sum on every replay in this
+    process (mapf_amd/__init__.py: with the HIP runtime's packet capture on, the captured memset that
+    zeroes the reduction's semaphores takes effect on the first replay only).  One exact fp32 sum of
+    1088 x 1536 ones, captured, its output poisoned with NaN before each of three replays."""
+    dev = torch.device(device)
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    if key not in _REDUCTIONS_OK:
+        x = torch.ones(1088, 1536, device=dev)
+        want = float(x.numel())                   # < 2^24: exact in fp32 whatever the order
+        g, s = torch.cuda.CUDAGraph(), torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                y = x.sum().reshape(1)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        got = []
+        for _ in range(3):
+            y.fill_(float("nan"))
+            g.replay()
+            got.append(y.item())
+        del g
+        _REDUCTIONS_OK[key] = all(v == want for v in got)
+        if not _REDUCTIONS_OK[key]:
+            import warnings
+            warnings.warn(f"captured torch reductions replay wrong on this HIP runtime ({got}, want {want}; "
+                          f"is DEBUG_CLR_GRAPH_PACKET_CAPTURE=1?): the PPO update runs eagerly", RuntimeWarning)
+    return _REDUCTIONS_OK[key]
+
+
 class _DeviceUpdate:
     """The static buffers and the body of one minibatch shape's device update (Model._train_device)."""
 
@@ -403,6 +436,8 @@ class _DeviceUpdate:
             self.stats.div_(dist.get_world_size())
 
     def run(self, graph=True, allreduce=False):
+        if graph and self.graph is None and not captured_reductions_ok(self.model.device):
+            graph = False                   # the runtime would replay the update wrong: eager
         if not graph or self.eager_runs < self.WARMUP:
             if graph:                       # warm-up on a side stream, as capture wants
                 s = torch.cuda.Stream()

@@ -7,6 +7,10 @@ include/mapf.h declares.  GPU tests (-m gpu) are the parity tests proper.
 import os
 import sys
 
+# before anything initialises the HIP runtime: captured memsets replay once under packet capture
+# (primal-ppo_amd/mapf_amd/__init__.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "primal-ppo_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:

@@ -5,11 +5,11 @@ MIOpen's deterministic algorithms the replays must apply the same updates as the
 kernels: bitwise in practice), change the weights, keep the AMP state on the device, and leave the
 acting path on the new weights.
 
-The graphed model trains first and its eager twins after it, not interleaved: a SECOND model's
-eager update (backward + fused Adam) run between two replays of the first model's captured update
-makes a later replay non-finite (tools/diag_graph3.py; acting forwards, foreach ops, a fused Adam
-step or pinned-memory traffic in between do not).  One training model per process -- the driver's
-layout -- never interleaves that way."""
+The graphed model and its eager twins train INTERLEAVED, with small tensors allocated and freed
+between updates: before round 5 that made a later replay non-finite.  The cause was the HIP
+runtime's packet capture replaying a captured memset only once, so every captured multi-block
+reduction (bias gradients, grad norm) summed stale partials (DESIGN.md 6a,
+test_gpu_graph_capture_mode.py); mapf_amd switches that capture mode off."""
 import copy
 
 import numpy as np
@@ -27,6 +27,14 @@ def _batch(g, rows=64, n=8):
     ps = torch.softmax(torch.randn(rows, n, 5, device="cuda", generator=g), -1)
     tv = (torch.rand(rows, n, 5, device="cuda", generator=g) < 0.7).float()
     return obs, vec, ret, cret, v, cv, act, ps, tv
+
+
+def _churn():
+    """small tensors of 4 B .. 256 KiB allocated, NaN-filled and freed (the small-pool traffic the
+    host side of an update or a second model makes)"""
+    ts = [torch.full((1 << (k % 17),), float("nan"), device="cuda") for k in range(600)]
+    torch.cuda.synchronize()
+    del ts
 
 
 @pytest.fixture
@@ -58,8 +66,11 @@ def test_graphed_updates_equal_eager_updates(deterministic_convs, hip_attention,
     batches = [_batch(g) for _ in range(6)]
     w0 = m1.network.conv1.weight.detach().clone()
     init = [p.detach().clone() for p in m1.network.parameters()]
-    runs = {id(m): [m.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0)
-                    for (obs, vec, ret, cret, v, cv, act, ps, tv) in batches] for m in (m1, m2, m4)}
+    runs = {id(m): [] for m in (m1, m2, m4)}
+    for (obs, vec, ret, cret, v, cv, act, ps, tv) in batches:
+        for m in (m1, m2, m4):               # a second model's eager update between two replays
+            runs[id(m)].append(m.train(obs, vec, ret, cret, v, cv, act, ps, None, tv, 1.0))
+            _churn()
     for k in range(len(batches)):
         s1, s2, s4 = runs[id(m1)][k], runs[id(m2)][k], runs[id(m4)][k]
         # (grad_norm, stats[8], is inf when the fp16 backward overflowed: the AMP step is then
@@ -67,9 +78,10 @@ def test_graphed_updates_equal_eager_updates(deterministic_convs, hip_attention,
         assert all(np.isfinite(float(x)) for i, x in enumerate(s1) if i != 8), (k, s1)
         for i, (a, b) in enumerate(zip(s1, s2)):
             a, b = float(a), float(b)
-            if i == 8 and not (np.isfinite(a) and np.isfinite(b)):
-                assert np.isinf(a) == np.isinf(b), (k, a, b)
-                continue
+            if i == 8:                          # a non-finite norm only where the eager one is too
+                assert np.isfinite(a) == np.isfinite(b) and not np.isnan(a), (k, a, b)
+                if not np.isfinite(b):
+                    continue
             assert abs(a - b) <= max(1e-5 * max(1.0, abs(b)), 3 * abs(float(s4[i]) - b)), (k, i, a, b, float(s4[i]))
     assert len(m1.network._h16) == 0            # the acting path's fp16 weights are re-read
     upd = next(iter(m1._updates.values()))
@@ -116,5 +128,5 @@ def test_update_shapes_get_their_own_graphs():
     for rows in (32, 48, 32, 48, 32, 48, 32):
         b = _batch(g, rows)
         s = m.train(*b[:8], None, b[8], 0.5)
-        assert all(np.isfinite(float(x)) for k, x in enumerate(s) if k != 8)
+        assert all(np.isfinite(float(x)) or (k == 8 and np.isinf(float(x))) for k, x in enumerate(s))
     assert len(m._updates) == 2 and all(u.graph is not None for u in m._updates.values())
