@@ -385,6 +385,9 @@ int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const fl
  * or 0 (default) the faster as measured per kernel: 2 for the residual + LayerNorm forms, 1 for
  * GELU.  MAPF_EINVAL on another value. */
 int mapf_linear512_select(int32_t row_tiles);
+/* LDS stages of the mapf_linear512_* kernels' K ring (process-wide, bit-identical results): 2, 3, 4
+ * (stages - 1 weight/activation chunks in flight) or 0 (default, as measured).  MAPF_EINVAL otherwise. */
+int mapf_linear512_stages(int32_t stages);
 
 /* 512 x 512 Linear (w: fp16 [512 out][512 in], torch's layout; bias fp16 [512]) on `rows` contiguous fp16
  * rows a[rows][512] with its epilogue, one launch (MFMA GEMM; the linear's fp16 output stays on chip):

@@ -22,6 +22,7 @@
 // the element index, keyed by `seed`) -- a different stream than torch's own generator; the
 // reference's masks are random anyway (the net is never eval()-ed, net.py:50-51).
 #include <hip/hip_fp16.h>
+#include <cstdlib>
 
 #include "mapf.h"
 #include "mapf_common.h"
@@ -478,13 +479,16 @@ typedef float gf16_t __attribute__((ext_vector_type(16)));
 constexpr int GL_BM = 64, GL_BK = 32, GL_D = 512;
 // MT = 64-row tiles per workgroup sharing each staged W chunk (round 5: MT = 2 halves the W bytes
 // per row -- 32 KiB of W per 32-deep chunk were 8 of every 9 bytes the kernel DMA'd at MT = 1)
-template <int MT>
+// S = LDS stages of the K ring (round 5): S - 1 chunks in flight when a chunk is waited for, one
+// raw s_barrier per chunk (S = 2: one in flight -- two workgroups per CU at MT = 1; S = 3, 4: one
+// workgroup per CU whose DMA latency the ring itself covers)
+template <int MT, int S = 2>
 struct GL {
     static constexpr int ABYTES = MT * GL_BM * GL_BK * 2, BBYTES = GL_D * GL_BK * 2, BUF = ABYTES + BBYTES;
-    static constexpr int LDS = 2 * BUF;
+    static constexpr int LDS = S * BUF;
     static_assert(GL_BM * GL_D * 2 <= LDS, "epilogue tile");
+    static_assert(LDS <= 163840, "LDS per workgroup");
 };
-constexpr int GL_LDS = GL<1>::LDS;
 
 __device__ __attribute__((aligned(16))) uint4 g_lin_zero[1];    // source of the rows past M
 
@@ -511,7 +515,9 @@ struct TokSrc {
     int x_every;        // > 1: write back only rows g with g % x_every == 0 (token 0 of each sequence)
 };
 
-template <int EPI, int MT>
+// DBG (diagnostic forms, MAPF_LIN_DEBUG): 1 = the GEMM with a plain fp16 store as the epilogue, 2 = the
+// epilogue without the GEMM (acc = 0)
+template <int EPI, int MT, int S, int DBG = 0>
 __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
                                                         const uint16_t *__restrict__ bias, long M,
                                                         uint16_t *__restrict__ out, float *__restrict__ x,
@@ -521,7 +527,7 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    using G = GL<MT>;
+    using G = GL<MT, S>;
     constexpr int AW = 4 * MT;                                 // waves that fill A (16 rows each)
     const long mt0 = (long)blockIdx.x * GL_BM * MT;
     // one DMA instruction fills 16 rows x 64 B lane-linearly: lane l -> row 16 g + (l >> 2),
@@ -548,18 +554,27 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
         for (int b = 0; b < 4; ++b)
             for (int r = 0; r < 16; ++r) acc[i][b][r] = 0.f;
     constexpr int NCH = GL_D / GL_BK;
-    issue(0, 0);
-    for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) {
-            issue(c + 1, (c + 1) & 1);
-            // chunk c's copies have landed: the 5 (A-filling waves) or 4 copies of chunk c + 1 may not
-            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0F70 | 5);
-            else __builtin_amdgcn_s_waitcnt(0x0F70 | 4);
+    // ring: chunks 0 .. S-2 in flight; at chunk c wait until only the chunks after it (at most S - 2)
+    // are outstanding -- each wave's DMAs per chunk: 5 (A-filling waves) or 4 -- then ONE raw
+    // barrier (every wave's copies of chunk c have landed, every wave is done reading chunk c - 1),
+    // then refill chunk c - 1's buffer with chunk c + S - 1 and compute chunk c.  lgkmcnt(0) before the
+    // barrier: chunk c - 1's LDS reads have returned before its buffer is restaged.
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c) if (DBG != 2) issue(c, c);
+    for (int c = 0; c < (DBG == 2 ? 0 : NCH); ++c) {
+        const int ahead = (NCH - 1 - c) < (S - 2) ? (NCH - 1 - c) : (S - 2);
+        if (ahead >= 2) {
+            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0070 | 10);
+            else __builtin_amdgcn_s_waitcnt(0x0070 | 8);
+        } else if (ahead == 1) {
+            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0070 | 5);
+            else __builtin_amdgcn_s_waitcnt(0x0070 | 4);
         } else {
-            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __builtin_amdgcn_s_waitcnt(0x0070);
         }
         __builtin_amdgcn_s_barrier();
-        const char *As = smem + (c & 1) * G::BUF;
+        if (c + S - 1 < NCH) issue(c + S - 1, (c + S - 1) % S);
+        const char *As = smem + (c % S) * G::BUF;
         const char *Bs = As + G::ABYTES;
 #pragma unroll
         for (int s = 0; s < GL_BK / 16; ++s) {
@@ -574,9 +589,10 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
                 for (int i = 0; i < MT; ++i) acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf, acc[i][b], 0, 0, 0);
             }
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
     }
+    static_assert(S <= 4, "the waits above count at most two chunks ahead");
+    __builtin_amdgcn_s_waitcnt(0xC07F);                        // every wave done reading the last chunk
+    __builtin_amdgcn_s_barrier();
     // the 64-row tiles one after the other through one LDS tile
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -594,6 +610,15 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
         }
     }
     __syncthreads();
+    if (DBG == 1) {
+        for (int row = wave; row < GL_BM; row += 8) {
+            const long g = m0 + row;
+            if (g >= M) break;
+            uint16_t *dst = EPI == 0 ? out : z;
+            reinterpret_cast<uint4 *>(dst)[g * 64 + lane] = *reinterpret_cast<const uint4 *>(smem + gl_tile(row, 8 * lane));
+        }
+        continue;
+    }
     if (EPI == 1) {
         // wave w takes rows w, w + 8, ..., four at a time (ln_rows: their reductions interleaved)
         constexpr int R = 4;
@@ -671,18 +696,38 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     }
 }
 
-// MT row tiles per workgroup (mapf_linear512_select): 2 (80 KiB of LDS, two workgroups per CU), 1, or
-// 0 (default): per kernel as measured (tools/bench_lin_impl.py: residual + LayerNorm 940 -> 917 us
-// at 128 rows, GELU 685 -> 795 us -- slower)
-static int g_lin_mt = 0;
+// MT row tiles per workgroup (mapf_linear512_select): 2 (80 KiB of LDS at S = 2, two workgroups per CU), 1,
+// or 0 (default, per kernel); S ring stages (mapf_linear512_stages): 2, 3, 4 or 0 (default).  Measured
+// (tools/bench_lin_impl.py, profiles/r05_lin_*.jsonl) -- the defaults are the fastest form per kernel.
+static int g_lin_mt = 0, g_lin_stages = 0;
+static int lin_debug() {
+    static const int d = [] { const char *e = getenv("MAPF_LIN_DEBUG"); return e ? atoi(e) : 0; }();
+    return d;
+}
+template <int EPI, int MT, int S, class... Args>
+static void launch_linear512_form(long rows, hipStream_t s, Args... args) {
+    constexpr int lds = GL<MT, S>::LDS;
+    const dim3 grid((unsigned)((rows + MT * GL_BM - 1) / (MT * GL_BM)));
+    if (S == 2 && lin_debug() == 1)
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 1>), grid, dim3(512), lds, s, args...);
+    else if (S == 2 && lin_debug() == 2)
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 2>), grid, dim3(512), lds, s, args...);
+    else
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S>), grid, dim3(512), lds, s, args...);
+}
 template <int EPI, class... Args>
 static void launch_linear512(long rows, hipStream_t s, Args... args) {
-    if (g_lin_mt == 2 || (g_lin_mt == 0 && EPI == 1))
-        hipLaunchKernelGGL((linear512_kernel<EPI, 2>), dim3((unsigned)((rows + 2 * GL_BM - 1) / (2 * GL_BM))), dim3(512),
-                           GL<2>::LDS, s, args...);
-    else
-        hipLaunchKernelGGL((linear512_kernel<EPI, 1>), dim3((unsigned)((rows + GL_BM - 1) / GL_BM)), dim3(512),
-                           GL<1>::LDS, s, args...);
+    const int mt = g_lin_mt ? g_lin_mt : (EPI == 1 ? 2 : 1);
+    const int st = g_lin_stages ? g_lin_stages : 2;
+    if (mt == 2) {
+        if (st == 4) launch_linear512_form<EPI, 2, 4>(rows, s, args...);
+        else if (st == 3) launch_linear512_form<EPI, 2, 3>(rows, s, args...);
+        else launch_linear512_form<EPI, 2, 2>(rows, s, args...);
+    } else {
+        if (st == 4) launch_linear512_form<EPI, 1, 4>(rows, s, args...);
+        else if (st == 3) launch_linear512_form<EPI, 1, 3>(rows, s, args...);
+        else launch_linear512_form<EPI, 1, 2>(rows, s, args...);
+    }
 }
 
 // ---- attention backward (the training forward's attention, transformer.py:48-85) ---------
@@ -900,6 +945,12 @@ int mapf_gelu_dropout_f16(uint16_t *h, int64_t n, float p, uint64_t seed, void *
 int mapf_linear512_select(int32_t row_tiles) {
     if (row_tiles < 0 || row_tiles > 2) return MAPF_EINVAL;
     pol::g_lin_mt = row_tiles;
+    return MAPF_OK;
+}
+
+int mapf_linear512_stages(int32_t stages) {
+    if (stages != 0 && (stages < 2 || stages > 4)) return MAPF_EINVAL;
+    pol::g_lin_stages = stages;
     return MAPF_OK;
 }
 

@@ -493,8 +493,8 @@ def test_training_forward_uses_hip_attention_and_matches_sdpa():
 
 @pytest.mark.parametrize("rows", [1, 64, 127, 129, 1000, 17 * 97])
 def test_linear512_row_tiles_are_bit_identical(rows):
-    """mapf_linear512_select: 128-row workgroups (two 64-row tiles sharing each staged weight chunk,
-    the default) give bit-identical outputs to 64-row workgroups -- the same MFMA sequence per
+    """mapf_linear512_select / _stages: 128-row workgroups (two 64-row tiles sharing each staged weight
+    chunk) and 2-, 3- and 4-stage K rings give bit-identical outputs to 64-row, 2-stage workgroups -- the same MFMA sequence per
     element, the same epilogues -- for the GELU, residual + LayerNorm, rows and tokens variants,
     ragged row counts included (the last workgroup's second tile partly or wholly past M)."""
     from mapf_amd import _lib
@@ -530,13 +530,18 @@ def test_linear512_row_tiles_are_bit_identical(rows):
         torch.cuda.synchronize()
         return out, x1, z1, x2, z2, x3, z3
 
+    forms = {}
     try:
-        _lib.check(L.mapf_linear512_select(2))
-        two = run()
-        _lib.check(L.mapf_linear512_select(1))
-        one = run()
+        for mt in (1, 2):
+            for stages in (2, 3, 4):              # mapf_linear512_stages: the K ring's depth
+                _lib.check(L.mapf_linear512_select(mt))
+                _lib.check(L.mapf_linear512_stages(stages))
+                forms[(mt, stages)] = run()
     finally:
         _lib.check(L.mapf_linear512_select(0))
-    for k, (u, v) in enumerate(zip(two, one)):
-        assert torch.isfinite(u.float()).all(), k
-        assert torch.equal(u, v), k
+        _lib.check(L.mapf_linear512_stages(0))
+    ref = forms[(1, 2)]
+    for form, outs in forms.items():
+        for k, (u, v) in enumerate(zip(outs, ref)):
+            assert torch.isfinite(u.float()).all(), (form, k)
+            assert torch.equal(u, v), (form, k)

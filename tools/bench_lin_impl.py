@@ -1,4 +1,5 @@
-"""A/B the 512 x 512 fused linears' row tiles (mapf_linear512_select 2 vs 1) at the c3 acting
+"""A/B the 512 x 512 fused linears' forms (row tiles: mapf_linear512_select 2 / 1; K-ring stages:
+mapf_linear512_stages 2 / 3 / 4) at the c3 acting
 forward's shape (32,768 agents x 17 tokens = 557,056 rows), interleaved in one process on random
 data.  Prints one JSON line per (round, kernel, row_tiles)."""
 import argparse
@@ -19,6 +20,8 @@ def main():
     ap.add_argument("--rows", type=int, default=32768 * 17)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--stages", default="2,3,4", help="K-ring stages to time")
+    ap.add_argument("--only", default=None, help="comma-separated kernels (default: all)")
     args = ap.parse_args()
     L = _lib.lib()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -32,14 +35,25 @@ def main():
     out = torch.empty(R, 512, dtype=torch.float16, device="cuda")
     x = torch.randn(R, 512, device="cuda", generator=g)
     z = torch.empty(R, 512, dtype=torch.float16, device="cuda")
+    tA = torch.rand(R // 17, 16, device="cuda", generator=g)
+    tVV = torch.randn(R // 17, 512, device="cuda", generator=g).half()
+    tcls, tpos = torch.randn(512, device="cuda", generator=g), torch.randn(17, 512, device="cuda", generator=g)
     kern = {"gelu_dropout": lambda: L.mapf_linear512_gelu_dropout(p(a), p(w), p(b), p(out), R, 0.2, 1, st),
             "residual_layernorm": lambda: L.mapf_linear512_residual_layernorm(p(a), p(w), p(b), p(x), p(gamma), p(beta),
-                                                                               p(z), R, 1e-5, 0.2, 2, st)}
+                                                                               p(z), R, 1e-5, 0.2, 2, st),
+            "rows_x17": lambda: L.mapf_linear512_residual_layernorm_rows(p(a), p(w), p(b), p(x), p(gamma), p(beta), p(z),
+                                                                         R, 1e-5, 0.2, 3, 17, st),
+            "tokens": lambda: L.mapf_linear512_tokens_residual_layernorm(p(a), p(w), p(b), p(x), p(gamma), p(beta), p(z),
+                                                                         R // 17, 16, 1e-5, 0.2, 4, p(tA), p(tVV),
+                                                                         p(tcls), p(tpos), 0.2, 5, st)}
     flop = 2.0 * R * 512 * 512
     for rnd in range(args.rounds):
         for name, fn in kern.items():
-            for mt in (2, 1):
+            if args.only and name not in args.only.split(","):
+                continue
+            for mt, stages in [(m, s_) for m in (2, 1) for s_ in map(int, args.stages.split(","))]:
                 _lib.check(L.mapf_linear512_select(mt))
+                _lib.check(L.mapf_linear512_stages(stages))
                 for _ in range(2):
                     _lib.check(fn())
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,9 +63,10 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / args.iters
-                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "us": round(us, 1),
+                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "stages": stages, "debug": os.environ.get("MAPF_LIN_DEBUG", "0"), "us": round(us, 1),
                                   "pflops": round(flop / us / 1e9, 3)}), flush=True)
     _lib.check(L.mapf_linear512_select(0))
+    _lib.check(L.mapf_linear512_stages(0))
 
 
 if __name__ == "__main__":
