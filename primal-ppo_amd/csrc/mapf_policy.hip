@@ -22,7 +22,6 @@
 // the element index, keyed by `seed`) -- a different stream than torch's own generator; the
 // reference's masks are random anyway (the net is never eval()-ed, net.py:50-51).
 #include <hip/hip_fp16.h>
-#include <cstdlib>
 
 #include "mapf.h"
 #include "mapf_common.h"
@@ -515,7 +514,7 @@ struct TokSrc {
     int x_every;        // > 1: write back only rows g with g % x_every == 0 (token 0 of each sequence)
 };
 
-// DBG (diagnostic forms, MAPF_LIN_DEBUG): 1 = the GEMM with a plain fp16 store as the epilogue, 2 = the
+// DBG (diagnostic builds, -DMAPF_LIN_DEBUG): 1 = the GEMM with a plain fp16 store as the epilogue, 2 = the
 // epilogue without the GEMM (acc = 0)
 template <int EPI, int MT, int S, int DBG = 0>
 __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
@@ -700,10 +699,10 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
 // or 0 (default, per kernel); S ring stages (mapf_linear512_stages): 2, 3, 4 or 0 (default).  Measured
 // (tools/bench_lin_impl.py, profiles/r05_lin_*.jsonl) -- the defaults are the fastest form per kernel.
 static int g_lin_mt = 0, g_lin_stages = 0;
-static int lin_debug() {
-    static const int d = [] { const char *e = getenv("MAPF_LIN_DEBUG"); return e ? atoi(e) : 0; }();
-    return d;
-}
+#ifndef MAPF_LIN_DEBUG
+#define MAPF_LIN_DEBUG 0     // diagnostic builds: make variant V=lindbg1 VFLAGS=-DMAPF_LIN_DEBUG=1
+#endif
+static constexpr int lin_debug() { return MAPF_LIN_DEBUG; }
 template <int EPI, int MT, int S, class... Args>
 static void launch_linear512_form(long rows, hipStream_t s, Args... args) {
     constexpr int lds = GL<MT, S>::LDS;

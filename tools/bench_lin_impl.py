@@ -63,7 +63,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / args.iters
-                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "stages": stages, "debug": os.environ.get("MAPF_LIN_DEBUG", "0"), "us": round(us, 1),
+                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "stages": stages, "lib": os.path.basename(os.environ.get("MAPF_LIB", "libmapf.so")), "us": round(us, 1),
                                   "pflops": round(flop / us / 1e9, 3)}), flush=True)
     _lib.check(L.mapf_linear512_select(0))
     _lib.check(L.mapf_linear512_stages(0))

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Counters of the 512-linear's GEMM core (MAPF_LIN_DEBUG=1: plain fp16 store epilogue), GELU form,
+# Counters of the 512-linear's GEMM core (libmapf_lindbg1.so: plain fp16 store epilogue), GELU form,
 # 2-stage ring, 128- and 64-row workgroups: L2 hit rate, TA busy, SQ waits / MFMA busy.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/${TAG:-r05l}; mkdir -p $OUT
-export MAPF_LIN_DEBUG=${DBG:-1}
+export MAPF_LIB=$ROOT/primal-ppo_amd/lib/libmapf_lindbg${DBG:-1}.so
 pass() {
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
