@@ -382,8 +382,8 @@ int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const fl
                           float eps, uint16_t *z, void *stream);
 /* Row tiles per workgroup of the mapf_linear512_* kernels (process-wide; bit-identical results
  * either way, for A/B timing): 2 (128 rows share each staged 512 x 32 weight chunk), 1 (64 rows),
- * or 0 (default) the faster as measured per kernel: 2 for the residual + LayerNorm forms, 1 for
- * GELU.  MAPF_EINVAL on another value. */
+ * or 0 (default: 1, the faster or within 1 % for every form at the c3 shape, round 5).  MAPF_EINVAL
+ * on another value. */
 int mapf_linear512_select(int32_t row_tiles);
 /* LDS stages of the mapf_linear512_* kernels' K ring (process-wide, bit-identical results): 2, 3, 4
  * (stages - 1 weight/activation chunks in flight) or 0 (default, as measured).  MAPF_EINVAL otherwise. */

@@ -575,19 +575,28 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
         if (c + S - 1 < NCH) issue(c + S - 1, (c + S - 1) % S);
         const char *As = smem + (c % S) * G::BUF;
         const char *Bs = As + G::ABYTES;
+        // every fragment of the chunk read first (the waits then retire them progressively under the
+        // MFMAs; reading each MFMA's operands just before it left the MFMA pipe waiting on LDS latency)
+        constexpr int KS = GL_BK / 16;
+        gh8_t af[KS][MT], bf[KS][4];
 #pragma unroll
-        for (int s = 0; s < GL_BK / 16; ++s) {
+        for (int s = 0; s < KS; ++s) {
             const int qq = 2 * s + fh;
-            gh8_t af[MT];
 #pragma unroll
-            for (int i = 0; i < MT; ++i) af[i] = *reinterpret_cast<const gh8_t *>(As + gl_swz(64 * i + 32 * wm + fr, qq));
+            for (int i = 0; i < MT; ++i) af[s][i] = *reinterpret_cast<const gh8_t *>(As + gl_swz(64 * i + 32 * wm + fr, qq));
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const gh8_t bf = *reinterpret_cast<const gh8_t *>(Bs + gl_swz(128 * wn + 32 * b + fr, qq));
-#pragma unroll
-                for (int i = 0; i < MT; ++i) acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf, acc[i][b], 0, 0, 0);
-            }
+            for (int b = 0; b < 4; ++b) bf[s][b] = *reinterpret_cast<const gh8_t *>(Bs + gl_swz(128 * wn + 32 * b + fr, qq));
         }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][i], bf[s][b], acc[i][b], 0, 0, 0);
+        // pin that order against the scheduler's register-saving interleave (read, wait, MFMA)
+        __builtin_amdgcn_sched_group_barrier(0x100, KS * (MT + 4), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KS * 4 * MT, 0);
     }
     static_assert(S <= 4, "the waits above count at most two chunks ahead");
     __builtin_amdgcn_s_waitcnt(0xC07F);                        // every wave done reading the last chunk
@@ -695,9 +704,11 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     }
 }
 
-// MT row tiles per workgroup (mapf_linear512_select): 2 (80 KiB of LDS at S = 2, two workgroups per CU), 1,
-// or 0 (default, per kernel); S ring stages (mapf_linear512_stages): 2, 3, 4 or 0 (default).  Measured
-// (tools/bench_lin_impl.py, profiles/r05_lin_*.jsonl) -- the defaults are the fastest form per kernel.
+// MT row tiles per workgroup (mapf_linear512_select): 2 (80 KiB of LDS at S = 2), 1, or 0 (default: 1);
+// S ring stages (mapf_linear512_stages): 2, 3, 4 or 0 (default: 2).  Measured at the c3 shape
+// (tools/bench_lin_impl.py, profiles/r05_lin_forms.jsonl): 64-row, 2-stage workgroups -- two per CU --
+// are the fastest or within 1 % for the GELU, rows and tokens forms; deeper rings cost the second
+// workgroup per CU and lose 10-25 %.
 static int g_lin_mt = 0, g_lin_stages = 0;
 #ifndef MAPF_LIN_DEBUG
 #define MAPF_LIN_DEBUG 0     // diagnostic builds: make variant V=lindbg1 VFLAGS=-DMAPF_LIN_DEBUG=1
@@ -716,7 +727,7 @@ static void launch_linear512_form(long rows, hipStream_t s, Args... args) {
 }
 template <int EPI, class... Args>
 static void launch_linear512(long rows, hipStream_t s, Args... args) {
-    const int mt = g_lin_mt ? g_lin_mt : (EPI == 1 ? 2 : 1);
+    const int mt = g_lin_mt ? g_lin_mt : 1;
     const int st = g_lin_stages ? g_lin_stages : 2;
     if (mt == 2) {
         if (st == 4) launch_linear512_form<EPI, 2, 4>(rows, s, args...);
