@@ -751,12 +751,19 @@ static void launch_linear512(long rows, hipStream_t s, Args... args) {
 // K, V, Q, dO staged as fp16 rows in LDS (every lane of a row pass reads the same K / V row:
 // broadcasts), P and dS as fp32 [i][j]; fp16 gradients out.  n <= 32, head_dim 32, 16 heads.
 constexpr int AB_ROW = 64;                                  // bytes per fp16 head row
-constexpr int AB_WAVE = 4 * 32 * AB_ROW + 2 * 32 * 32 * 4;  // Q, dO, K, V + P, dS per wave: 4 waves = 64 KiB
-// P / dS element (i, j) at i * 32 + (j ^ i): the row pass (lanes = i, one j) and the column pass
-// (lanes = j, one i) both hit 32 distinct banks.  (64 KiB: a captured graph's kernel node gets no
-// more dynamic LDS than that unless the function's attribute is raised.)
-__device__ inline int ab_pij(int i, int j) { return i * 32 + (j ^ (i & 31)); }
-static_assert(4 * AB_WAVE <= 65536, "attention_bwd_f16 LDS");
+// One workgroup of ONE wave per (sequence, head group) (round 5: was one workgroup per sequence, four
+// waves looping over four heads each with workgroup barriers between the passes): n <= 20 packs three
+// heads side by side in the wave (21 lanes each: 51 of 64 lanes carry a row instead of 17).  NC = row capacity: 20
+// (n <= 20, the 17-token layers) or 32.  LDS per wave: Q, dO, K, V rows + P, dS in fp32.
+// P / dS element (i, j): NC = 32 at i * 32 + (j ^ i) -- the row pass (lanes = i, one j) and the column
+// pass (lanes = j, one i) both hit distinct banks; NC = 20 at i * 21 + j (odd stride: distinct banks
+// for both passes too).
+template <int NC> struct AB {
+    static constexpr int PS = NC == 32 ? 32 : NC + 1;
+    static constexpr int LDS = 4 * NC * AB_ROW + 2 * NC * PS * 4;
+    static __device__ inline int pij(int i, int j) { return NC == 32 ? i * 32 + (j ^ (i & 31)) : i * PS + j; }
+};
+static_assert(AB<32>::LDS <= 65536 && AB<20>::LDS <= 65536, "attention_bwd_f16 LDS");
 __device__ inline void ab_row_to_f32(const char *src, float *f) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -810,51 +817,56 @@ __device__ inline void ab_store(uint16_t *dst, const float *f, float scale) {
                        f2h(f[8 * c + 6] * scale) | (f2h(f[8 * c + 7] * scale) << 16));
 }
 
-__global__ __launch_bounds__(256) void attention_bwd_f16(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
+template <int NC, int HPW>
+__global__ __launch_bounds__(64) void attention_bwd_f16(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
                                                          const uint16_t *__restrict__ v, const uint16_t *__restrict__ o,
                                                          const uint16_t *__restrict__ dout, uint16_t *__restrict__ dq,
                                                          uint16_t *__restrict__ dk, uint16_t *__restrict__ dv, int n,
                                                          int rows, long q_ts, long q_ss, long kv_ts, long kv_ss,
                                                          long o_ts, long o_ss, float scale) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
+    using G = AB<NC>;
+    constexpr int GLN = 64 / HPW;                          // lanes per head: HPW heads side by side
+    const int lane = (int)threadIdx.x, g = lane / GLN, r = lane - g * GLN;
+    const int h = (int)blockIdx.y * HPW + g;
+    const bool hv = g < HPW && h < 16;                     // lanes past the last head group idle
     const long b = blockIdx.x;
-    char *Qh = smem + wave * AB_WAVE, *dOh = Qh + 32 * AB_ROW, *Kh = dOh + 32 * AB_ROW, *Vh = Kh + 32 * AB_ROW;
-    float *P = reinterpret_cast<float *>(Vh + 32 * AB_ROW), *dS = P + 32 * 32;
-    for (int h = wave; h < 16; h += 4) {
-        if (lane < n) {
-            const uint4 *ks = reinterpret_cast<const uint4 *>(k + b * kv_ss + lane * kv_ts + h * 32);
-            const uint4 *vs = reinterpret_cast<const uint4 *>(v + b * kv_ss + lane * kv_ts + h * 32);
+    char *Qh = smem + (hv ? g : 0) * G::LDS, *dOh = Qh + NC * AB_ROW, *Kh = dOh + NC * AB_ROW, *Vh = Kh + NC * AB_ROW;
+    float *P = reinterpret_cast<float *>(Vh + NC * AB_ROW), *dS = P + NC * G::PS;
+    {
+        if (hv && r < n) {
+            const uint4 *ks = reinterpret_cast<const uint4 *>(k + b * kv_ss + r * kv_ts + h * 32);
+            const uint4 *vs = reinterpret_cast<const uint4 *>(v + b * kv_ss + r * kv_ts + h * 32);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                reinterpret_cast<uint4 *>(Kh + lane * AB_ROW)[c] = ks[c];
-                reinterpret_cast<uint4 *>(Vh + lane * AB_ROW)[c] = vs[c];
+                reinterpret_cast<uint4 *>(Kh + r * AB_ROW)[c] = ks[c];
+                reinterpret_cast<uint4 *>(Vh + r * AB_ROW)[c] = vs[c];
             }
         }
         uint32_t qh[16], gh[16];                           // this row's q and dO, fp16 pairs
         float D = 0.f;
-        if (lane < rows) {
-            ab_load_h(reinterpret_cast<const char *>(q + b * q_ss + lane * q_ts + h * 32), qh);
-            ab_load_h(reinterpret_cast<const char *>(dout + b * o_ss + lane * o_ts + h * 32), gh);
+        if (hv && r < rows) {
+            ab_load_h(reinterpret_cast<const char *>(q + b * q_ss + r * q_ts + h * 32), qh);
+            ab_load_h(reinterpret_cast<const char *>(dout + b * o_ss + r * o_ts + h * 32), gh);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                reinterpret_cast<uint4 *>(Qh + lane * AB_ROW)[c] = make_uint4(qh[4 * c], qh[4 * c + 1], qh[4 * c + 2], qh[4 * c + 3]);
-                reinterpret_cast<uint4 *>(dOh + lane * AB_ROW)[c] = make_uint4(gh[4 * c], gh[4 * c + 1], gh[4 * c + 2], gh[4 * c + 3]);
+                reinterpret_cast<uint4 *>(Qh + r * AB_ROW)[c] = make_uint4(qh[4 * c], qh[4 * c + 1], qh[4 * c + 2], qh[4 * c + 3]);
+                reinterpret_cast<uint4 *>(dOh + r * AB_ROW)[c] = make_uint4(gh[4 * c], gh[4 * c + 1], gh[4 * c + 2], gh[4 * c + 3]);
             }
-            D = ab_dot(gh, reinterpret_cast<const char *>(o + b * o_ss + lane * o_ts + h * 32));
+            D = ab_dot(gh, reinterpret_cast<const char *>(o + b * o_ss + r * o_ts + h * 32));
         }
         __syncthreads();
-        if (lane < rows) {                                 // row pass
-            float sv[32];
+        if (hv && r < rows) {                              // row pass
+            float sv[NC];
             float m = -INFINITY;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
+            for (int j = 0; j < NC; ++j) {
                 sv[j] = j < n ? scale * ab_dot(qh, Kh + j * AB_ROW) : -INFINITY;
                 m = fmaxf(m, sv[j]);
             }
             float l = 0.f;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
+            for (int j = 0; j < NC; ++j) {
                 sv[j] = j < n ? __expf(sv[j] - m) : 0.f;
                 l += sv[j];
             }
@@ -863,28 +875,28 @@ __global__ __launch_bounds__(256) void attention_bwd_f16(const uint16_t *__restr
 #pragma unroll
             for (int d = 0; d < 32; ++d) gq[d] = 0.f;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
+            for (int j = 0; j < NC; ++j) {
                 if (j < n) {
                     const float pj = sv[j] * rl;
                     const float ds = pj * (ab_dot(gh, Vh + j * AB_ROW) - D);
-                    P[ab_pij(lane, j)] = pj;
-                    dS[ab_pij(lane, j)] = ds;
+                    P[G::pij(r, j)] = pj;
+                    dS[G::pij(r, j)] = ds;
                     ab_axpy(gq, ds, Kh + j * AB_ROW);
                 }
             }
-            ab_store(dq + b * q_ss + lane * q_ts + h * 32, gq, scale);
+            ab_store(dq + b * q_ss + r * q_ts + h * 32, gq, scale);
         }
         __syncthreads();
-        if (lane < n) {                                    // column pass
+        if (hv && r < n) {                                 // column pass
             float gk[32], gv[32];
 #pragma unroll
             for (int d = 0; d < 32; ++d) gk[d] = gv[d] = 0.f;
             for (int i = 0; i < rows; ++i) {
-                ab_axpy(gv, P[ab_pij(i, lane)], dOh + i * AB_ROW);
-                ab_axpy(gk, dS[ab_pij(i, lane)], Qh + i * AB_ROW);
+                ab_axpy(gv, P[G::pij(i, r)], dOh + i * AB_ROW);
+                ab_axpy(gk, dS[G::pij(i, r)], Qh + i * AB_ROW);
             }
-            ab_store(dk + b * kv_ss + lane * kv_ts + h * 32, gk, scale);
-            ab_store(dv + b * kv_ss + lane * kv_ts + h * 32, gv, 1.f);
+            ab_store(dk + b * kv_ss + r * kv_ts + h * 32, gk, scale);
+            ab_store(dv + b * kv_ss + r * kv_ts + h * 32, gv, 1.f);
         }
         __syncthreads();
     }
@@ -1070,10 +1082,16 @@ int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t 
           (uintptr_t)dk | (uintptr_t)dv) & 15))
         return MAPF_EINVAL;
     if (B == 0) return MAPF_OK;
-    hipLaunchKernelGGL(pol::attention_bwd_f16, dim3((unsigned)B), dim3(256), 4 * pol::AB_WAVE, (hipStream_t)stream, q,
-                       k, v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride,
-                       (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride, (long)out_seq_stride,
-                       scale);
+    if (n <= 20)        // three heads per wave (21 lanes each), six workgroups per sequence
+        hipLaunchKernelGGL((pol::attention_bwd_f16<20, 3>), dim3((unsigned)B, 6), dim3(64), 3 * pol::AB<20>::LDS,
+                           (hipStream_t)stream, q, k, v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride,
+                           (long)q_seq_stride, (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride,
+                           (long)out_seq_stride, scale);
+    else
+        hipLaunchKernelGGL((pol::attention_bwd_f16<32, 1>), dim3((unsigned)B, 16), dim3(64), pol::AB<32>::LDS,
+                           (hipStream_t)stream, q, k, v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride,
+                           (long)q_seq_stride, (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride,
+                           (long)out_seq_stride, scale);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

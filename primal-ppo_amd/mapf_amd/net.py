@@ -109,6 +109,59 @@ class _HipAttention(torch.autograd.Function):
         return gq, (None if same else gkv), None, None, None, None, None
 
 
+class _SplitKLinear(torch.autograd.Function):
+    """F.linear under fp16 autocast for the TRAINING forward's 17-token layers (34,816 rows at 2,048
+    agents): the forward is autocast's (fp16 operands, one GEMM with the bias), the input gradient
+    one GEMM; the WEIGHT gradient is split over SPLIT row chunks, one batched GEMM with fp32 partial
+    products summed in fp32, then rounded to fp16 as autograd's one-GEMM fp16 weight gradient is
+    (so an fp16 overflow still reaches GradScaler's found-inf).  hipBLASLt's one GEMM has only
+    (out / 64) x (in / 128) output tiles for the 34,816-deep reduction -- 32 tiles on 256 CUs for a
+    512 x 512 weight (tools/profile_update.py)."""
+
+    SPLIT = 4
+    out_dtype_ok = True             # torch.bmm(..., out_dtype=float32) on this build; else fp16 partials
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float16)
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        n_out, n_in = w.shape
+        gy2 = gy.reshape(-1, n_out)
+        x2 = x.reshape(-1, n_in)
+        gx = (gy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        S = _SplitKLinear.SPLIT
+        r = gy2.shape[0] // S
+        a = gy2.view(S, r, n_out).transpose(1, 2)
+        c = x2.view(S, r, n_in)
+        parts = None
+        if _SplitKLinear.out_dtype_ok:
+            try:
+                parts = torch.bmm(a, c, out_dtype=torch.float32)
+            except (NotImplementedError, RuntimeError, TypeError):
+                _SplitKLinear.out_dtype_ok = False
+        if parts is None:
+            parts = torch.bmm(a, c).float()
+        gw = parts.sum(0).to(torch.float16).to(w.dtype)
+        gb = gy2.sum(0) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def _train_linear(x, w, b):
+    """F.linear(x, w, b) of the training forward: the split weight gradient (_SplitKLinear) when x
+    has many rows (grad enabled, on the GPU), plain autocast F.linear otherwise."""
+    rows = x.numel() // x.shape[-1]
+    if (torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda") and rows >= 8192 and
+            rows % _SplitKLinear.SPLIT == 0 and w.requires_grad):
+        return _SplitKLinear.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
 class _SelfAttention(nn.Module):
     """transformer.py:48-85: fused qkv projection, softmax(q k^T / sqrt(dim)) v, output projection.
     Note the reference scales by dim ** -0.5 (the model width), not the head width.
@@ -137,10 +190,10 @@ class _SelfAttention(nn.Module):
     def forward(self, x):
         b, n, d = x.shape
         h = self.heads
-        qkv = self.to_qkv(x)
+        qkv = _train_linear(x, self.to_qkv.weight, self.to_qkv.bias)
         if self._hip(x, qkv):
-            return self.do1(self.nn1(_HipAttention.apply(qkv.contiguous(), qkv.contiguous(), n, 0, d, 2 * d,
-                                                         self.scale)))
+            att = _HipAttention.apply(qkv.contiguous(), qkv.contiguous(), n, 0, d, 2 * d, self.scale)
+            return self.do1(_train_linear(att, self.nn1.weight, self.nn1.bias))
         qkv = qkv.view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
         q, k, v = qkv[0], qkv[1], qkv[2]
         out = F.scaled_dot_product_attention(q, k, v, scale=self.scale).transpose(1, 2).reshape(b, n, d)
@@ -153,7 +206,7 @@ class _SelfAttention(nn.Module):
         w, bias = self.to_qkv.weight, self.to_qkv.bias
         # x[:, 0] is a 2-D strided view: one GEMM with lda = n*d ([b, 1, d] would run as a slow bmm)
         q = F.linear(x[:, 0], w[:d], bias[:d])
-        kv = F.linear(x, w[d:], bias[d:])
+        kv = _train_linear(x, w[d:], bias[d:])
         if self._hip(x, q):
             return self.do1(self.nn1(_HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale)))
         q = q.view(b, 1, h, d // h).transpose(1, 2)                                             # b, h, 1, dh
@@ -178,7 +231,8 @@ class _FeedForward(nn.Module):
         self.do2 = nn.Dropout(dropout)
 
     def forward(self, x):
-        return self.do2(self.nn2(self.do1(self.af1(self.nn1(x)))))
+        h = self.do1(self.af1(_train_linear(x, self.nn1.weight, self.nn1.bias)))
+        return self.do2(_train_linear(h, self.nn2.weight, self.nn2.bias))
 
 
 class _Encoder(nn.Module):

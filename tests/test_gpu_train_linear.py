@@ -1,0 +1,41 @@
+"""The training forward's split weight-gradient linear (net._SplitKLinear, used by _train_linear for
+the 17-token layers): under fp16 autocast its output, input gradient and bias gradient equal plain
+F.linear's (the same GEMMs), and its weight gradient -- eight row chunks, fp32 partial products
+summed in fp32, rounded to fp16 -- matches autograd's one-GEMM fp16 weight gradient to fp16
+rounding (relative 2e-3 in norm, elementwise within a few fp16 ulps of the gradient's scale)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,n_in,n_out", [(34816, 512, 1536), (34816, 512, 512), (8192, 512, 1024)])
+def test_split_weight_gradient_matches_autocast_linear(rows, n_in, n_out):
+    from mapf_amd.net import _SplitKLinear, _train_linear
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(rows + n_out)
+    x0 = torch.randn(rows, n_in, device="cuda", generator=g)
+    w0 = torch.randn(n_out, n_in, device="cuda", generator=g) / n_in ** 0.5
+    b0 = torch.randn(n_out, device="cuda", generator=g) * 0.1
+    gy = torch.randn(rows, n_out, device="cuda", generator=g).half()
+    res = []
+    for split in (True, False):
+        x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        with torch.autocast(device_type="cuda"):
+            y = _train_linear(x, w, b) if split else F.linear(x, w, b)
+        assert y.dtype == torch.float16
+        y.backward(gy)
+        res.append((y.detach(), x.grad, w.grad, b.grad))
+    (ys, gxs, gws, gbs), (yp, gxp, gwp, gbp) = res
+    assert torch.equal(ys, yp)
+    torch.testing.assert_close(gxs, gxp, rtol=0, atol=0)
+    torch.testing.assert_close(gbs, gbp, rtol=1e-3, atol=1e-3)
+    assert gws.dtype == torch.float32 and torch.isfinite(gws).all()
+    rel = ((gws - gwp).norm() / gwp.norm()).item()
+    assert rel < 2e-3, rel
+    scale = gwp.abs().max().item()
+    assert (gws - gwp).abs().max().item() <= 4 * 2 ** -10 * scale
+    print(f"rows {rows} {n_out}x{n_in}: weight-gradient rel diff {rel:.2e}; fp32 partials: "
+          f"{_SplitKLinear.out_dtype_ok}")

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--updates", type=int, default=20)
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--split", type=int, default=None, help="net._SplitKLinear.SPLIT (row chunks)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from mapf_amd.config import EnvParameters, make_config
@@ -28,6 +29,9 @@ def main():
     from mapf_amd.maps import generate_warehouse
     from mapf_amd.model import Model
     from mapf_amd.runner import DeviceRunner
+    if args.split:
+        from mapf_amd.net import _SplitKLinear
+        _SplitKLinear.SPLIT = args.split
     N = args.agents
     EnvParameters.N_AGENTS = N
     EnvParameters.FOV_SIZE = 9
@@ -66,7 +70,7 @@ def main():
         for _ in range(args.updates):
             upd()
         torch.cuda.synchronize()
-    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), flush=True)
+    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=70, max_name_column_width=150), flush=True)
 
 
 if __name__ == "__main__":
