@@ -199,6 +199,97 @@ __global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x
     ln_row(xr[lane], xr[64 + lane], lane, gamma, beta, eps, y + row * 512);
 }
 
+// ---- LayerNorm backward (the training forward's PreNorm, transformer.py:7-24) ------------
+// z = fp16(LayerNorm(x)) is what the next fp16 linear reads under autocast (layernorm_f16); given
+// dz (fp16), with mean / rstd recomputed from x exactly as layernorm_f16 computes them:
+//   xhat = (x - mean) rstd, g = dz gamma,
+//   dx = rstd (g - mean_k(g) - xhat mean_k(g xhat))       (fp32, one wave per row)
+//   dgamma = sum_rows dz xhat, dbeta = sum_rows dz        (per-workgroup partials, then ln_bwd_colsum)
+constexpr int LNB_WG = 512;                                 // partial rows of the gamma / beta gradients
+__global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict__ x, long xstride,
+                                                         const float *__restrict__ gamma,
+                                                         const uint16_t *__restrict__ dz, float *__restrict__ dx,
+                                                         float *__restrict__ part, long rows, float eps) {
+    constexpr int D = 512;
+    __shared__ float red[2][4][D];
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+    const float4 g0 = reinterpret_cast<const float4 *>(gamma)[lane], g1 = reinterpret_cast<const float4 *>(gamma)[64 + lane];
+    const float gm[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    float ag[8], ab[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[k] = ab[k] = 0.f;
+    for (long row = (long)blockIdx.x * 4 + wave; row < rows; row += (long)gridDim.x * 4) {
+        const float4 *xr = reinterpret_cast<const float4 *>(x + row * xstride);
+        const float4 a = xr[lane], c = xr[64 + lane];
+        const uint2 z0 = reinterpret_cast<const uint2 *>(dz + row * D)[lane];
+        const uint2 z1 = reinterpret_cast<const uint2 *>(dz + row * D)[64 + lane];
+        const float dzv[8] = {h2f(z0.x), h2f(z0.x >> 16), h2f(z0.y), h2f(z0.y >> 16),
+                              h2f(z1.x), h2f(z1.x >> 16), h2f(z1.y), h2f(z1.y >> 16)};
+        float sm = a.x + a.y + a.z + a.w + c.x + c.y + c.z + c.w;          // layernorm_f16's order
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) sm += __shfl_xor(sm, st, 64);
+        const float mean = sm * (1.f / D);
+        const float d[8] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean, c.x - mean, c.y - mean, c.z - mean, c.w - mean};
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ss += d[k] * d[k];
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) ss += __shfl_xor(ss, st, 64);
+        const float rstd = 1.f / sqrtf(ss * (1.f / D) + eps);
+        float xh[8], gg[8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            xh[k] = d[k] * rstd;
+            gg[k] = dzv[k] * gm[k];
+            s1 += gg[k];
+            s2 += gg[k] * xh[k];
+            ag[k] += dzv[k] * xh[k];
+            ab[k] += dzv[k];
+        }
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) {
+            s1 += __shfl_xor(s1, st, 64);
+            s2 += __shfl_xor(s2, st, 64);
+        }
+        const float m1 = s1 * (1.f / D), m2 = s2 * (1.f / D);
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (gg[k] - m1 - xh[k] * m2);
+        float4 *dr = reinterpret_cast<float4 *>(dx + row * D);
+        dr[lane] = make_float4(o[0], o[1], o[2], o[3]);
+        dr[64 + lane] = make_float4(o[4], o[5], o[6], o[7]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int col = (k < 4 ? 4 * lane : 256 + 4 * lane) + (k & 3);
+        red[0][wave][col] = ag[k];
+        red[1][wave][col] = ab[k];
+    }
+    __syncthreads();
+    for (int i = (int)threadIdx.x; i < 2 * D; i += 256) {
+        const int w = i / D, col = i - w * D;
+        part[((long)w * gridDim.x + blockIdx.x) * D + col] =
+            (red[w][0][col] + red[w][1][col]) + (red[w][2][col] + red[w][3][col]);
+    }
+}
+
+// column sums of the [2][G][512] partials -> dgamma, dbeta (fixed order: deterministic)
+__global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ part, int G, float *__restrict__ dgamma,
+                                                     float *__restrict__ dbeta) {
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);   // 0 .. 1023
+    if (i >= 1024) return;
+    const int w = i >> 9, col = i & 511;
+    const float *p = part + (long)w * G * 512 + col;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int gi = 0;
+    for (; gi + 4 <= G; gi += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += p[(long)(gi + u) * 512];
+    }
+    for (; gi < G; ++gi) acc[0] += p[(long)gi * 512];
+    (w ? dbeta : dgamma)[col] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
 // ---- dropout epilogues -----------------------------------------------------------
 __device__ inline float4 add_dropped(float4 a, uint2 v, unsigned k, float scale) {
     a.x += (k & 1u) ? h2f(f2h(h2f(v.x) * scale)) : 0.f;
@@ -935,6 +1026,20 @@ int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma,
     if (rows == 0) return MAPF_OK;
     hipLaunchKernelGGL(pol::layernorm_f16, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x,
                        (long)x_row_stride, gamma, beta, y, (long)rows, eps);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz, float *dx,
+                           float *dgamma, float *dbeta, float *work, int64_t rows, int32_t dim, float eps,
+                           void *stream) {
+    if (!x || !gamma || !dz || !dx || !dgamma || !dbeta || !work || rows < 0 || dim != 512 || (x_row_stride & 3) ||
+        (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)dx) & 15) || ((uintptr_t)dz & 7))
+        return MAPF_EINVAL;
+    const int G = (int)(rows < 4 * pol::LNB_WG ? (rows + 3) / 4 : pol::LNB_WG);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x,
+                           (long)x_row_stride, gamma, dz, dx, work, (long)rows, eps);
+    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(4), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

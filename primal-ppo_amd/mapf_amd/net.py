@@ -44,8 +44,50 @@ def _xavier_like(module):
             module.bias.data.fill_(0)
 
 
+class _HipLayerNorm(torch.autograd.Function):
+    """fp16(LayerNorm(x)) of the TRAINING forward under autocast -- what the next fp16 linear reads
+    (autocast runs layer_norm in fp32 and casts at the linear): the forward is mapf_layernorm_f16
+    (the acting path's kernel), the backward mapf_layernorm_bwd_f16 (dx in fp32, dgamma / dbeta
+    summed over the rows).  Replaces torch's LayerNorm forward, its two backward kernels and the
+    fp32 <-> fp16 casts on either side (tools/profile_update.py).  x: fp32 [.., 512]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        from . import _lib
+        x2 = x.reshape(-1, 512)
+        if x2.stride(0) % 4 or x2.stride(1) != 1:
+            x2 = x2.contiguous()
+        rows = x2.shape[0]
+        z = torch.empty(rows, 512, dtype=torch.float16, device=x.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(_lib.lib().mapf_layernorm_f16(ctypes.c_void_p(x2.data_ptr()), x2.stride(0),
+                                                 ctypes.c_void_p(weight.data_ptr()), ctypes.c_void_p(bias.data_ptr()),
+                                                 ctypes.c_void_p(z.data_ptr()), rows, 512, float(eps), st))
+        ctx.save_for_backward(x2, weight)
+        ctx.eps, ctx.shape = float(eps), x.shape
+        return z.view(*x.shape[:-1], 512)
+
+    @staticmethod
+    def backward(ctx, dz):
+        from . import _lib
+        x2, weight = ctx.saved_tensors
+        rows = x2.shape[0]
+        dz = dz.reshape(rows, 512).to(torch.float16).contiguous()
+        dx = torch.empty(rows, 512, dtype=torch.float32, device=dz.device)
+        dg = torch.empty(512, dtype=torch.float32, device=dz.device)
+        db = torch.empty(512, dtype=torch.float32, device=dz.device)
+        work = torch.empty(2 * 512 * 512, dtype=torch.float32, device=dz.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dz.device).cuda_stream)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_layernorm_bwd_f16(p(x2), x2.stride(0), p(weight), p(dz), p(dx), p(dg), p(db),
+                                                     p(work), rows, 512, ctx.eps, st))
+        return dx.view(ctx.shape), dg, db, None
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
+
+    hip_layernorm = True               # the training forward's LayerNorm on _HipLayerNorm (GPU, autocast)
 
     def __init__(self, dim, fn):
         super().__init__()
@@ -53,12 +95,19 @@ class _PreNorm(nn.Module):
         self.fn.norm = nn.LayerNorm(dim)
         self.fn.fn = fn
 
+    def _norm(self, x):
+        n = self.fn.norm
+        if (self.hip_layernorm and x.is_cuda and x.dtype == torch.float32 and x.shape[-1] == 512 and
+                torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and n.elementwise_affine):
+            return _HipLayerNorm.apply(x, n.weight, n.bias, n.eps)
+        return n(x)
+
     def forward(self, x):
-        return self.fn.fn(self.fn.norm(x)) + x
+        return self.fn.fn(self._norm(x)) + x
 
     def forward_first(self, x):
         """Token 0 of forward(x) only (x: [b, n, d] -> [b, 1, d])."""
-        return self.fn.fn.forward_first(self.fn.norm(x)) + x[:, :1]
+        return self.fn.fn.forward_first(self._norm(x)) + x[:, :1]
 
 
 class _HipAttention(torch.autograd.Function):

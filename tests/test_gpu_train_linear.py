@@ -39,3 +39,31 @@ def test_split_weight_gradient_matches_autocast_linear(rows, n_in, n_out):
     assert (gws - gwp).abs().max().item() <= 4 * 2 ** -10 * scale
     print(f"rows {rows} {n_out}x{n_in}: weight-gradient rel diff {rel:.2e}; fp32 partials: "
           f"{_SplitKLinear.out_dtype_ok}")
+
+
+@pytest.mark.parametrize("rows", [34816, 2048, 35, 1])
+def test_hip_layernorm_matches_autocast_layernorm(rows):
+    """net._HipLayerNorm (mapf_layernorm_f16 forward, mapf_layernorm_bwd_f16 backward) against torch's
+    LayerNorm under autocast followed by the fp16 cast the next linear makes: z within one fp16 ulp,
+    dx / dgamma / dbeta to fp32 rounding of the reductions."""
+    from mapf_amd.net import _HipLayerNorm
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    x0 = torch.randn(rows, 512, device="cuda", generator=g) * 2 + 0.5
+    w0 = 1 + 0.1 * torch.randn(512, device="cuda", generator=g)
+    b0 = 0.1 * torch.randn(512, device="cuda", generator=g)
+    dz = torch.randn(rows, 512, device="cuda", generator=g).half()
+    out = []
+    for hip in (True, False):
+        x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        with torch.autocast(device_type="cuda"):
+            z = _HipLayerNorm.apply(x, w, b, 1e-5) if hip else F.layer_norm(x, (512,), w, b, 1e-5).half()
+        assert z.dtype == torch.float16
+        z.backward(dz)
+        out.append((z.detach(), x.grad, w.grad, b.grad))
+    (zh, dxh, dwh, dbh), (zt, dxt, dwt, dbt) = out
+    torch.testing.assert_close(zh.float(), zt.float(), rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(dxh, dxt, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dwh, dwt, rtol=1e-4, atol=1e-3 * max(1.0, rows ** 0.5 / 10))
+    torch.testing.assert_close(dbh, dbt, rtol=1e-4, atol=1e-3 * max(1.0, rows ** 0.5 / 10))
