@@ -273,21 +273,32 @@ __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict
     }
 }
 
-// column sums of the [2][G][512] partials -> dgamma, dbeta (fixed order: deterministic)
+// column sums of the [2][G][512] partials -> dgamma, dbeta (fixed order: deterministic).  A block
+// takes 32 of the 1,024 columns; its 8 x 32 threads sum 8 slices of the G rows (4 chains each), then
+// the 8 slices are added in order.
 __global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ part, int G, float *__restrict__ dgamma,
                                                      float *__restrict__ dbeta) {
-    const int i = (int)(blockIdx.x * 256 + threadIdx.x);   // 0 .. 1023
-    if (i >= 1024) return;
+    __shared__ float sl[8][32];
+    const int t = (int)threadIdx.x, cl = t & 31, slice = t >> 5;
+    const int i = (int)blockIdx.x * 32 + cl;               // 0 .. 1023: [gamma | beta] x 512 columns
     const int w = i >> 9, col = i & 511;
     const float *p = part + (long)w * G * 512 + col;
+    const int per = (G + 7) / 8, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    int gi = 0;
-    for (; gi + 4 <= G; gi += 4) {
+    int gi = g0;
+    for (; gi + 4 <= g1; gi += 4) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc[u] += p[(long)(gi + u) * 512];
     }
-    for (; gi < G; ++gi) acc[0] += p[(long)gi * 512];
-    (w ? dbeta : dgamma)[col] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    for (; gi < g1; ++gi) acc[0] += p[(long)gi * 512];
+    sl[slice][cl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (slice == 0) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v += sl[k][cl];
+        (w ? dbeta : dgamma)[col] = v;
+    }
 }
 
 // ---- dropout epilogues -----------------------------------------------------------
@@ -1039,7 +1050,7 @@ int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *ga
     if (G > 0)
         hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x,
                            (long)x_row_stride, gamma, dz, dx, work, (long)rows, eps);
-    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(4), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
+    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
