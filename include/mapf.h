@@ -366,6 +366,15 @@ int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t 
                               int32_t C, void *stream);
 int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
                        int64_t rows, int32_t dim, float eps, void *stream);
+/* Multi-tensor casts in ONE launch (the training forward's fp16 copies of the fp32 weights under
+ * autocast, and their fp16 gradients back to fp32: one launch each way instead of one per tensor):
+ * dst[i][k] = (fp16) src[i][k] (round to nearest even) or the exact reverse, k < n[i], i < count <= 64.
+ * src / dst / n are HOST arrays of device pointers and element counts (copied into the launch's
+ * arguments; capturable).  MAPF_EINVAL on a bad count or a null pointer with n[i] > 0. */
+int mapf_cast_f32_to_f16_multi(const float *const *src, uint16_t *const *dst, const int64_t *n, int32_t count,
+                               void *stream);
+int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, const int64_t *n, int32_t count,
+                               void *stream);
 /* Backward of z = fp16(LayerNorm(x)) (mapf_layernorm_f16; the training forward's PreNorm,
  * transformer.py:7-24 under autocast): given dz fp16 [rows][512], dx fp32 [rows][512] (contiguous),
  * dgamma / dbeta fp32 [512] (sums over the rows, fixed order).  mean / rstd are recomputed from x as

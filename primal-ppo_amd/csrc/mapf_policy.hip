@@ -301,6 +301,52 @@ __global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ p
     }
 }
 
+// ---- multi-tensor casts (the training forward's fp16 weight copies and their gradients) --
+constexpr int CAST_MAX = 64, CAST_PER_BLOCK = 4096;         // tensors per launch, elements per block
+struct CastList {
+    const void *src[CAST_MAX];
+    void *dst[CAST_MAX];
+    long n[CAST_MAX];
+    int blk0[CAST_MAX + 1];                                 // first block of tensor i; blk0[count] = grid
+    int count;
+};
+template <bool TO_F16>
+__global__ __launch_bounds__(256) void cast_multi(CastList L) {
+    const int b = (int)blockIdx.x;
+    int t = 0;
+    while (t + 1 < L.count && L.blk0[t + 1] <= b) ++t;      // uniform scan over <= 64 entries
+    const long base = (long)(b - L.blk0[t]) * CAST_PER_BLOCK, n = L.n[t];
+    for (int e = (int)threadIdx.x; e < CAST_PER_BLOCK; e += 256) {
+        const long i = base + e;
+        if (i >= n) break;
+        if (TO_F16)
+            static_cast<uint16_t *>(L.dst[t])[i] = (uint16_t)f2h(static_cast<const float *>(L.src[t])[i]);
+        else
+            static_cast<float *>(L.dst[t])[i] = h2f(static_cast<const uint16_t *>(L.src[t])[i]);
+    }
+}
+
+template <bool TO_F16>
+static int cast_multi_api(const void *const *src, void *const *dst, const int64_t *n, int32_t count, void *stream) {
+    if (!src || !dst || !n || count < 0 || count > CAST_MAX) return MAPF_EINVAL;
+    CastList L{};
+    long blocks = 0;
+    for (int i = 0; i < count; ++i) {
+        if (n[i] < 0 || (n[i] > 0 && (!src[i] || !dst[i]))) return MAPF_EINVAL;
+        L.src[i] = src[i];
+        L.dst[i] = dst[i];
+        L.n[i] = (long)n[i];
+        L.blk0[i] = (int)blocks;
+        blocks += (n[i] + CAST_PER_BLOCK - 1) / CAST_PER_BLOCK;
+        if (blocks > (1L << 30)) return MAPF_EINVAL;
+    }
+    L.blk0[count] = (int)blocks;
+    L.count = count;
+    if (blocks == 0) return MAPF_OK;
+    hipLaunchKernelGGL(cast_multi<TO_F16>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
 // ---- dropout epilogues -----------------------------------------------------------
 __device__ inline float4 add_dropped(float4 a, uint2 v, unsigned k, float scale) {
     a.x += (k & 1u) ? h2f(f2h(h2f(v.x) * scale)) : 0.f;
@@ -1038,6 +1084,18 @@ int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma,
     hipLaunchKernelGGL(pol::layernorm_f16, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x,
                        (long)x_row_stride, gamma, beta, y, (long)rows, eps);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_cast_f32_to_f16_multi(const float *const *src, uint16_t *const *dst, const int64_t *n, int32_t count,
+                               void *stream) {
+    return pol::cast_multi_api<true>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst),
+                                     n, count, stream);
+}
+
+int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, const int64_t *n, int32_t count,
+                               void *stream) {
+    return pol::cast_multi_api<false>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst), n,
+                                 count, stream);
 }
 
 int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz, float *dx,

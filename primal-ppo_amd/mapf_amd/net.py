@@ -84,6 +84,56 @@ class _HipLayerNorm(torch.autograd.Function):
         return dx.view(ctx.shape), dg, db, None
 
 
+def _cast_multi(fn, srcs, dsts, stream):
+    from . import _lib
+    k = len(srcs)
+    arr = lambda ts: (ctypes.c_void_p * k)(*[t.data_ptr() for t in ts])  # noqa: E731
+    _lib.check(fn(arr(srcs), arr(dsts), (ctypes.c_int64 * k)(*[t.numel() for t in srcs]), k, stream))
+
+
+class _CastParams(torch.autograd.Function):
+    """fp16 copies of fp32 parameters in ONE launch (mapf_cast_f32_to_f16_multi), their gradients back
+    to fp32 in one (mapf_cast_f16_to_f32_multi): what autocast's per-weight casts and their
+    ToCopyBackward nodes compute (round to nearest even; exact), in 2 launches instead of ~90 per
+    update (tools/profile_update.py)."""
+
+    @staticmethod
+    def dense(t):
+        """storage is exactly the tensor's numel elements (any dense layout: contiguous, channels_last)"""
+        return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+    @staticmethod
+    def forward(ctx, *params):
+        from . import _lib
+        ctx.set_materialize_grads(False)
+        assert all(_CastParams.dense(p) for p in params)
+        ctx.layouts = [(p.shape, p.stride()) for p in params]
+        outs = [torch.empty_strided(p.shape, p.stride(), dtype=torch.float16, device=p.device) for p in params]
+        st = ctypes.c_void_p(torch.cuda.current_stream(params[0].device).cuda_stream)
+        _cast_multi(_lib.lib().mapf_cast_f32_to_f16_multi, params, outs, st)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        from . import _lib
+        live = [i for i, g in enumerate(grads) if g is not None]
+        outs = [None] * len(grads)
+        if live:
+            src, dst = [], []
+            for i in live:
+                shape, stride = ctx.layouts[i]
+                g = grads[i]
+                if g.stride() != stride:        # the parameter's own layout (AccumulateGrad keeps it)
+                    g = torch.empty_strided(shape, stride, dtype=g.dtype, device=g.device).copy_(g)
+                src.append(g)
+                dst.append(torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device))
+            st = ctypes.c_void_p(torch.cuda.current_stream(src[0].device).cuda_stream)
+            _cast_multi(_lib.lib().mapf_cast_f16_to_f32_multi, src, dst, st)
+            for i, d in zip(live, dst):
+                outs[i] = d
+        return tuple(outs)
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
 
@@ -349,6 +399,18 @@ class SCRIMPNet(nn.Module):
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
 
     _OWN_CONV = {(128, 128, 3), (128, 256, 2), (256, 256, 2)}    # (Cin, Cout, kernel) of mapf_conv_nhwc_f16
+    cast_params = True             # training forward: conv / linear weights to fp16 in one launch (_CastParams)
+    _in_cast = False
+
+    def _cast_names(self):
+        """the parameters autocast would cast to fp16 in the training forward: every Conv2d / Linear
+        weight and bias (LayerNorm's stay fp32; token_wA / token_wV are summed in fp32 first)"""
+        names = getattr(self, "_cast_names_cache", None)
+        if names is None:
+            names = [f"{mn}.{pn}" for mn, m in self.named_modules() if isinstance(m, (nn.Conv2d, nn.Linear))
+                     for pn, p in m.named_parameters(recurse=False)]
+            self._cast_names_cache = names
+        return names
 
     def weights_updated(self):
         """Forget the acting path's fp16 weight copies: an update replayed from a captured graph
@@ -361,6 +423,17 @@ class SCRIMPNet(nn.Module):
         when not given at construction).  Acting on the GPU (no grad): _forward_fused."""
         if self.fused_acting and obs.is_cuda and not torch.is_grad_enabled() and self.cT == 512:
             return self._forward_fused(obs, vector)
+        if self.cast_params and obs.is_cuda and torch.is_grad_enabled() and not self._in_cast:
+            # the same forward on fp16 copies of the conv / linear weights, made in one launch
+            # (autocast would cast each weight on use and its ToCopyBackward each gradient)
+            names = self._cast_names()
+            own = dict(self.named_parameters())
+            p16 = _CastParams.apply(*[own[n] for n in names])
+            self._in_cast = True
+            try:
+                return torch.func.functional_call(self, dict(zip(names, p16)), (obs, vector, input_state))
+            finally:
+                self._in_cast = False
         with torch.autocast(device_type=obs.device.type, enabled=obs.device.type == "cuda"):
             n_agents = self.num_agents or EnvParameters.N_AGENTS
             F_ = self.fov or obs.shape[-1]
