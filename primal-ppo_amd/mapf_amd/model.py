@@ -130,6 +130,8 @@ class Model:
         self.network = SCRIMPNet(numChannel=numChannel, num_agents=num_agents, fov=fov).to(self.device)
         if self.device.type == "cuda":     # NHWC convolutions: no layout transposes around MIOpen's kernels
             self.network = self.network.to(memory_format=torch.channels_last)
+            from .gemm_tuning import use_tuned_gemms
+            use_tuned_gemms()              # the measured-best hipBLASLt solution per GEMM shape (gemm_tuning.py)
             # MIOpen find mode: the per-shape conv solver is measured once and cached
             # (c3 policy forward 23.1 -> 20.7 ms at 32,768 agents)
             torch.backends.cudnn.benchmark = True
