@@ -226,7 +226,9 @@ def test_driver_block_verbatim_over_device_runners_c3(n_runners):
             job_results, proxy, ReferenceBatchValues, ReferenceOneEpPerformance, TP)
     torch.cuda.synchronize()
     peak = torch.cuda.max_memory_allocated() - before
-    assert not guard.hits and peak < 2 << 30, (guard.hits, peak)
+    # (3 GiB: the update's own working set is ~1.8 GB, plus ~0.5 GB of hipBLASLt workspace for the
+    # tuned GEMM solutions, mapf_amd/gemm_tuning.py -- a materialised rollout would be 16 GB)
+    assert not guard.hits and peak < 3 << 30, (guard.hits, peak)
     assert steps == n_runners * T and episodes == n_runners
     for k in BATCH_FIELDS:
         v = getattr(mb, k)
