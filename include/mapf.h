@@ -366,6 +366,12 @@ int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t 
                               int32_t C, void *stream);
 int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
                        int64_t rows, int32_t dim, float eps, void *stream);
+/* Backward of y = relu(conv + bias) over NHWC fp16 rows [rows][C] (mapf_nhwc_bias_relu's forward; the
+ * training forward's conv layers): dx = dy where y > 0 else 0 (fp16, [rows][C]), dbias = fp16 of the
+ * fp32 sum of dx over the rows (fixed order).  C % 4 == 0, C <= 1024; work: 512 * C floats of
+ * scratch.  rows == 0 zeroes dbias.  Capturable. */
+int mapf_relu_bias_bwd_f16(const uint16_t *y, const uint16_t *dy, uint16_t *dx, uint16_t *dbias, float *work,
+                           int64_t rows, int32_t C, void *stream);
 /* Multi-tensor casts in ONE launch (the training forward's fp16 copies of the fp32 weights under
  * autocast, and their fp16 gradients back to fp32: one launch each way instead of one per tensor):
  * dst[i][k] = (fp16) src[i][k] (round to nearest even) or the exact reverse, k < n[i], i < count <= 64.

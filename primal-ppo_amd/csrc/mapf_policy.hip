@@ -301,6 +301,69 @@ __global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ p
     }
 }
 
+// ---- bias + ReLU backward (the training forward's conv layers: y = relu(conv(x) + b), NHWC fp16) --
+// dx = dy where y > 0 (torch's threshold_backward on the ReLU output), and per-workgroup partial
+// sums of dx over the rows for the bias gradient (then colsum_to_f16: fixed order).
+constexpr int RB_WG = 512;
+__global__ __launch_bounds__(256) void relu_bias_bwd(const uint16_t *__restrict__ y, const uint16_t *__restrict__ dy,
+                                                     uint16_t *__restrict__ dx, float *__restrict__ part, long rows,
+                                                     int C) {
+    __shared__ float acc_s[256][4];
+    const int c4n = C >> 2;
+    const int per = 256 / c4n;                              // rows per block pass
+    const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tr < per) {
+        for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
+            const uint2 yv = reinterpret_cast<const uint2 *>(y + r * C)[c4];
+            const uint2 gv = reinterpret_cast<const uint2 *>(dy + r * C)[c4];
+            const uint32_t yy[4] = {yv.x & 0xFFFFu, yv.x >> 16, yv.y & 0xFFFFu, yv.y >> 16};
+            const uint32_t gg[4] = {gv.x & 0xFFFFu, gv.x >> 16, gv.y & 0xFFFFu, gv.y >> 16};
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[k] = h2f(yy[k]) > 0.f ? gg[k] : 0u;
+                a[k] += h2f(o[k]);
+            }
+            reinterpret_cast<uint2 *>(dx + r * C)[c4] = pack4(o[0], o[1], o[2], o[3]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc_s[threadIdx.x][k] = a[k];
+    __syncthreads();
+    for (int c = (int)threadIdx.x; c < C; c += 256) {       // channel c: threads (tr, c >> 2), tr in order
+        float v = 0.f;
+        for (int t = 0; t < per; ++t) v += acc_s[t * c4n + (c >> 2)][c & 3];
+        part[(long)blockIdx.x * C + c] = v;
+    }
+}
+
+// out[c] = fp16(sum_g part[g][c]) over G partial rows in a fixed order (8 slices x 4 chains each)
+__global__ __launch_bounds__(256) void colsum_to_f16(const float *__restrict__ part, int G, int C,
+                                                     uint16_t *__restrict__ out) {
+    __shared__ float sl[8][32];
+    const int t = (int)threadIdx.x, cl = t & 31, slice = t >> 5;
+    const int c = (int)blockIdx.x * 32 + cl;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
+        const int per = (G + 7) / 8, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
+        int gi = g0;
+        for (; gi + 4 <= g1; gi += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += part[(long)(gi + u) * C + c];
+        }
+        for (; gi < g1; ++gi) acc[0] += part[(long)gi * C + c];
+    }
+    sl[slice][cl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (slice == 0 && c < C) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v += sl[k][cl];
+        out[c] = (uint16_t)f2h(v);
+    }
+}
+
 // ---- multi-tensor casts (the training forward's fp16 weight copies and their gradients) --
 constexpr int CAST_MAX = 64, CAST_PER_BLOCK = 4096;         // tensors per launch, elements per block
 struct CastList {
@@ -1096,6 +1159,22 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
                                void *stream) {
     return pol::cast_multi_api<false>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst), n,
                                  count, stream);
+}
+
+int mapf_relu_bias_bwd_f16(const uint16_t *y, const uint16_t *dy, uint16_t *dx, uint16_t *dbias, float *work,
+                           int64_t rows, int32_t C, void *stream) {
+    if (!y || !dy || !dx || !dbias || !work || rows < 0 || C <= 0 || (C & 3) || C > 1024 ||
+        (((uintptr_t)y | (uintptr_t)dy | (uintptr_t)dx) & 7))
+        return MAPF_EINVAL;
+    const int per = 256 / (C / 4);
+    const long need = (rows + per - 1) / per;
+    const int G = (int)(need < pol::RB_WG ? need : pol::RB_WG);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::relu_bias_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, y, dy, dx, work,
+                           (long)rows, (int)C);
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+                       (int)C, dbias);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
 int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz, float *dx,

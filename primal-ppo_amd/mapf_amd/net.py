@@ -134,6 +134,41 @@ class _CastParams(torch.autograd.Function):
         return tuple(outs)
 
 
+class _BiasReLU(torch.autograd.Function):
+    """relu(y + b) in place on a convolution's NHWC fp16 output (mapf_nhwc_bias_relu, the acting
+    path's epilogue), for the TRAINING forward's conv layers run without MIOpen's bias; backward
+    mapf_relu_bias_bwd_f16: the ReLU mask and the bias gradient (fp32 sums rounded to fp16, as
+    torch's fp16 sum) in one pass -- in place of MIOpen's bias add, torch's ReLU and threshold
+    backward and its bias-gradient reduction.  y: fp16 channels_last, b: fp16 [C]."""
+
+    @staticmethod
+    def forward(ctx, y, b):
+        from . import _lib
+        C = y.shape[1]
+        rows = y.numel() // C
+        st = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
+        _lib.check(_lib.lib().mapf_nhwc_bias_relu(ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(b.data_ptr()), rows,
+                                                  C, st))
+        ctx.mark_dirty(y)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        y, = ctx.saved_tensors
+        C = y.shape[1]
+        rows = y.numel() // C
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(y)
+        db = torch.empty(C, dtype=torch.float16, device=y.device)
+        work = torch.empty(512 * C, dtype=torch.float32, device=y.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_relu_bias_bwd_f16(p(y), p(dy), p(dx), p(db), p(work), rows, C, st))
+        return dx, db
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
 
@@ -402,6 +437,21 @@ class SCRIMPNet(nn.Module):
     cast_params = True             # training forward: conv / linear weights to fp16 in one launch (_CastParams)
     _in_cast = False
 
+    hip_bias_relu = True           # training forward: conv bias + ReLU on _BiasReLU (GPU, autocast)
+
+    def _conv_relu(self, x, m):
+        """F.relu(m(x)) under autocast; on the GPU with grad, the convolution without its bias and
+        _BiasReLU after it (NHWC fp16)"""
+        if (self.hip_bias_relu and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
+                m.bias is not None and m.out_channels % 4 == 0 and m.out_channels <= 1024 and
+                m.weight.is_contiguous(memory_format=torch.channels_last)):
+            y = F.conv2d(x, m.weight, None, m.stride, m.padding)
+            if y.dtype == torch.float16 and y.is_contiguous(memory_format=torch.channels_last) and y.numel() > 0:
+                b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
+                return _BiasReLU.apply(y, b)
+            return F.relu(y + m.bias)
+        return F.relu(m(x))
+
     def _cast_names(self):
         """the parameters autocast would cast to fp16 in the training forward: every Conv2d / Linear
         weight and bias (LayerNorm's stay fp32; token_wA / token_wV are summed in fp32 first)"""
@@ -441,15 +491,16 @@ class SCRIMPNet(nn.Module):
             if self.conv1.weight.is_contiguous(memory_format=torch.channels_last) and x.is_cuda:
                 x = x.contiguous(memory_format=torch.channels_last)
             v = vector.reshape(-1, NetParameters.VECTOR_LEN)
-            x = F.relu(self.conv1(x))
-            x = F.relu(self.conv1a(x))
-            x = F.relu(self.conv1b(x))
+            cr = self._conv_relu
+            x = cr(x, self.conv1)
+            x = cr(x, self.conv1a)
+            x = cr(x, self.conv1b)
             x = self.pool1(x)
-            x = F.relu(self.conv2(x))
-            x = F.relu(self.conv2a(x))
-            x = F.relu(self.conv2b(x))
+            x = cr(x, self.conv2)
+            x = cr(x, self.conv2a)
+            x = cr(x, self.conv2b)
             x = self.pool2(x)
-            x = F.relu(self.conv3(x).flatten(1))
+            x = cr(x, self.conv3).flatten(1)
             g = F.relu(self.fully_connected_1(v))
             x3 = torch.cat((x, g), -1)
             h = self.fully_connected_3(F.relu(self.fully_connected_2(x3)))

@@ -67,3 +67,50 @@ def test_hip_layernorm_matches_autocast_layernorm(rows):
     torch.testing.assert_close(dxh, dxt, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dwh, dwt, rtol=1e-4, atol=1e-3 * max(1.0, rows ** 0.5 / 10))
     torch.testing.assert_close(dbh, dbt, rtol=1e-4, atol=1e-3 * max(1.0, rows ** 0.5 / 10))
+
+
+@pytest.mark.parametrize("cin,cout,ks,pad,hw", [(128, 128, 3, 1, 9), (128, 256, 2, 1, 4), (256, 500, 3, 0, 3)])
+def test_conv_bias_relu_matches_autocast_conv_relu(cin, cout, ks, pad, hw):
+    """SCRIMPNet._conv_relu's GPU training form (conv without bias, then net._BiasReLU: in-place bias +
+    ReLU, mapf_relu_bias_bwd_f16 backward) against (a) the same arithmetic in torch ops -- fp16 conv,
+    fp32 bias add rounded to fp16, ReLU -- to fp16 tolerance, and (b) F.relu(conv(x)) under autocast
+    (MIOpen adds the bias before rounding, so a few ReLU masks at y ~ 0 differ: 2e-2)."""
+    import torch.nn.functional as F_
+    from mapf_amd.net import SCRIMPNet
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(cout + ks)
+    conv = torch.nn.Conv2d(cin, cout, ks, 1, pad).cuda().to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv.bias.normal_(0, 0.1)
+    x0 = torch.randn(64, cin, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9)
+    forms = {
+        "hip": lambda x: net._conv_relu(x, conv),
+        "same": lambda x: torch.relu((F_.conv2d(x, conv.weight, None, 1, pad).float() +
+                                      conv.bias.half().float().view(-1, 1, 1)).half()),
+        "torch": lambda x: torch.relu(conv(x)),
+    }
+    res = {}
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False   # one MIOpen algorithm
+    try:
+        for name, fn in forms.items():
+            res[name] = _run_form(fn, conv, x0)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    torch.testing.assert_close(res["hip"][0], res["same"][0], rtol=0, atol=0)
+    for ref, tol in (("same", 2e-3), ("torch", 2e-2)):
+        for k, (a, b) in enumerate(zip(res["hip"][1:], res[ref][1:])):
+            rel = ((a - b).norm() / b.norm()).item()
+            assert rel < tol, (ref, k, rel)
+
+
+def _run_form(fn, conv, x0):
+    conv.zero_grad()
+    x = x0.clone().requires_grad_(True)
+    with torch.autocast(device_type="cuda"):
+        y = fn(x)
+    gy = torch.randn(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)).half()
+    y.backward(gy.contiguous(memory_format=torch.channels_last))
+    return y.detach().float(), x.grad.float(), conv.weight.grad.clone(), conv.bias.grad.clone()
