@@ -252,7 +252,7 @@ class _SplitKLinear(torch.autograd.Function):
     (out / 64) x (in / 128) output tiles for the 34,816-deep reduction -- 32 tiles on 256 CUs for a
     512 x 512 weight (tools/profile_update.py)."""
 
-    SPLIT = 4
+    SPLIT = 8
     out_dtype_ok = True             # torch.bmm(..., out_dtype=float32) on this build; else fp16 partials
 
     @staticmethod

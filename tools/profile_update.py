@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--split", type=int, default=None, help="net._SplitKLinear.SPLIT (row chunks)")
+    ap.add_argument("--fp16-partials", action="store_true", help="split weight gradients with fp16 partials")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from mapf_amd.config import EnvParameters, make_config
@@ -29,9 +30,11 @@ def main():
     from mapf_amd.maps import generate_warehouse
     from mapf_amd.model import Model
     from mapf_amd.runner import DeviceRunner
+    from mapf_amd.net import _SplitKLinear
     if args.split:
-        from mapf_amd.net import _SplitKLinear
         _SplitKLinear.SPLIT = args.split
+    if args.fp16_partials:
+        _SplitKLinear.out_dtype_ok = False
     N = args.agents
     EnvParameters.N_AGENTS = N
     EnvParameters.FOV_SIZE = 9
