@@ -366,6 +366,10 @@ int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t 
                               int32_t C, void *stream);
 int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
                        int64_t rows, int32_t dim, float eps, void *stream);
+/* out[c] = fp16 of the fp32 sum over the rows of g fp16 [rows][C] (fixed order): a linear's bias
+ * gradient (the training forward's 17-token linears, net._SplitKLinear).  C % 4 == 0, C <= 4096;
+ * work: 512 * C floats of scratch.  rows == 0 zeroes out.  Capturable. */
+int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows, int32_t C, void *stream);
 /* Backward of y = relu(conv + bias) over NHWC fp16 rows [rows][C] (mapf_nhwc_bias_relu's forward; the
  * training forward's conv layers): dx = dy where y > 0 else 0 (fp16, [rows][C]), dbias = fp16 of the
  * fp32 sum of dx over the rows (fixed order).  C % 4 == 0, C <= 1024; work: 512 * C floats of

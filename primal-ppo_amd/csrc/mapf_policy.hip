@@ -338,6 +338,35 @@ __global__ __launch_bounds__(256) void relu_bias_bwd(const uint16_t *__restrict_
     }
 }
 
+// per-workgroup partial column sums of an fp16 [rows][C] matrix (a linear's bias gradient: the
+// output gradient summed over the rows); blockIdx.y takes 1,024-column chunks (C % 4 == 0)
+__global__ __launch_bounds__(256) void colsum_partial_f16(const uint16_t *__restrict__ g, float *__restrict__ part,
+                                                          long rows, int C) {
+    __shared__ float acc_s[256][4];
+    const int c0 = (int)blockIdx.y * 1024, Cc = C - c0 < 1024 ? C - c0 : 1024;
+    const int c4n = Cc >> 2;
+    const int per = 256 / c4n;
+    const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tr < per) {
+        for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
+            const uint2 v = reinterpret_cast<const uint2 *>(g + r * C + c0)[c4];
+            a[0] += h2f(v.x & 0xFFFFu);
+            a[1] += h2f(v.x >> 16);
+            a[2] += h2f(v.y & 0xFFFFu);
+            a[3] += h2f(v.y >> 16);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc_s[threadIdx.x][k] = a[k];
+    __syncthreads();
+    for (int c = (int)threadIdx.x; c < Cc; c += 256) {
+        float v = 0.f;
+        for (int t = 0; t < per; ++t) v += acc_s[t * c4n + (c >> 2)][c & 3];
+        part[(long)blockIdx.x * C + c0 + c] = v;
+    }
+}
+
 // out[c] = fp16(sum_g part[g][c]) over G partial rows in a fixed order (8 slices x 4 chains each)
 __global__ __launch_bounds__(256) void colsum_to_f16(const float *__restrict__ part, int G, int C,
                                                      uint16_t *__restrict__ out) {
@@ -1159,6 +1188,19 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
                                void *stream) {
     return pol::cast_multi_api<false>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst), n,
                                  count, stream);
+}
+
+int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows, int32_t C, void *stream) {
+    if (!g || !out || !work || rows < 0 || C <= 0 || (C & 3) || C > 4096 || ((uintptr_t)g & 7)) return MAPF_EINVAL;
+    const int per = 256 / ((C < 1024 ? C : 1024) / 4);
+    const long need = (rows + per - 1) / per;
+    const int G = (int)(need < pol::RB_WG ? need : pol::RB_WG);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::colsum_partial_f16, dim3((unsigned)G, (unsigned)((C + 1023) / 1024)), dim3(256), 0,
+                           (hipStream_t)stream, g, work, (long)rows, (int)C);
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+                       (int)C, out);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
 int mapf_relu_bias_bwd_f16(const uint16_t *y, const uint16_t *dy, uint16_t *dx, uint16_t *dbias, float *work,

@@ -259,6 +259,7 @@ class _SplitKLinear(torch.autograd.Function):
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float16)
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
+        ctx.bias_dtype = b.dtype if b is not None else None
         return F.linear(x, w, b)
 
     @staticmethod
@@ -282,7 +283,18 @@ class _SplitKLinear(torch.autograd.Function):
         if parts is None:
             parts = torch.bmm(a, c).float()
         gw = parts.sum(0).to(torch.float16).to(w.dtype)
-        gb = gy2.sum(0) if ctx.needs_input_grad[2] else None
+        gb = None
+        if ctx.needs_input_grad[2] and n_out % 4:
+            gb = gy2.sum(0).to(ctx.bias_dtype)
+        elif ctx.needs_input_grad[2]:   # bias gradient: the column sums of gy (mapf_colsum_f16, fp32 sums -> fp16)
+            from . import _lib
+            gy2 = gy2.contiguous()
+            gb = torch.empty(n_out, dtype=torch.float16, device=gy.device)
+            work = torch.empty(512 * n_out, dtype=torch.float32, device=gy.device)
+            st = ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream)
+            _lib.check(_lib.lib().mapf_colsum_f16(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(gb.data_ptr()),
+                                                  ctypes.c_void_p(work.data_ptr()), gy2.shape[0], n_out, st))
+            gb = gb.to(ctx.bias_dtype)
         return gx, gw, gb
 
 
