@@ -370,6 +370,14 @@ int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma,
  * gradient (the training forward's 17-token linears, net._SplitKLinear).  C % 4 == 0, C <= 4096;
  * work: 512 * C floats of scratch.  rows == 0 zeroes out.  Capturable. */
 int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows, int32_t C, void *stream);
+/* Backward of p = maxpool2x2(relu(fp16(r + bias))) (mapf_nhwc_bias_relu_pool2's forward from the raw
+ * conv output r fp16 NHWC [B][H][W][C]; the training forward's pooled conv layers, net.py:106-111):
+ * dr gets dp at each window's first strictly greatest activation in (row, column) order -- torch's
+ * max_pool2d argmax -- where that activation is > 0; 0 elsewhere, including rows / columns no window
+ * covers.  dbias = fp16 of the fp32 sum of dr over B, H, W.  work: 512 * C floats.  Capturable. */
+int mapf_relu_bias_pool_bwd_f16(const uint16_t *r, const uint16_t *bias, const uint16_t *dp, uint16_t *dr,
+                                uint16_t *dbias, float *work, int32_t B, int32_t H, int32_t W, int32_t C,
+                                void *stream);
 /* Backward of y = relu(conv + bias) over NHWC fp16 rows [rows][C] (mapf_nhwc_bias_relu's forward; the
  * training forward's conv layers): dx = dy where y > 0 else 0 (fp16, [rows][C]), dbias = fp16 of the
  * fp32 sum of dx over the rows (fixed order).  C % 4 == 0, C <= 1024; work: 512 * C floats of

@@ -338,6 +338,89 @@ __global__ __launch_bounds__(256) void relu_bias_bwd(const uint16_t *__restrict_
     }
 }
 
+// backward of p = maxpool2x2(relu(fp16(r + bias))) over NHWC fp16 (the training forward's pooled conv
+// layers; forward nhwc_bias_relu_pool2 from the raw conv output r): per window and channel, the
+// gradient dp goes to the window's first strictly greatest activation in (row, column) order --
+// torch's max_pool2d argmax -- if that activation is > 0 (the ReLU mask); every other position,
+// and the rows / columns no window covers (odd H / W), get 0.  Bias-gradient partial sums per block
+// as relu_bias_bwd.
+__global__ __launch_bounds__(256) void relu_bias_pool_bwd(const uint16_t *__restrict__ r,
+                                                          const uint16_t *__restrict__ bias,
+                                                          const uint16_t *__restrict__ dp, uint16_t *__restrict__ dr,
+                                                          float *__restrict__ part, int B, int H, int W, int C) {
+    __shared__ float acc_s[256][4];
+    const int Ho = H / 2, Wo = W / 2;
+    const int E = H * W - 4 * Ho * Wo;                      // uncovered positions per image
+    const long units = (long)B * Ho * Wo + (long)B * E;
+    const int c4n = C >> 2;
+    const int per = 256 / c4n;
+    const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tr < per) {
+        const uint2 bb = *reinterpret_cast<const uint2 *>(bias + 4 * c4);
+        const float bv[4] = {h2f(bb.x), h2f(bb.x >> 16), h2f(bb.y), h2f(bb.y >> 16)};
+        const long nwin = (long)B * Ho * Wo;
+        for (long u = (long)blockIdx.x * per + tr; u < units; u += (long)gridDim.x * per) {
+            if (u < nwin) {
+                const long b = u / (Ho * Wo);
+                const int rem = (int)(u - b * Ho * Wo), i = rem / Wo, j = rem - i * Wo;
+                const uint2 g = *(reinterpret_cast<const uint2 *>(dp + u * C) + c4);
+                const float gv[4] = {h2f(g.x & 0xFFFFu), h2f(g.x >> 16), h2f(g.y & 0xFFFFu), h2f(g.y >> 16)};
+                float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                int am[4] = {0, 0, 0, 0};
+                long pos[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    pos[w] = ((b * H + 2 * i + (w >> 1)) * (long)W + 2 * j + (w & 1)) * C;
+                    const uint2 v = *(reinterpret_cast<const uint2 *>(r + pos[w]) + c4);
+                    const uint32_t vv[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float act = fmaxf(h2f(f2h(h2f(vv[k]) + bv[k])), 0.f);
+                        if (act > m[k]) {
+                            m[k] = act;
+                            am[k] = w;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    uint32_t o[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const bool hit = am[k] == w && m[k] > 0.f;
+                        o[k] = hit ? (uint32_t)f2h(gv[k]) : 0u;
+                        if (hit) a[k] += gv[k];
+                    }
+                    *(reinterpret_cast<uint2 *>(dr + pos[w]) + c4) = pack4(o[0], o[1], o[2], o[3]);
+                }
+            } else {                                        // an uncovered position: last column, then last row
+                const long e = u - nwin;
+                const long b = e / E;
+                const int k = (int)(e - b * E);
+                const int colE = (W & 1) ? H : 0;
+                int h, w;
+                if (k < colE) {
+                    h = k;
+                    w = W - 1;
+                } else {
+                    h = H - 1;
+                    w = k - colE;
+                }
+                *(reinterpret_cast<uint2 *>(dr + ((b * H + h) * (long)W + w) * C) + c4) = make_uint2(0u, 0u);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc_s[threadIdx.x][k] = a[k];
+    __syncthreads();
+    for (int c = (int)threadIdx.x; c < C; c += 256) {
+        float v = 0.f;
+        for (int t = 0; t < per; ++t) v += acc_s[t * c4n + (c >> 2)][c & 3];
+        part[(long)blockIdx.x * C + c] = v;
+    }
+}
+
 // per-workgroup partial column sums of an fp16 [rows][C] matrix (a linear's bias gradient: the
 // output gradient summed over the rows); blockIdx.y takes 1,024-column chunks (C % 4 == 0)
 __global__ __launch_bounds__(256) void colsum_partial_f16(const uint16_t *__restrict__ g, float *__restrict__ part,
@@ -1200,6 +1283,24 @@ int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows,
                            (hipStream_t)stream, g, work, (long)rows, (int)C);
     hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
                        (int)C, out);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_relu_bias_pool_bwd_f16(const uint16_t *r, const uint16_t *bias, const uint16_t *dp, uint16_t *dr,
+                                uint16_t *dbias, float *work, int32_t B, int32_t H, int32_t W, int32_t C,
+                                void *stream) {
+    if (!r || !bias || !dp || !dr || !dbias || !work || B < 0 || H < 2 || W < 2 || C <= 0 || (C & 3) || C > 1024 ||
+        (((uintptr_t)r | (uintptr_t)dp | (uintptr_t)dr | (uintptr_t)bias) & 7))
+        return MAPF_EINVAL;
+    const int per = 256 / (C / 4);
+    const long units = (long)B * (H / 2) * (W / 2) + (long)B * (H * W - 4 * (H / 2) * (W / 2));
+    const long need = (units + per - 1) / per;
+    const int G = (int)(need < pol::RB_WG ? need : pol::RB_WG);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::relu_bias_pool_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, r, bias, dp,
+                           dr, work, (int)B, (int)H, (int)W, (int)C);
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+                       (int)C, dbias);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

@@ -97,6 +97,7 @@ SIGNATURES = {
     "mapf_nhwc_bias_relu_pool2": (ctypes.c_int, [P, P, P, I32, I32, I32, I32, P]),
     "mapf_layernorm_f16": (ctypes.c_int, [P, I64, P, P, P, I64, I32, ctypes.c_float, P]),
     "mapf_colsum_f16": (ctypes.c_int, [P, P, P, I64, I32, P]),
+    "mapf_relu_bias_pool_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
     "mapf_relu_bias_bwd_f16": (ctypes.c_int, [P, P, P, P, P, I64, I32, P]),
     "mapf_cast_f32_to_f16_multi": (ctypes.c_int, [P, P, P, I32, P]),
     "mapf_cast_f16_to_f32_multi": (ctypes.c_int, [P, P, P, I32, P]),

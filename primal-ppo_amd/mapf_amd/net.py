@@ -169,6 +169,40 @@ class _BiasReLU(torch.autograd.Function):
         return dx, db
 
 
+class _BiasReLUPool(torch.autograd.Function):
+    """maxpool2x2(relu(r + b)) from a convolution's raw NHWC fp16 output r in one pass
+    (mapf_nhwc_bias_relu_pool2, the acting path's epilogue) for the TRAINING forward's pooled layers
+    (conv1b, conv2b; net.py:106-111); backward mapf_relu_bias_pool_bwd_f16: torch's max_pool2d argmax
+    routing, the ReLU mask and the bias gradient in one pass -- in place of the bias + ReLU pass, torch's
+    max-pool forward / backward and the masked-gradient pass."""
+
+    @staticmethod
+    def forward(ctx, r, b):
+        from . import _lib
+        B, C, H, W = r.shape
+        p = torch.empty((B, C, H // 2, W // 2), dtype=torch.float16, device=r.device,
+                        memory_format=torch.channels_last)
+        st = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+        _lib.check(_lib.lib().mapf_nhwc_bias_relu_pool2(ctypes.c_void_p(r.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                                        ctypes.c_void_p(p.data_ptr()), B, H, W, C, st))
+        ctx.save_for_backward(r, b)
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        from . import _lib
+        r, b = ctx.saved_tensors
+        B, C, H, W = r.shape
+        dp = dp.contiguous(memory_format=torch.channels_last)
+        dr = torch.empty_like(r)
+        db = torch.empty(C, dtype=torch.float16, device=r.device)
+        work = torch.empty(512 * C, dtype=torch.float32, device=r.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_relu_bias_pool_bwd_f16(p(r), p(b), p(dp), p(dr), p(db), p(work), B, H, W, C, st))
+        return dr, db
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
 
@@ -461,8 +495,25 @@ class SCRIMPNet(nn.Module):
             if y.dtype == torch.float16 and y.is_contiguous(memory_format=torch.channels_last) and y.numel() > 0:
                 b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
                 return _BiasReLU.apply(y, b)
-            return F.relu(y + m.bias)
+            return F.relu(y + m.bias.view(-1, 1, 1))
         return F.relu(m(x))
+
+    def _conv_relu_pool(self, x, m, pool):
+        """pool(F.relu(m(x))) under autocast; on the GPU with grad and a 2x2 / stride-2 max-pool, the
+        convolution without its bias and _BiasReLUPool after it (NHWC fp16)"""
+        ks = pool.kernel_size if isinstance(pool.kernel_size, int) else None
+        st = pool.stride if isinstance(pool.stride, int) else None
+        if (self.hip_bias_relu and ks == 2 and st == 2 and pool.padding == 0 and pool.dilation == 1 and
+                not pool.ceil_mode and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
+                m.bias is not None and m.out_channels % 4 == 0 and m.out_channels <= 1024 and
+                m.weight.is_contiguous(memory_format=torch.channels_last)):
+            r = F.conv2d(x, m.weight, None, m.stride, m.padding)
+            if (r.dtype == torch.float16 and r.is_contiguous(memory_format=torch.channels_last) and r.numel() > 0 and
+                    r.shape[2] >= 2 and r.shape[3] >= 2):
+                b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
+                return _BiasReLUPool.apply(r, b)
+            return pool(F.relu(r + m.bias.view(-1, 1, 1)))
+        return pool(self._conv_relu(x, m))
 
     def _cast_names(self):
         """the parameters autocast would cast to fp16 in the training forward: every Conv2d / Linear
@@ -506,12 +557,10 @@ class SCRIMPNet(nn.Module):
             cr = self._conv_relu
             x = cr(x, self.conv1)
             x = cr(x, self.conv1a)
-            x = cr(x, self.conv1b)
-            x = self.pool1(x)
+            x = self._conv_relu_pool(x, self.conv1b, self.pool1)
             x = cr(x, self.conv2)
             x = cr(x, self.conv2a)
-            x = cr(x, self.conv2b)
-            x = self.pool2(x)
+            x = self._conv_relu_pool(x, self.conv2b, self.pool2)
             x = cr(x, self.conv3).flatten(1)
             g = F.relu(self.fully_connected_1(v))
             x3 = torch.cat((x, g), -1)

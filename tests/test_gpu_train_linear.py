@@ -114,3 +114,42 @@ def _run_form(fn, conv, x0):
     gy = torch.randn(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)).half()
     y.backward(gy.contiguous(memory_format=torch.channels_last))
     return y.detach().float(), x.grad.float(), conv.weight.grad.clone(), conv.bias.grad.clone()
+
+
+@pytest.mark.parametrize("cin,cout,ks,pad,hw", [(128, 128, 3, 1, 9), (256, 256, 2, 1, 6), (128, 128, 3, 1, 8)])
+def test_conv_bias_relu_pool_matches_autocast(cin, cout, ks, pad, hw):
+    """SCRIMPNet._conv_relu_pool's GPU training form (net._BiasReLUPool: mapf_nhwc_bias_relu_pool2 +
+    mapf_relu_bias_pool_bwd_f16) against the same arithmetic in torch ops (fp16 conv, fp32 bias add
+    rounded to fp16, ReLU, MaxPool2d(2): torch's argmax routing) -- outputs bit-identical, gradients to
+    fp16 tolerance -- and against pool(relu(conv(x))) under autocast (2e-2, see the unpooled test).
+    Odd sizes (9x9, 7x7) leave a row and a column no window covers: their gradient must be 0."""
+    import torch.nn.functional as F_
+    from mapf_amd.net import SCRIMPNet
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(cout + ks + hw)
+    conv = torch.nn.Conv2d(cin, cout, ks, 1, pad).cuda().to(memory_format=torch.channels_last)
+    pool = torch.nn.MaxPool2d(2)
+    with torch.no_grad():
+        conv.bias.normal_(0, 0.1)
+    x0 = torch.randn(64, cin, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9)
+    forms = {
+        "hip": lambda x: net._conv_relu_pool(x, conv, pool),
+        "same": lambda x: pool(torch.relu((F_.conv2d(x, conv.weight, None, 1, pad).float() +
+                                           conv.bias.half().float().view(-1, 1, 1)).half())),
+        "torch": lambda x: pool(torch.relu(conv(x))),
+    }
+    res = {}
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        for name, fn in forms.items():
+            res[name] = _run_form(fn, conv, x0)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    torch.testing.assert_close(res["hip"][0], res["same"][0], rtol=0, atol=0)
+    for ref, tol in (("same", 2e-3), ("torch", 2e-2)):
+        for k, (a, b) in enumerate(zip(res["hip"][1:], res[ref][1:])):
+            rel = ((a - b).norm() / b.norm()).item()
+            assert rel < tol, (ref, k, rel)
