@@ -314,18 +314,32 @@ __global__ __launch_bounds__(256) void relu_bias_bwd(const uint16_t *__restrict_
     const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     if (tr < per) {
-        for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
-            const uint2 yv = reinterpret_cast<const uint2 *>(y + r * C)[c4];
-            const uint2 gv = reinterpret_cast<const uint2 *>(dy + r * C)[c4];
-            const uint32_t yy[4] = {yv.x & 0xFFFFu, yv.x >> 16, yv.y & 0xFFFFu, yv.y >> 16};
-            const uint32_t gg[4] = {gv.x & 0xFFFFu, gv.x >> 16, gv.y & 0xFFFFu, gv.y >> 16};
-            uint32_t o[4];
+        // four rows' loads in flight per step (the loop is latency-bound otherwise); the sums keep
+        // the row order, so results do not depend on the unrolling
+        const long step = (long)gridDim.x * per;
+        constexpr int U = 4;
+        for (long r0 = (long)blockIdx.x * per + tr; r0 < rows; r0 += U * step) {
+            uint2 yv[U], gv[U];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                o[k] = h2f(yy[k]) > 0.f ? gg[k] : 0u;
-                a[k] += h2f(o[k]);
+            for (int q = 0; q < U; ++q) {
+                const long r = r0 + q * step;
+                yv[q] = r < rows ? reinterpret_cast<const uint2 *>(y + r * C)[c4] : make_uint2(0u, 0u);
+                gv[q] = r < rows ? reinterpret_cast<const uint2 *>(dy + r * C)[c4] : make_uint2(0u, 0u);
             }
-            reinterpret_cast<uint2 *>(dx + r * C)[c4] = pack4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                const long r = r0 + q * step;
+                if (r >= rows) break;
+                const uint32_t yy[4] = {yv[q].x & 0xFFFFu, yv[q].x >> 16, yv[q].y & 0xFFFFu, yv[q].y >> 16};
+                const uint32_t gg[4] = {gv[q].x & 0xFFFFu, gv[q].x >> 16, gv[q].y & 0xFFFFu, gv[q].y >> 16};
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    o[k] = h2f(yy[k]) > 0.f ? gg[k] : 0u;
+                    a[k] += h2f(o[k]);
+                }
+                reinterpret_cast<uint2 *>(dx + r * C)[c4] = pack4(o[0], o[1], o[2], o[3]);
+            }
         }
     }
 #pragma unroll
@@ -432,12 +446,22 @@ __global__ __launch_bounds__(256) void colsum_partial_f16(const uint16_t *__rest
     const int tr = (int)threadIdx.x / c4n, c4 = (int)threadIdx.x - tr * c4n;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     if (tr < per) {
-        for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
-            const uint2 v = reinterpret_cast<const uint2 *>(g + r * C + c0)[c4];
-            a[0] += h2f(v.x & 0xFFFFu);
-            a[1] += h2f(v.x >> 16);
-            a[2] += h2f(v.y & 0xFFFFu);
-            a[3] += h2f(v.y >> 16);
+        const long step = (long)gridDim.x * per;
+        constexpr int U = 8;                                // eight rows' loads in flight per step
+        for (long r0 = (long)blockIdx.x * per + tr; r0 < rows; r0 += U * step) {
+            uint2 v[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                const long r = r0 + q * step;
+                v[q] = r < rows ? reinterpret_cast<const uint2 *>(g + r * C + c0)[c4] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int q = 0; q < U; ++q) {               // (zero rows past the end add nothing)
+                a[0] += h2f(v[q].x & 0xFFFFu);
+                a[1] += h2f(v[q].x >> 16);
+                a[2] += h2f(v[q].y & 0xFFFFu);
+                a[3] += h2f(v[q].y >> 16);
+            }
         }
     }
 #pragma unroll
