@@ -396,11 +396,13 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
 /* Backward of z = fp16(LayerNorm(x)) (mapf_layernorm_f16; the training forward's PreNorm,
  * transformer.py:7-24 under autocast): given dz fp16 [rows][512], dx fp32 [rows][512] (contiguous),
  * dgamma / dbeta fp32 [512] (sums over the rows, fixed order).  mean / rstd are recomputed from x as
- * mapf_layernorm_f16 computes them.  work: 2 * 512 * 512 floats of scratch.  rows == 0 zeroes
- * dgamma / dbeta.  No host synchronisation, no memset: capturable. */
-int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz, float *dx,
-                           float *dgamma, float *dbeta, float *work, int64_t rows, int32_t dim, float eps,
-                           void *stream);
+ * mapf_layernorm_f16 computes them.  dres: NULL, or fp32 [rows][512] added to dx -- the gradient the
+ * residual path x + fn(LN(x)) brings to x, so the two need no separate add.  work: 2 * 512 * 512
+ * floats of scratch.  rows == 0 zeroes dgamma / dbeta.  No host synchronisation, no memset:
+ * capturable. */
+int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz,
+                           const float *dres, float *dx, float *dgamma, float *dbeta, float *work, int64_t rows,
+                           int32_t dim, float eps, void *stream);
 int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint64_t seed, void *stream);
 /* mapf_dropout_residual on rows x 512 contiguous x, y, then z = LayerNorm(x) as fp16 (like
  * mapf_layernorm_f16) in one pass; bit-identical to the two calls with the same seed. */

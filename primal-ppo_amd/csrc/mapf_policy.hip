@@ -208,7 +208,8 @@ __global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x
 constexpr int LNB_WG = 512;                                 // partial rows of the gamma / beta gradients
 __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict__ x, long xstride,
                                                          const float *__restrict__ gamma,
-                                                         const uint16_t *__restrict__ dz, float *__restrict__ dx,
+                                                         const uint16_t *__restrict__ dz,
+                                                         const float *__restrict__ dres, float *__restrict__ dx,
                                                          float *__restrict__ part, long rows, float eps) {
     constexpr int D = 512;
     __shared__ float red[2][4][D];
@@ -255,6 +256,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict
         float o[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = rstd * (gg[k] - m1 - xh[k] * m2);
+        if (dres) {                                         // + the residual path's gradient (x + fn(LN(x)))
+            const float4 *rr = reinterpret_cast<const float4 *>(dres + row * D);
+            const float4 r0 = rr[lane], r1 = rr[64 + lane];
+            o[0] += r0.x; o[1] += r0.y; o[2] += r0.z; o[3] += r0.w;
+            o[4] += r1.x; o[5] += r1.y; o[6] += r1.z; o[7] += r1.w;
+        }
         float4 *dr = reinterpret_cast<float4 *>(dx + row * D);
         dr[lane] = make_float4(o[0], o[1], o[2], o[3]);
         dr[64 + lane] = make_float4(o[4], o[5], o[6], o[7]);
@@ -1344,16 +1351,16 @@ int mapf_relu_bias_bwd_f16(const uint16_t *y, const uint16_t *dy, uint16_t *dx, 
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
-int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz, float *dx,
-                           float *dgamma, float *dbeta, float *work, int64_t rows, int32_t dim, float eps,
-                           void *stream) {
+int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz,
+                           const float *dres, float *dx, float *dgamma, float *dbeta, float *work, int64_t rows,
+                           int32_t dim, float eps, void *stream) {
     if (!x || !gamma || !dz || !dx || !dgamma || !dbeta || !work || rows < 0 || dim != 512 || (x_row_stride & 3) ||
-        (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)dx) & 15) || ((uintptr_t)dz & 7))
+        (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)dx | (uintptr_t)dres) & 15) || ((uintptr_t)dz & 7))
         return MAPF_EINVAL;
     const int G = (int)(rows < 4 * pol::LNB_WG ? (rows + 3) / 4 : pol::LNB_WG);
     if (G > 0)
         hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x,
-                           (long)x_row_stride, gamma, dz, dx, work, (long)rows, eps);
+                           (long)x_row_stride, gamma, dz, dres, dx, work, (long)rows, eps);
     hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }

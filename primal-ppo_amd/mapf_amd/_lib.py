@@ -101,7 +101,7 @@ SIGNATURES = {
     "mapf_relu_bias_bwd_f16": (ctypes.c_int, [P, P, P, P, P, I64, I32, P]),
     "mapf_cast_f32_to_f16_multi": (ctypes.c_int, [P, P, P, I32, P]),
     "mapf_cast_f16_to_f32_multi": (ctypes.c_int, [P, P, P, I32, P]),
-    "mapf_layernorm_bwd_f16": (ctypes.c_int, [P, I64, P, P, P, P, P, P, I64, I32, ctypes.c_float, P]),
+    "mapf_layernorm_bwd_f16": (ctypes.c_int, [P, I64, P, P, P, P, P, P, P, I64, I32, ctypes.c_float, P]),
     "mapf_dropout_residual": (ctypes.c_int, [P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_dropout_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, I64, I32, ctypes.c_float, ctypes.c_float,
                                                         ctypes.c_uint64, P]),

@@ -53,7 +53,10 @@ class _HipLayerNorm(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, eps):
+        """returns (z, x viewed): the PreNorm adds the second output back as its residual, so the
+        residual path's gradient arrives in backward and is added to dx by the kernel"""
         from . import _lib
+        ctx.set_materialize_grads(False)
         x2 = x.reshape(-1, 512)
         if x2.stride(0) % 4 or x2.stride(1) != 1:
             x2 = x2.contiguous()
@@ -65,21 +68,26 @@ class _HipLayerNorm(torch.autograd.Function):
                                                  ctypes.c_void_p(z.data_ptr()), rows, 512, float(eps), st))
         ctx.save_for_backward(x2, weight)
         ctx.eps, ctx.shape = float(eps), x.shape
-        return z.view(*x.shape[:-1], 512)
+        return z.view(*x.shape[:-1], 512), x.view_as(x)
 
     @staticmethod
-    def backward(ctx, dz):
+    def backward(ctx, dz, dres):
         from . import _lib
         x2, weight = ctx.saved_tensors
         rows = x2.shape[0]
+        if dz is None:
+            dz = torch.zeros(rows, 512, dtype=torch.float16, device=x2.device)
         dz = dz.reshape(rows, 512).to(torch.float16).contiguous()
+        if dres is not None:
+            dres = dres.reshape(rows, 512).to(torch.float32).contiguous()
         dx = torch.empty(rows, 512, dtype=torch.float32, device=dz.device)
         dg = torch.empty(512, dtype=torch.float32, device=dz.device)
         db = torch.empty(512, dtype=torch.float32, device=dz.device)
         work = torch.empty(2 * 512 * 512, dtype=torch.float32, device=dz.device)
         st = ctypes.c_void_p(torch.cuda.current_stream(dz.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        _lib.check(_lib.lib().mapf_layernorm_bwd_f16(p(x2), x2.stride(0), p(weight), p(dz), p(dx), p(dg), p(db),
+        _lib.check(_lib.lib().mapf_layernorm_bwd_f16(p(x2), x2.stride(0), p(weight), p(dz),
+                                                     None if dres is None else p(dres), p(dx), p(dg), p(db),
                                                      p(work), rows, 512, ctx.eps, st))
         return dx.view(ctx.shape), dg, db, None
 
@@ -215,18 +223,22 @@ class _PreNorm(nn.Module):
         self.fn.fn = fn
 
     def _norm(self, x):
+        """(LayerNorm(x), the residual x): on the GPU training path one _HipLayerNorm whose backward
+        also takes the residual's gradient"""
         n = self.fn.norm
         if (self.hip_layernorm and x.is_cuda and x.dtype == torch.float32 and x.shape[-1] == 512 and
                 torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and n.elementwise_affine):
             return _HipLayerNorm.apply(x, n.weight, n.bias, n.eps)
-        return n(x)
+        return n(x), x
 
     def forward(self, x):
-        return self.fn.fn(self._norm(x)) + x
+        z, res = self._norm(x)
+        return self.fn.fn(z) + res
 
     def forward_first(self, x):
         """Token 0 of forward(x) only (x: [b, n, d] -> [b, 1, d])."""
-        return self.fn.fn.forward_first(self._norm(x)) + x[:, :1]
+        z, res = self._norm(x)
+        return self.fn.fn.forward_first(z) + res[:, :1]
 
 
 class _HipAttention(torch.autograd.Function):

@@ -54,13 +54,18 @@ def test_hip_layernorm_matches_autocast_layernorm(rows):
     w0 = 1 + 0.1 * torch.randn(512, device="cuda", generator=g)
     b0 = 0.1 * torch.randn(512, device="cuda", generator=g)
     dz = torch.randn(rows, 512, device="cuda", generator=g).half()
+    dres = torch.randn(rows, 512, device="cuda", generator=g)
     out = []
     for hip in (True, False):
         x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
         with torch.autocast(device_type="cuda"):
-            z = _HipLayerNorm.apply(x, w, b, 1e-5) if hip else F.layer_norm(x, (512,), w, b, 1e-5).half()
+            if hip:
+                z, res = _HipLayerNorm.apply(x, w, b, 1e-5)
+            else:
+                z, res = F.layer_norm(x, (512,), w, b, 1e-5).half(), x
         assert z.dtype == torch.float16
-        z.backward(dz)
+        # the PreNorm's residual: its gradient (dres) reaches x beside the LayerNorm's
+        torch.autograd.backward([z, res], [dz, dres])
         out.append((z.detach(), x.grad, w.grad, b.grad))
     (zh, dxh, dwh, dbh), (zt, dxt, dwt, dbt) = out
     torch.testing.assert_close(zh.float(), zt.float(), rtol=2e-3, atol=2e-3)
