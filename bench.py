@@ -579,8 +579,15 @@ def main():
             line["note"] = (f"{B * N} agents per GPU: one rollout step is a chain of dependent wave-level "
                             "phases (latency-bound, a few us), so a single CPU thread stepping small "
                             "batches can be faster; the GPU path is for thousands of envs (c2-c5)")
-        if world_size == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(world, H, W, N, F, C, args.cpu_seconds)
+        if not args.no_cpu:
+            # north_star: "1/2/4/8-GPU throughput and the CPU baseline reported in the same run" -- so
+            # every line carries it, multi-rank ones too: rank 0 times it after the timed region and
+            # the final barrier (the other ranks' GPU work is done), on a shorter sample when N > 1
+            secs = args.cpu_seconds if world_size == 1 else min(args.cpu_seconds, 6.0)
+            line["cpu_baseline"] = cpu_baseline(world, H, W, N, F, C, secs)
+            if world_size > 1:
+                line["cpu_baseline"]["timed_on"] = (f"rank 0's host after the {world_size}-rank timed region "
+                                                    f"(other ranks idle), {secs:.0f} s sample")
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

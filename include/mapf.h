@@ -263,9 +263,12 @@ int mapf_rollout_plan(const mapf_env *env, int32_t slots, char *buf, int32_t n);
 int mapf_flush(mapf_env *env, void *stream);
 
 /* Return every argument slot that captured persistent launches of this handle took (16 per
- * handle; a capture past them fails with MAPF_ESTATE and launches nothing).  Call only once every
- * hipGraph holding such a launch of this handle has been destroyed: their replays would read
- * slots that later captures overwrite. */
+ * handle; a capture past them fails with MAPF_ESTATE and launches nothing).  The store of a
+ * launch's argument block is captured with the launch, so every replay re-writes its block
+ * (stream-ordered) before its kernel reads it: a graph captured before the release still replays
+ * right on its own.  What the release allows is a later capture sharing that slot -- replays of the
+ * two graphs must then not overlap in time (two streams at once), or one kernel may read the other's
+ * block.  Safest: call it once the graphs holding this handle's captured launches are destroyed. */
 int mapf_release_captures(mapf_env *env);
 
 /* Uniform random policy (Philox, counter = env clock): DEVICE int32 [B][N]. */

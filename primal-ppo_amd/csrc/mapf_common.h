@@ -179,4 +179,11 @@ struct RegMap {
 };
 __host__ __device__ inline bool regmap_fits(const DevEnv &e) { return e.shared_map && e.Hp * e.WW <= 64; }
 
+// torch's NaN semantics for the network's epilogues (fmaxf would turn a NaN into 0, so a
+// NaN from an fp16 overflow would never reach the loss and GradScaler's found-inf):
+// relu(x) = x <= 0 ? 0 : x  (NaN kept; -0 -> +0), the gradient mask likewise !(y <= 0);
+// max_pool2d's running max: a NaN wins (val > max || isnan(val)).
+__device__ inline float relu_nan(float v) { return (v > 0.f || v != v) ? v : 0.f; }
+__device__ inline float max_nan(float m, float v) { return (v > m || v != v) ? v : m; }
+
 }  // namespace mapf

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm_kernel(const uint16_t *
         for (int r = 0; r < 16; ++r) {
             const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
             float v = h2f(f2h(acc[b][r]));                    // the conv's fp16 output
-            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);        // + bias (fp16), ReLU
+            if (epi) v = relu_nan(h2f(f2h(v + bv)));        // + bias (fp16), ReLU
             const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
             *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
                 (uint16_t)f2h(v);
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
         for (int r = 0; r < 16; ++r) {
             const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
             float v = h2f(f2h(acc[b][r]));
-            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);
+            if (epi) v = relu_nan(h2f(f2h(v + bv)));
             const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
             *reinterpret_cast<uint16_t *>(T + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
                 (uint16_t)f2h(v);
@@ -331,8 +331,8 @@ __global__ __launch_bounds__(64 * WAVES) void conv_igemm32_kernel(const uint16_t
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     const int sh = 16 * hh;
-                    const float m = fmaxf(fmaxf(h2f(w0 >> sh), h2f(w1 >> sh)), fmaxf(h2f(w2 >> sh), h2f(w3 >> sh)));
-                    h2[hh] = f2h(fmaxf(h2f(f2h(m + h2f(bw[e] >> sh))), 0.f));
+                    const float m = max_nan(max_nan(max_nan(h2f(w0 >> sh), h2f(w1 >> sh)), h2f(w2 >> sh)), h2f(w3 >> sh));
+                    h2[hh] = f2h(relu_nan(h2f(f2h(m + h2f(bw[e] >> sh)))));
                 }
                 o[e] = h2[0] | (h2[1] << 16);
             }
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(64 * WAVES) void conv_img_kernel(const uint16_t *__
         for (int e = 0; e < 16; ++e) {
             const int row = wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
             float v = h2f(f2h(acc[b][e]));
-            if (epi) v = fmaxf(h2f(f2h(v + bv)), 0.f);
+            if (epi) v = relu_nan(h2f(f2h(v + bv)));
             const int byte = n * 2, g = byte >> 7, pq = (byte >> 4) & 7;
             *reinterpret_cast<uint16_t *>(Tt + row * RB + g * 128 + ((pq ^ (row & 7)) << 4) + (byte & 15)) =
                 (uint16_t)f2h(v);
@@ -525,8 +525,8 @@ __global__ __launch_bounds__(64 * WAVES) void conv_img_kernel(const uint16_t *__
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     const int sh = 16 * hh;
-                    const float m = fmaxf(fmaxf(h2f(w0 >> sh), h2f(w1 >> sh)), fmaxf(h2f(w2 >> sh), h2f(w3 >> sh)));
-                    h2[hh] = f2h(fmaxf(h2f(f2h(m + h2f(bw[e] >> sh))), 0.f));
+                    const float m = max_nan(max_nan(max_nan(h2f(w0 >> sh), h2f(w1 >> sh)), h2f(w2 >> sh)), h2f(w3 >> sh));
+                    h2[hh] = f2h(relu_nan(h2f(f2h(m + h2f(bw[e] >> sh)))));
                 }
                 o[e] = h2[0] | (h2[1] << 16);
             }
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const float *__restrict
                 const float bv[4] = {h2f(bb.x), h2f(bb.x >> 16), h2f(bb.y), h2f(bb.y >> 16)};
                 uint32_t hv[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) hv[e] = f2h(fmaxf(h2f(f2h(h2f(f2h(acc[i][4 * gq + e])) + bv[e])), 0.f));
+                for (int e = 0; e < 4; ++e) hv[e] = f2h(relu_nan(h2f(f2h(h2f(f2h(acc[i][4 * gq + e])) + bv[e]))));
                 *reinterpret_cast<uint2 *>(out + (size_t)m * COUT + n0) =
                     make_uint2(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16));
             }

@@ -111,7 +111,9 @@ void describe_rollout_wide(const DevEnv &e, int slots, const mapf_tuning &tu, ch
 // slot unless more than ARG_SLOTS are.  A launch recorded into a hipGraph keeps its slot's
 // address for every replay, so captured launches never take a ring slot (a later direct
 // launch would overwrite it between replays): each gets one of ARG_CAPTURE_SLOTS slots of its
-// own for the life of the handle, and a capture past them fails (MAPF_ESTATE).
+// own for the life of the handle, and a capture past them fails (MAPF_ESTATE).  The block's store
+// (store_args_kernel) is captured with the kernel, so each replay re-writes its own slot first;
+// after release_captures a slot may be shared by two graphs, whose replays must not overlap.
 constexpr size_t ARG_SLOT_BYTES = 2048, ARG_SLOTS = 16, ARG_CAPTURE_SLOTS = 16;
 struct ArgRing {
     char *base = nullptr;     // (ARG_SLOTS + ARG_CAPTURE_SLOTS) * ARG_SLOT_BYTES of device memory (the handle's)

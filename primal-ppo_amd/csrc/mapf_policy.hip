@@ -15,7 +15,9 @@
 //   tokens                  x = dropout(cat(cls, A * VV) + pos_embedding)   (net.py:124-131)
 //   tokens_layernorm        tokens + the first block's LayerNorm, one pass
 //   attention_f16           softmax(q k^T * scale) v over the 17 tokens, 16 heads of 32 (MFMA)
-// The training forward keeps PyTorch's ops (autograd needs them).
+// The training forward (autograd) uses the conv epilogues and LayerNorm here too, with their
+// backward kernels below (relu_bias_bwd, relu_bias_pool_bwd, layernorm_bwd_f16, colsum, casts,
+// attention_bwd_f16).  ReLU and max-pool keep torch's NaN semantics (relu_nan / max_nan).
 //
 // Dropout: keep with probability 1 - p, kept values scaled by 1 / (1 - p) (torch's
 // inverted dropout); the mask bits come from a counter hash (keep4: murmur3's finaliser of
@@ -72,8 +74,8 @@ __global__ __launch_bounds__(256) void nhwc_bias_relu(uint16_t *__restrict__ x, 
     for (long r = (long)blockIdx.x * per + tr; r < rows; r += (long)gridDim.x * per) {
         uint2 *p = reinterpret_cast<uint2 *>(x + r * C) + c4;
         const uint2 v = *p;
-        *p = pack4(f2h(fmaxf(h2f(f2h(h2f(v.x) + b0)), 0.f)), f2h(fmaxf(h2f(f2h(h2f(v.x >> 16) + b1)), 0.f)),
-                   f2h(fmaxf(h2f(f2h(h2f(v.y) + b2)), 0.f)), f2h(fmaxf(h2f(f2h(h2f(v.y >> 16) + b3)), 0.f)));
+        *p = pack4(f2h(relu_nan(h2f(f2h(h2f(v.x) + b0)))), f2h(relu_nan(h2f(f2h(h2f(v.x >> 16) + b1)))),
+                   f2h(relu_nan(h2f(f2h(h2f(v.y) + b2)))), f2h(relu_nan(h2f(f2h(h2f(v.y >> 16) + b3)))));
     }
 }
 
@@ -100,14 +102,14 @@ __global__ __launch_bounds__(256) void nhwc_bias_relu_pool2(const uint16_t *__re
             for (int dj = 0; dj < 2; ++dj) {
                 const uint2 v =
                     *(reinterpret_cast<const uint2 *>(x + ((b * H + 2 * i + di) * (long)W + 2 * j + dj) * C) + c4);
-                m[0] = fmaxf(m[0], h2f(v.x));
-                m[1] = fmaxf(m[1], h2f(v.x >> 16));
-                m[2] = fmaxf(m[2], h2f(v.y));
-                m[3] = fmaxf(m[3], h2f(v.y >> 16));
+                m[0] = max_nan(m[0], h2f(v.x));
+                m[1] = max_nan(m[1], h2f(v.x >> 16));
+                m[2] = max_nan(m[2], h2f(v.y));
+                m[3] = max_nan(m[3], h2f(v.y >> 16));
             }
         uint32_t o[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = f2h(fmaxf(h2f(f2h(m[k] + bv[k])), 0.f));
+        for (int k = 0; k < 4; ++k) o[k] = f2h(relu_nan(h2f(f2h(m[k] + bv[k]))));
         *(reinterpret_cast<uint2 *>(out + r * C) + c4) = pack4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(256) void relu_bias_bwd(const uint16_t *__restrict_
                 uint32_t o[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    o[k] = h2f(yy[k]) > 0.f ? gg[k] : 0u;
+                    o[k] = h2f(yy[k]) <= 0.f ? 0u : gg[k];       // threshold_backward: NaN passes
                     a[k] += h2f(o[k]);
                 }
                 reinterpret_cast<uint2 *>(dx + r * C)[c4] = pack4(o[0], o[1], o[2], o[3]);
@@ -397,8 +399,8 @@ __global__ __launch_bounds__(256) void relu_bias_pool_bwd(const uint16_t *__rest
                     const uint32_t vv[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const float act = fmaxf(h2f(f2h(h2f(vv[k]) + bv[k])), 0.f);
-                        if (act > m[k]) {
+                        const float act = relu_nan(h2f(f2h(h2f(vv[k]) + bv[k])));
+                        if (act > m[k] || act != act) {     // torch's argmax: a NaN wins (the last one)
                             m[k] = act;
                             am[k] = w;
                         }
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(256) void relu_bias_pool_bwd(const uint16_t *__rest
                     uint32_t o[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const bool hit = am[k] == w && m[k] > 0.f;
+                        const bool hit = am[k] == w && !(m[k] <= 0.f);
                         o[k] = hit ? (uint32_t)f2h(gv[k]) : 0u;
                         if (hit) a[k] += gv[k];
                     }

@@ -444,11 +444,13 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void r
     rollout_wide_body<T, RW, NT>(args->e, T_steps, args->ro);
 }
 
-// The three-wave form is not built for 128-bit rows spread over two lanes (maps over 64 x 64 cells on
-// both axes): at 168 VGPRs that instantiation spilled 136-188 B per lane to scratch, and
-// such maps carry the BFS channel in the BASELINE configs (c5), which the three-wave form excludes.
+// The three-wave form is not built for 128-bit rows spread over two lanes (maps wider than 64 cells):
+// capped at 168 VGPRs (three waves per SIMD), <Row2,2> spilled 136-188 B per lane to scratch
+// and <Row2,1> 12 B (4-5 scratch instructions, tools/scratch_audit.py).  Such maps take
+// the one- or two-wave form (no BASELINE config is a wide map without the BFS channel, which the
+// three-wave form excludes anyway).
 template <class T, int RW>
-constexpr bool wide3_form() { return !(std::is_same<T, srch::Row2>::value && RW == 2); }
+constexpr bool wide3_form() { return !std::is_same<T, srch::Row2>::value; }
 
 template <class T, int RW>
 static bool wide_fits(const DevEnv &e) { return wide_lds_bytes<T, RW>(e) <= 64 * 1024; }

@@ -506,15 +506,24 @@ def normalize_advantages_distributed(returns, values, cost_returns, cost_values,
     mapf_normalize_advantages_stats.  lam2: the multiplier in device memory instead of
     `lagrange` (float32 [2] = {f32(lagrange), f32(lagrange + 1)}, as normalize_advantages_dlam;
     mapf_normalize_advantages_stats_dlam) -- Model.train's distributed device update."""
+    if returns.device.type != "cuda":
+        raise ValueError("normalize_advantages_distributed: tensors must be on the GPU")
+    if lam2 is not None:
+        _check(lam2, torch.float32, 2, returns.device, "lam2")
+    stats = advantage_stats_distributed(returns, values, cost_returns, cost_values, group=group)
+    return normalize_advantages_with_stats(returns, values, cost_returns, cost_values, stats, lagrange, mix, lam2)
+
+
+def advantage_stats_distributed(returns, values, cost_returns, cost_values, group=None, out=None):
+    """The GLOBAL advantage statistics of normalize_advantages_distributed: float64 [4] = {mean(r - v),
+    mean(cr - cv), unbiased var(r - v), unbiased var(cr - cv)} over every rank's rows (two-pass fp64
+    moments, each pass all-reduced).  out: a float64 [4] device tensor to write them into (the
+    segmented captured update keeps them in a static buffer its graph reads)."""
     import torch.distributed as dist
     dev, M = returns.device, returns.numel()
-    if dev.type != "cuda":
-        raise ValueError("normalize_advantages_distributed: tensors must be on the GPU")
     for name, t in (("returns", returns), ("values", values), ("cost_returns", cost_returns),
                     ("cost_values", cost_values)):
         _check(t, torch.float32, M, dev, name)
-    if lam2 is not None:
-        _check(lam2, torch.float32, 2, dev, "lam2")
     st, L = _stream(dev), _lib.lib()
     ptrs = [_ptr(t) for t in (returns, values, cost_returns, cost_values)]
     buf = torch.zeros(3, dtype=torch.float64, device=dev)          # sum x, sum c, rows
@@ -525,7 +534,26 @@ def normalize_advantages_distributed(returns, values, cost_returns, cost_values,
     q = torch.zeros(2, dtype=torch.float64, device=dev)
     _lib.check(L.mapf_advantage_moments(*ptrs, M, _ptr(mean), _ptr(q), st))
     dist.all_reduce(q, group=group)
-    stats = torch.cat([mean, q / (buf[2] - 1).clamp_min(1)]).contiguous()
+    stats = torch.cat([mean, q / (buf[2] - 1).clamp_min(1)])
+    if out is None:
+        return stats.contiguous()
+    _check(out, torch.float64, 4, dev, "out")
+    return out.copy_(stats)
+
+
+def normalize_advantages_with_stats(returns, values, cost_returns, cost_values, stats, lagrange=0.0, mix=False,
+                                    lam2=None):
+    """model.py:106-113 with given statistics (advantage_stats_distributed's float64 [4]): this rank's
+    rows normalised (mapf_normalize_advantages_stats[_dlam]); no collective, so capturable."""
+    dev, M = returns.device, returns.numel()
+    for name, t in (("returns", returns), ("values", values), ("cost_returns", cost_returns),
+                    ("cost_values", cost_values)):
+        _check(t, torch.float32, M, dev, name)
+    _check(stats, torch.float64, 4, dev, "stats")
+    if lam2 is not None:
+        _check(lam2, torch.float32, 2, dev, "lam2")
+    st, L = _stream(dev), _lib.lib()
+    ptrs = [_ptr(t) for t in (returns, values, cost_returns, cost_values)]
     adv = torch.empty_like(returns)
     cadv = torch.empty_like(returns)
     if lam2 is None:

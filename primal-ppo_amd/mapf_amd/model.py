@@ -124,21 +124,29 @@ def _normalize(x):
 
 
 class Model:
+    # PyTorch TunableOp with the shipped per-shape GEMM solutions (gemm_tuning.py).  PROCESS-WIDE: once a
+    # CUDA Model is built, every later GEMM of the process whose shape is in the file (user code too)
+    # takes the listed hipBLASLt solution.  Set Model.tuned_gemms = False before the first Model to keep
+    # torch's defaults (or set PYTORCH_TUNABLEOP_ENABLED yourself).
+    tuned_gemms = True
+
     def __init__(self, env_id, device, global_model=False, numChannel=None, num_agents=None, fov=None):
         self.ID = env_id
         self.device = torch.device(device)
         self.network = SCRIMPNet(numChannel=numChannel, num_agents=num_agents, fov=fov).to(self.device)
         if self.device.type == "cuda":     # NHWC convolutions: no layout transposes around MIOpen's kernels
             self.network = self.network.to(memory_format=torch.channels_last)
-            from .gemm_tuning import use_tuned_gemms
-            use_tuned_gemms()              # the measured-best hipBLASLt solution per GEMM shape (gemm_tuning.py)
+            if self.tuned_gemms:
+                from .gemm_tuning import use_tuned_gemms
+                use_tuned_gemms()          # the measured-best hipBLASLt solution per GEMM shape (gemm_tuning.py)
             # MIOpen find mode: the per-shape conv solver is measured once and cached
             # (c3 policy forward 23.1 -> 20.7 ms at 32,768 agents)
             torch.backends.cudnn.benchmark = True
         self.num_agents = num_agents or EnvParameters.N_AGENTS
         self._flat = None
         self.fused_loss = True        # GPU: the loss terms + their gradient in one launch (_FusedPPOLoss)
-        self.graph_update = True      # GPU, one rank: the whole update as one captured hipGraph (_DeviceUpdate)
+        self.graph_update = True      # GPU: the update replayed from captured hipGraphs (_DeviceUpdate)
+        self.distributed_update = None  # None: the all-reduced update when world size > 1; True / False: forced
         self._updates = {}
         if global_model:
             # fused Adam on the GPU: one launch for every parameter, and the AMP found-inf skip taken
@@ -224,6 +232,8 @@ class Model:
 
         lam = self.lagrange.get_lagrangian_param()
         distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if self.distributed_update is not None:     # forced (measurement: the c4 path at world size 1)
+            distributed = bool(self.distributed_update) and dist.is_available() and dist.is_initialized()
         if dev.type == "cuda" and self.fused_loss:      # the device update (fused loss, captured graph)
             return self._train_device(observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps,
                                       input_state, train_valid, episode_cost, lam, distributed)
@@ -275,11 +285,13 @@ class Model:
         coefficients in device memory), backward, [RCCL all-reduce of the gradient bucket],
         AMP unscale + found-inf on the device, clip, fused Adam skipping on found-inf, loss-scale
         update -- GradScaler's semantics (init 2^16, x2 every 2000 finite steps, x0.5 on inf).
-        One rank: after two eager updates of a minibatch shape the same body is captured into a
-        hipGraph and every later update of that shape is one replay (the host launched ~1,500
-        small ops per update).  Distributed: eager (the all-reduce sits between backward and
-        unscale, model.py:177-185), the advantages normalised with the global minibatch's
-        statistics.  input_state is ignored, as the network ignores it (net.py:102-155 never
+        After two eager updates of a minibatch shape the body is captured and every later update of
+        that shape replays it (the host launched ~1,500 small ops per update): one hipGraph on one
+        rank; distributed, two graph segments with the collectives between them run eagerly -- the
+        advantage moments' two all-reduces (global statistics) before segment A (normalise ->
+        forward -> loss -> backward into a static gradient bucket), the bucket's all-reduce between
+        backward and unscale (model.py:177-185), segment B (unscale -> clip -> Adam -> scale update),
+        then the stats' all-reduce (_DeviceUpdate.run).  input_state is ignored, as the network ignores it (net.py:102-155 never
         reads it): driver.py passes the rollout's zero hiddenState rows, never None.
         The loss scale and its growth tracker are net_scaler's own tensors (one AMP state per
         model, as the reference's one GradScaler, shared by every minibatch shape and by the
@@ -297,7 +309,7 @@ class Model:
         upd.load(observation, vector, returns, cost_returns, old_v, old_cv, action, old_ps, train_valid,
                  coef=(T.CLIP_RANGE, T.ENTROPY_COEF, T.VALUE_COEF, T.VALID_COEF, T.COST_VALUE_COEF, T.COST_COEF * lam),
                  lam=lam)
-        upd.run(graph=self.graph_update and not distributed, allreduce=distributed)
+        upd.run(graph=self.graph_update, allreduce=distributed)
         # the Lagrangian step (host, model.py:180) depends only on the episode cost
         if distributed:   # every rank must update the multiplier with the same episode cost
             c = torch.tensor([float(episode_cost)], dtype=torch.float64, device=self.device)
@@ -382,7 +394,11 @@ class _DeviceUpdate:
         self.amp = self._amp_settings(sc)
         self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
         self.stats = torch.zeros(11, dtype=torch.float32, device=dev)
-        self.graph = None
+        self.nstats = torch.zeros(4, dtype=torch.float64, device=dev)    # global advantage statistics (distributed)
+        self.grad_params, self.flat = None, None                          # the gradient bucket (distributed)
+        self.live = None
+        self.graph = None                    # one CUDAGraph, or (segment A, segment B) when distributed
+        self.graph_allreduce = False
         self.eager_runs = 0
 
     @staticmethod
@@ -403,14 +419,18 @@ class _DeviceUpdate:
         h = torch.tensor(list(coef) + [lam, lam + 1.0], dtype=torch.float64).float()
         self.dyn.copy_(h.pin_memory() if torch.cuda.is_available() else h, non_blocking=True)
 
-    def body(self, allreduce=False):
-        m, net, opt = self.model, self.model.network, self.model.net_optimizer
+    def _front(self, allreduce):
+        """normalise -> forward -> fused loss -> backward (graph segment A when distributed); with
+        allreduce, the normalisation reads the global statistics in self.nstats (computed and
+        all-reduced by _moments before the segment) and the gradients end in the static bucket"""
+        net, opt = self.model.network, self.model.net_optimizer
         T = TrainingParameters
         opt.zero_grad(set_to_none=True)
-        from .env import normalize_advantages_distributed, normalize_advantages_dlam
+        from .env import normalize_advantages_dlam, normalize_advantages_with_stats
         ins = (self.ret.reshape(-1), self.v.reshape(-1), self.cret.reshape(-1), self.cv.reshape(-1))
         if allreduce:    # model.py:106-113 over the GLOBAL minibatch: moments all-reduced
-            adv, cadv = normalize_advantages_distributed(*ins, mix=T.MINUS_ADV_WITH_CADV, lam2=self.dyn[6:8])
+            adv, cadv = normalize_advantages_with_stats(*ins, self.nstats, mix=T.MINUS_ADV_WITH_CADV,
+                                                        lam2=self.dyn[6:8])
         else:
             adv, cadv = normalize_advantages_dlam(*ins, self.dyn[6:8], T.MINUS_ADV_WITH_CADV)
         adv, cadv = adv.view(self.ret.shape), cadv.view(self.ret.shape)
@@ -419,8 +439,30 @@ class _DeviceUpdate:
         all_loss, terms = _FusedPPOLoss.apply(new_ps, new_v, new_cv, policy_sig, self.old_ps, self.action.unsqueeze(-1),
                                               self.v, self.ret, self.cv, self.cret, adv, cadv, self.tv, self.dyn[:6])
         (all_loss * self.scale).backward()
-        if allreduce:
-            m._allreduce_grads()
+        self.live = (all_loss, terms, adv, cadv)       # read by _back (kept alive: graph A writes them)
+        if allreduce:    # the flattened gradient bucket (model.py:177-185: all-reduced between backward and unscale)
+            gp = [p for p in net.parameters() if p.grad is not None]
+            if self.grad_params is None:
+                self.grad_params = gp
+                self.flat = torch.empty(sum(p.numel() for p in gp), dtype=torch.float32, device=self.model.device)
+            assert len(gp) == len(self.grad_params) and all(a is b for a, b in zip(gp, self.grad_params))
+            # each gradient's elements in memory order (AccumulateGrad lays a dense parameter's gradient out
+            # like the parameter: contiguous or channels_last), so _back's views of the bucket take the
+            # parameter's own strides -- fused Adam wants parameter and gradient alike
+            assert all(p.grad.stride() == p.stride() for p in gp)
+            torch.cat([p.grad.as_strided((p.numel(),), (1,)) for p in gp], out=self.flat)
+
+    def _back(self, allreduce):
+        """[bucket averaged over the ranks] -> unscale + found-inf -> clip -> fused Adam -> loss-scale
+        update -> stats (graph segment B when distributed)"""
+        net, opt = self.model.network, self.model.net_optimizer
+        T = TrainingParameters
+        if allreduce:    # the parameters' gradients become views of the all-reduced bucket (no copy back)
+            self.flat.div_(dist.get_world_size())
+            off = 0
+            for p in self.grad_params:
+                p.grad = self.flat.as_strided(p.shape, p.stride(), off)
+                off += p.numel()
         params = [p for p in net.parameters() if p.grad is not None]
         self.found_inf.zero_()
         torch._amp_foreach_non_finite_check_and_unscale_([p.grad for p in params], self.found_inf,
@@ -430,14 +472,54 @@ class _DeviceUpdate:
         opt.step()
         opt.grad_scale = opt.found_inf = None
         torch._amp_update_scale_(self.scale, self.growth, self.found_inf, *self.amp)
+        all_loss, terms, adv, cadv = self.live
         self.stats.copy_(torch.stack([t.detach().float().reshape(()) for t in (
             all_loss, terms[0], terms[1], terms[2], terms[3], terms[4], terms[5], terms[6], grad_norm,
             torch.mean(adv), torch.mean(cadv))]))
-        if allreduce:    # the loss terms' and advantages' means over the global minibatch (equal shards)
-            dist.all_reduce(self.stats)
-            self.stats.div_(dist.get_world_size())
+
+    def _moments(self):
+        """eager, before segment A: the global advantage statistics (two all-reduced moment passes)"""
+        from .env import advantage_stats_distributed
+        advantage_stats_distributed(self.ret.reshape(-1), self.v.reshape(-1), self.cret.reshape(-1),
+                                    self.cv.reshape(-1), out=self.nstats)
+
+    def _exchange(self):
+        """eager, between the segments: the gradient bucket's all-reduce (RCCL over xGMI)"""
+        dist.all_reduce(self.flat)
+
+    def _exchange_stats(self):
+        """eager, after segment B: the loss terms' and advantages' means over the global minibatch"""
+        dist.all_reduce(self.stats)
+        self.stats.div_(dist.get_world_size())
+
+    def body(self, allreduce=False):
+        """one whole update, eagerly (or captured whole when not distributed)"""
+        if allreduce:
+            self._moments()
+        self._front(allreduce)
+        if allreduce:
+            self._exchange()
+        self._back(allreduce)
+        if allreduce:
+            self._exchange_stats()
+
+    @staticmethod
+    def _capture(fn):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                fn()
+        torch.cuda.current_stream().wait_stream(s)
+        return g
 
     def run(self, graph=True, allreduce=False):
+        """graph: after WARMUP eager updates of this shape, replay captured graphs -- one graph for the
+        whole update on one rank; distributed, two segments (A: normalise -> backward into the static
+        gradient bucket; B: unscale -> clip -> Adam -> scale update -> stats) with the collectives run
+        eagerly around and between them (moments before A, the bucket all-reduce between, the stats
+        after B), so the c4 update replays its ~1,500 small ops too."""
         if graph and self.graph is None and not captured_reductions_ok(self.model.device):
             graph = False                   # the runtime would replay the update wrong: eager
         if not graph or self.eager_runs < self.WARMUP:
@@ -445,19 +527,23 @@ class _DeviceUpdate:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    self.body()
+                    self.body(allreduce=allreduce)
                 torch.cuda.current_stream().wait_stream(s)
             else:
                 self.body(allreduce=allreduce)
             self.eager_runs += 1
             return
         if self.graph is None:
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
-                    self.body()
-            torch.cuda.current_stream().wait_stream(s)
-            self.graph = g
-        self.graph.replay()
+            self.graph = (self._capture(lambda: self._front(True)), self._capture(lambda: self._back(True))) \
+                if allreduce else self._capture(self.body)
+            self.graph_allreduce = allreduce
+        if self.graph_allreduce != allreduce:
+            raise RuntimeError("a minibatch shape's captured update switched between one rank and distributed")
+        if allreduce:
+            self._moments()
+            self.graph[0].replay()
+            self._exchange()
+            self.graph[1].replay()
+            self._exchange_stats()
+        else:
+            self.graph.replay()

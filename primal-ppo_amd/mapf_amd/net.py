@@ -299,7 +299,27 @@ class _SplitKLinear(torch.autograd.Function):
     512 x 512 weight (tools/profile_update.py)."""
 
     SPLIT = 8
-    out_dtype_ok = True             # torch.bmm(..., out_dtype=float32) on this build; else fp16 partials
+    MIN_ROWS = 8192                 # _train_linear takes this form from this many rows on
+    out_dtype_ok = None             # torch.bmm(..., out_dtype=float32) on this build (decided once, _fp32_bmm)
+
+    @staticmethod
+    def _fp32_bmm(a, c):
+        """torch.bmm(a, c, out_dtype=float32), or None when this torch build has no such overload --
+        decided once, by the call's signature error (TypeError / NotImplementedError) only: any other
+        error (an OOM, a launch failure) propagates instead of switching every later gradient to fp16
+        partial products"""
+        if _SplitKLinear.out_dtype_ok is False:
+            return None
+        try:
+            parts = torch.bmm(a, c, out_dtype=torch.float32)
+        except (TypeError, NotImplementedError) as e:
+            import warnings
+            warnings.warn(f"torch.bmm(..., out_dtype=float32) unavailable ({e}): split weight gradients use fp16 "
+                          f"partial products", RuntimeWarning)
+            _SplitKLinear.out_dtype_ok = False
+            return None
+        _SplitKLinear.out_dtype_ok = True
+        return parts
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float16)
@@ -320,12 +340,7 @@ class _SplitKLinear(torch.autograd.Function):
         r = gy2.shape[0] // S
         a = gy2.view(S, r, n_out).transpose(1, 2)
         c = x2.view(S, r, n_in)
-        parts = None
-        if _SplitKLinear.out_dtype_ok:
-            try:
-                parts = torch.bmm(a, c, out_dtype=torch.float32)
-            except (NotImplementedError, RuntimeError, TypeError):
-                _SplitKLinear.out_dtype_ok = False
+        parts = _SplitKLinear._fp32_bmm(a, c)
         if parts is None:
             parts = torch.bmm(a, c).float()
         gw = parts.sum(0).to(torch.float16).to(w.dtype)
@@ -348,8 +363,8 @@ def _train_linear(x, w, b):
     """F.linear(x, w, b) of the training forward: the split weight gradient (_SplitKLinear) when x
     has many rows (grad enabled, on the GPU), plain autocast F.linear otherwise."""
     rows = x.numel() // x.shape[-1]
-    if (torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda") and rows >= 8192 and
-            rows % _SplitKLinear.SPLIT == 0 and w.requires_grad):
+    if (torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda") and
+            rows >= _SplitKLinear.MIN_ROWS and rows % _SplitKLinear.SPLIT == 0 and w.requires_grad):
         return _SplitKLinear.apply(x, w, b)
     return F.linear(x, w, b)
 

@@ -27,12 +27,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIELDS = ["observation", "vector", "returns", "cost_returns", "old_v", "old_cv", "action", "old_ps", "train_valid"]
 
 
-def _batches():
-    z = load("g5_net")
-    out = [{k: z["train_" + k] for k in FIELDS}]
-    g = np.random.default_rng(7)
-    R, N = z["train_returns"].shape
-    for _ in range(2):
+def _batches(R=None, N=None, count=2, seed=7):
+    """g5's reference minibatch (when R, N are not given) then `count` seeded ones of R rows x N agents"""
+    out = []
+    if R is None:
+        z = load("g5_net")
+        out.append({k: z["train_" + k] for k in FIELDS})
+        R, N = z["train_returns"].shape
+    g = np.random.default_rng(seed)
+    for _ in range(count):
         ps = g.random((R, N, 5)).astype(np.float32) + 0.05
         out.append({"observation": (g.random((R, N, 6, 9, 9)) < 0.3).astype(np.float32),
                     "vector": g.normal(size=(R, N, 4)).astype(np.float32),
@@ -48,15 +51,17 @@ def _batches():
 
 def _train(batches, world=1, rank=0, perm=None):
     """Model.train (default device path) over `batches`, this rank's rows; returns the weights
-    after each update and the advantages the normalisation produced."""
+    after each update, the advantages the normalisation produced, the stats, the gradients and the
+    form each update ran in ("eager", "graph", "segments": the distributed captured update)."""
     sys.path[:0] = [ROOT, os.path.join(ROOT, "primal-ppo_amd"), os.path.join(ROOT, "tests")]
     from mapf_amd import env as E
     from mapf_amd.config import EnvParameters
     flags, n_agents = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark), EnvParameters.N_AGENTS
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
-    EnvParameters.N_AGENTS = 2
+    n = batches[0]["returns"].shape[1]
+    EnvParameters.N_AGENTS = n
     seen, saved = [], {}
-    for name in ("normalize_advantages_dlam", "normalize_advantages_distributed"):
+    for name in ("normalize_advantages_dlam", "normalize_advantages_distributed", "normalize_advantages_with_stats"):
         fn = saved[name] = getattr(E, name)
         setattr(E, name, lambda *a, _fn=fn, **k: seen.append(_fn(*a, **k)) or seen[-1])
     try:
@@ -71,16 +76,22 @@ def _train_recorded(batches, world, rank, perm, seen):
     return _train_model(batches, world, rank, perm, seen, [])
 
 
+def _form(m):
+    upd = next(iter(m._updates.values()))
+    return "eager" if upd.graph is None else "segments" if isinstance(upd.graph, tuple) else "graph"
+
+
 def _train_model(batches, world, rank, perm, seen, grads):
     from mapf_amd.model import Model
     from test_net import det_weights
-    m = Model(0, "cuda", global_model=True, numChannel=6, num_agents=2, fov=9)
+    n = batches[0]["returns"].shape[1]
+    m = Model(0, "cuda", global_model=True, numChannel=6, num_agents=n, fov=9)
     m.network.load_state_dict(det_weights(m.network.state_dict()))
     m.network.eval()
     m.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
     assert m.fused_loss
     flat = lambda: torch.cat([p.detach().flatten() for p in m.network.parameters()]).cpu().numpy()  # noqa: E731
-    weights, advs, stats = [flat()], [], []
+    weights, advs, stats, forms = [flat()], [], [], []
     for b in batches:
         rows = np.arange(len(b["returns"]))
         if perm is not None:
@@ -88,8 +99,9 @@ def _train_model(batches, world, rank, perm, seen, grads):
         sl = rows[rank * len(rows) // world:(rank + 1) * len(rows) // world]
         g = lambda k: b[k][sl]  # noqa: E731
         s = m.train(g("observation"), g("vector"), g("returns"), g("cost_returns"), g("old_v"), g("old_cv"),
-                    g("action"), g("old_ps"), np.zeros((len(sl), 2, 2, 512), np.float32), g("train_valid"), 3.0)
+                    g("action"), g("old_ps"), np.zeros((len(sl), n, 2, 512), np.float32), g("train_valid"), 3.0)
         stats.append(np.array([float(np.asarray(x)) for x in s]))
+        forms.append(_form(m))
         # the update's gradient (all-reduced, unscaled, clipped) as the parameters hold it after the step
         grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.network.parameters()
                                 if p.grad is not None]).cpu().numpy())
@@ -97,7 +109,7 @@ def _train_model(batches, world, rank, perm, seen, grads):
         adv, cadv = seen[-1]
         advs.append((adv.detach().cpu().numpy().reshape(len(sl), -1), cadv.detach().cpu().numpy().reshape(len(sl), -1),
                      sl))
-    return weights, advs, stats, grads
+    return weights, advs, stats, grads, forms
 
 
 def _worker(rank, world, port, batches, q):
@@ -107,18 +119,41 @@ def _worker(rank, world, port, batches, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        w, a, s, g = _train(batches, world, rank)
-        q.put((rank, w, [(x, y) for x, y, _ in a], s, g))
+        w, a, s, g, f = _train(batches, world, rank)
+        q.put((rank, w, [(x, y) for x, y, _ in a], s, g, f))
     finally:
         dist.destroy_process_group()
 
 
-def test_model_train_two_ranks_equals_one_process():
+def _collect(q, procs, n, timeout):
+    """n results from the ranks; fails at once (no hang) when a rank exits without one"""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > timeout:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"a rank died or timed out (exit codes {[p.exitcode for p in procs]})")
+        print(f"  rank results so far: {len(out)} of {n}", flush=True)   # (a heartbeat while the ranks run)
+    return out
+
+
+@pytest.mark.parametrize("shape", ["g5", "c4"])
+def test_model_train_two_ranks_equals_one_process(shape):
+    """g5: the reference minibatch (16 rows x 2 agents) + two seeded ones -- two eager warm-ups, then
+    the captured form (one process: one graph; two ranks: the two segments around the collectives).
+    c4: BASELINE c4's update shape (256 rows x 16 agents, 128 per rank), five seeded minibatches --
+    two warm-ups, the capture, two more replays."""
     import torch.multiprocessing as mp
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
-    batches = _batches()
-    w1, a1, s1, g1 = _train(batches)
+    batches = _batches() if shape == "g5" else _batches(256, 16, count=5, seed=11)
+    w1, a1, s1, g1, f1 = _train(batches)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -128,11 +163,14 @@ def test_model_train_two_ranks_equals_one_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, batches, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    res = sorted(_collect(q, procs, 2, 300), key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, w_r0, a_r0, s_r0, g_r0), (_, w_r1, a_r1, s_r1, g_r1) = res
+    (_, w_r0, a_r0, s_r0, g_r0, f_r0), (_, w_r1, a_r1, s_r1, g_r1, f_r1) = res
+    # two eager warm-ups per shape, then the captured update: one graph on one rank, two segments on two
+    assert f1 == ["eager", "eager"] + ["graph"] * (len(batches) - 2), f1
+    assert f_r0 == f_r1 == ["eager", "eager"] + ["segments"] * (len(batches) - 2), f_r0
     lr = 1e-5                                   # TrainingParameters.lr (alg_parameters.py:52)
     for k in range(len(batches)):
         R = len(batches[k]["returns"])

@@ -2,7 +2,7 @@
 capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE=1, the runtime default) a captured hipMemsetAsync takes
 effect on the first replay only, so captured multi-block torch reductions -- their semaphores are
 zeroed by a captured memset -- return stale partial sums from the second replay on
-(tools/diag_graph20.py).  mapf_amd (and tests/conftest.py) switch the mode off before the runtime
+(profiles/r05_diag20_packet_capture_{on,off}.log).  mapf_amd (and tests/conftest.py) switch the mode off before the runtime
 starts; these tests pin that the replays are then right, including the autocast Linear whose
 captured bias gradient went wrong, and that Model falls back to an eager update when a process runs
 with the mode on."""
@@ -75,7 +75,7 @@ def test_captured_memset_replays():
 
 
 def test_captured_autocast_linear_bias_grad_after_churn():
-    """tools/diag_graph18.py's failing case: nn.Linear under fp16 autocast, forward + backward
+    """round 4's failing case: nn.Linear under fp16 autocast, forward + backward
     captured; small NaN tensors allocated and freed between replays; the bias gradient (a captured
     column sum) must equal the eager backward's on every replay."""
     _need_gpu()

@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--minibatch", type=int, default=256, help="rows per PPO minibatch (x N agents)")
     ap.add_argument("--updates", type=int, default=20)
     ap.add_argument("--update-warmup", type=int, default=12)
+    ap.add_argument("--distributed-path", action="store_true",
+                    help="time the update's distributed form (the c4 path: moments all-reduced, two graph segments "
+                         "around the gradient-bucket all-reduce) at this world size -- with one process, a 1-rank "
+                         "RCCL process group")
     ap.add_argument("--reference-maps", action="store_true",
                     help="runner.py:30 semantics: a fresh MapfGym() (random-size warehouse, padded to 40x60) "
                          "per env per rollout, instead of --size")
@@ -38,9 +42,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.distributed_path:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from mapf_amd.config import EnvParameters, make_config
     from mapf_amd.env import BatchedMapfGym
     from mapf_amd.maps import generate_warehouse
@@ -57,6 +66,8 @@ def main():
     new_maps = reference_maps(env, seed=rank) if args.reference_maps else None
     env.reset_seeded(new_maps(0) if new_maps else generate_warehouse(H, H))
     model = Model(0, dev, global_model=True, numChannel=6, num_agents=N, fov=F)   # broadcasts rank 0's weights
+    if args.distributed_path:
+        model.distributed_update = True
     runner = DeviceRunner(env, model, n_steps=args.steps, seed=rank, new_maps=new_maps)
     runner.run()                       # warm-up (kernels, autotuning)
     torch.cuda.synchronize()
@@ -90,13 +101,26 @@ def main():
             each.append(round((time.perf_counter() - t1) * 1e3, 2))
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        upd_obj = next(iter(model._updates.values()))
+        form = ("eager" if upd_obj.graph is None else
+                "two captured segments around the eager collectives" if isinstance(upd_obj.graph, tuple) else
+                "one captured graph")
+        allreduced = world > 1 or args.distributed_path
         if rank == 0:
-            print(json.dumps({"phase": "PPO minibatch update (fwd+bwd+RCCL all-reduce+Adam)", "n_gpus": world,
-                              "ms_per_update": round(dt / args.updates * 1e3, 3),
-                              "ms_median": sorted(each)[len(each) // 2], "ms_each": each, "rows_per_update_per_gpu": rows, "agents": N,
-                              "grad_bytes_allreduced": 4 * sum(p.numel() for p in model.network.parameters())}),
+            phase = ("PPO minibatch update (fwd+bwd+RCCL gradient all-reduce+Adam)" if allreduced else
+                     "PPO minibatch update (fwd+bwd+Adam; one rank: no all-reduce)")
+            print(json.dumps({"phase": phase, "n_gpus": world, "form": form,
+                              "ms_median": float(np.median(each)), "ms_mean": round(dt / args.updates * 1e3, 3),
+                              "updates_timed": args.updates, "ms_each": each,
+                              "timing": "wall time per Model.train call (it returns host stats: one sync per update) "
+                                        "through driver.py:125-130's call shape (host index array into the "
+                                        "DeviceRunner's BatchValues), after --update-warmup updates",
+                              "rows_per_update_per_gpu": rows, "agents": N,
+                              "collectives": (f"RCCL, world size {world}" if allreduced else None),
+                              "grad_bytes_allreduced": (4 * sum(p.numel() for p in model.network.parameters())
+                                                        if allreduced else 0)}),
                   flush=True)
-    if world > 1:
+    if world > 1 or args.distributed_path:
         torch.distributed.destroy_process_group()
 
 
