@@ -428,6 +428,10 @@ int mapf_linear512_select(int32_t row_tiles);
 /* LDS stages of the mapf_linear512_* kernels' K ring (process-wide, bit-identical results): 2, 3, 4
  * (stages - 1 weight/activation chunks in flight) or 0 (default, as measured).  MAPF_EINVAL otherwise. */
 int mapf_linear512_stages(int32_t stages);
+/* K per staged chunk of the mapf_linear512_* kernels (process-wide, bit-identical results: the same
+ * MFMA sequence per element): 32 (64-B half-line LDS rows), 64 (full 128-B lines, two stages; with 2
+ * row tiles all 160 KiB of a CU's LDS) or 0 (default: 32).  MAPF_EINVAL otherwise. */
+int mapf_linear512_kdepth(int32_t k);
 
 /* 512 x 512 Linear (w: fp16 [512 out][512 in], torch's layout; bias fp16 [512]) on `rows` contiguous fp16
  * rows a[rows][512] with its epilogue, one launch (MFMA GEMM; the linear's fp16 output stays on chip):

@@ -831,23 +831,39 @@ inline int grid_for(long items, int per_block) {
 // elementwise epilogue (ln_row).
 typedef _Float16 gh8_t __attribute__((ext_vector_type(8)));
 typedef float gf16_t __attribute__((ext_vector_type(16)));
-constexpr int GL_BM = 64, GL_BK = 32, GL_D = 512;
+constexpr int GL_BM = 64, GL_D = 512;
 // MT = 64-row tiles per workgroup sharing each staged W chunk (round 5: MT = 2 halves the W bytes
 // per row -- 32 KiB of W per 32-deep chunk were 8 of every 9 bytes the kernel DMA'd at MT = 1)
 // S = LDS stages of the K ring (round 5): S - 1 chunks in flight when a chunk is waited for, one
 // raw s_barrier per chunk (S = 2: one in flight -- two workgroups per CU at MT = 1; S = 3, 4: one
 // workgroup per CU whose DMA latency the ring itself covers)
-template <int MT, int S = 2>
+// BK = K per chunk (round 6): 32 (64-B LDS rows: a DMA instruction fills 16 rows x 64 B, half-line
+// fragments), or 64 -- full 128-B lines, 8 rows per DMA instruction, half the barriers; with MT = 2
+// and S = 2 that is 2 x (16 + 64) KiB = all 160 KiB of the CU's LDS (one workgroup per CU)
+template <int MT, int S = 2, int BK = 32>
 struct GL {
-    static constexpr int ABYTES = MT * GL_BM * GL_BK * 2, BBYTES = GL_D * GL_BK * 2, BUF = ABYTES + BBYTES;
+    static constexpr int ABYTES = MT * GL_BM * BK * 2, BBYTES = GL_D * BK * 2, BUF = ABYTES + BBYTES;
     static constexpr int LDS = S * BUF;
+    static constexpr int ROWB = BK * 2;                       // LDS bytes per staged row
+    static constexpr int RPI = 1024 / ROWB;                   // rows one DMA instruction fills (64 lanes x 16 B)
+    static_assert(BK == 32 || BK == 64, "chunk depth");
     static_assert(GL_BM * GL_D * 2 <= LDS, "epilogue tile");
     static_assert(LDS <= 163840, "LDS per workgroup");
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_lin_zero[1];    // source of the rows past M
 
-__device__ inline int gl_swz(int r, int q) { return r * 64 + ((q ^ ((r >> 2) & 3)) << 4); }
+// s_waitcnt immediate: vmcnt(n) (6 bits: [3:0] and [15:14]) and lgkmcnt(0), expcnt unconstrained
+constexpr int vm_lgkm0(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0070; }
+
+// byte offset of 16-B piece q of staged row r: 64-B rows XOR-keyed by (r >> 2) & 3 (4 rows per 256-B
+// bank row), 128-B rows by (r >> 1) & 7 (2 rows per bank row) -- a ds_read_b128 16-lane group reads
+// 16 consecutive rows at one logical piece and gets 16 distinct bank slots either way
+template <int BK>
+__device__ inline int gl_swz(int r, int q) {
+    if constexpr (BK == 32) return r * 64 + ((q ^ ((r >> 2) & 3)) << 4);
+    else return r * 128 + ((q ^ ((r >> 1) & 7)) << 4);
+}
 __device__ inline void gl_dma16(const void *src, void *lds) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
@@ -872,7 +888,7 @@ struct TokSrc {
 
 // DBG (diagnostic builds, -DMAPF_LIN_DEBUG): 1 = the GEMM with a plain fp16 store as the epilogue, 2 = the
 // epilogue without the GEMM (acc = 0)
-template <int EPI, int MT, int S, int DBG = 0>
+template <int EPI, int MT, int S, int DBG = 0, int BK = 32>
 __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ W,
                                                         const uint16_t *__restrict__ bias, long M,
                                                         uint16_t *__restrict__ out, float *__restrict__ x,
@@ -882,23 +898,44 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = (int)threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    using G = GL<MT, S>;
-    constexpr int AW = 4 * MT;                                 // waves that fill A (16 rows each)
+    using G = GL<MT, S, BK>;
+    constexpr int RPI = G::RPI, ROWB = G::ROWB;
+    // A rows MT * 64, W rows 512: DMA instructions of RPI rows; instruction g of A / W goes to wave
+    // g % 8 (BK = 32: waves 0..4 MT - 1 fill one A instruction each; BK = 64: 8 MT A + 64 W
+    // instructions, MT + 8 per wave)
+    constexpr int JA = (MT * GL_BM / RPI + 7) / 8, JW = GL_D / RPI / 8;
+    constexpr int NA = MT * GL_BM / RPI;                       // A instructions in all
     const long mt0 = (long)blockIdx.x * GL_BM * MT;
-    // one DMA instruction fills 16 rows x 64 B lane-linearly: lane l -> row 16 g + (l >> 2),
-    // physical piece l & 3 = logical piece q (the same for every g)
-    const int q = (lane & 3) ^ ((lane >> 4) & 3);
-    const long rowA = mt0 + 16 * wave + (lane >> 2);           // waves 0..AW-1 fill A rows 16w..16w+15
-    const uint16_t *srcA = (wave < AW && rowA < M) ? A + rowA * GL_D + q * 8 : nullptr;
+    // one DMA instruction fills RPI rows lane-linearly: lane l -> row RPI g + l / (64 / RPI), physical
+    // piece l % (64 / RPI); the source is pre-swizzled: the lane fetches the logical piece that lands in
+    // its physical slot (gl_swz), which depends on g only through its parity (BK = 64) or not (BK = 32)
+    const int lpr = 64 / RPI;                                  // lanes per row: 4 or 8
+    auto logical_piece = [&](int g) {
+        const int r = RPI * g + lane / lpr, ph = lane % lpr;
+        return BK == 32 ? (ph ^ ((r >> 2) & 3)) : (ph ^ ((r >> 1) & 7));
+    };
+    const int q0 = logical_piece(0), q1 = logical_piece(1);
+    const uint16_t *srcA[JA];
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+        const int g = wave + 8 * j;
+        const long rowA = mt0 + RPI * g + lane / lpr;
+        srcA[j] = (g < NA && rowA < M) ? A + rowA * GL_D + ((g & 1) ? q1 : q0) * 8 : nullptr;
+    }
     auto issue = [&](int c, int buf) {
         char *As = smem + buf * G::BUF;
         char *Bs = As + G::ABYTES;
-        if (wave < AW)
-            gl_dma16(srcA ? (const void *)(srcA + c * GL_BK) : (const void *)g_lin_zero, As + 16 * wave * 64);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {                          // wave w fills W rows 64w..64w+63
-            const int n = 64 * wave + 16 * j + (lane >> 2);
-            gl_dma16(W + (size_t)n * GL_D + c * GL_BK + q * 8, Bs + (64 * wave + 16 * j) * 64);
+        for (int j = 0; j < JA; ++j) {
+            const int g = wave + 8 * j;
+            if (g < NA)
+                gl_dma16(srcA[j] ? (const void *)(srcA[j] + c * BK) : (const void *)g_lin_zero, As + RPI * g * ROWB);
+        }
+#pragma unroll
+        for (int j = 0; j < JW; ++j) {                         // BK 32: wave w fills W rows 64w..64w+63
+            const int g = JW * wave + j;
+            const int n = RPI * g + lane / lpr;
+            gl_dma16(W + (size_t)n * GL_D + c * BK + ((g & 1) ? q1 : q0) * 8, Bs + RPI * g * ROWB);
         }
     };
     const int wm = wave & 1, wn = wave >> 1, fr = lane & 31, fh = lane >> 5;
@@ -908,53 +945,61 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
 #pragma unroll
         for (int b = 0; b < 4; ++b)
             for (int r = 0; r < 16; ++r) acc[i][b][r] = 0.f;
-    constexpr int NCH = GL_D / GL_BK;
+    constexpr int NCH = GL_D / BK;
     // ring: chunks 0 .. S-2 in flight; at chunk c wait until only the chunks after it (at most S - 2)
-    // are outstanding -- each wave's DMAs per chunk: 5 (A-filling waves) or 4 -- then ONE raw
-    // barrier (every wave's copies of chunk c have landed, every wave is done reading chunk c - 1),
-    // then refill chunk c - 1's buffer with chunk c + S - 1 and compute chunk c.  lgkmcnt(0) before the
-    // barrier: chunk c - 1's LDS reads have returned before its buffer is restaged.
+    // are outstanding -- each wave's DMAs per chunk: DA (the waves that fill an A instruction) or DB
+    // -- then ONE raw barrier (every wave's copies of chunk c have landed, every wave is done reading
+    // chunk c - 1), then refill chunk c - 1's buffer with chunk c + S - 1 and compute chunk c.
+    // lgkmcnt(0) before the barrier: chunk c - 1's LDS reads have returned before its buffer is restaged.
+    constexpr int DB = JW, DA = JW + JA;                       // (BK = 32, MT = 1: 4 / 5)
+    const bool fills_a = wave < NA;                            // (waves with JA A instructions: NA >= 8 fills all)
 #pragma unroll
     for (int c = 0; c < S - 1; ++c) if (DBG != 2) issue(c, c);
     for (int c = 0; c < (DBG == 2 ? 0 : NCH); ++c) {
         const int ahead = (NCH - 1 - c) < (S - 2) ? (NCH - 1 - c) : (S - 2);
         if (ahead >= 2) {
-            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0070 | 10);
-            else __builtin_amdgcn_s_waitcnt(0x0070 | 8);
+            if (fills_a) __builtin_amdgcn_s_waitcnt(vm_lgkm0(2 * DA));
+            else __builtin_amdgcn_s_waitcnt(vm_lgkm0(2 * DB));
         } else if (ahead == 1) {
-            if (wave < AW) __builtin_amdgcn_s_waitcnt(0x0070 | 5);
-            else __builtin_amdgcn_s_waitcnt(0x0070 | 4);
+            if (fills_a) __builtin_amdgcn_s_waitcnt(vm_lgkm0(DA));
+            else __builtin_amdgcn_s_waitcnt(vm_lgkm0(DB));
         } else {
-            __builtin_amdgcn_s_waitcnt(0x0070);
+            __builtin_amdgcn_s_waitcnt(vm_lgkm0(0));
         }
         __builtin_amdgcn_s_barrier();
         if (c + S - 1 < NCH) issue(c + S - 1, (c + S - 1) % S);
         const char *As = smem + (c % S) * G::BUF;
         const char *Bs = As + G::ABYTES;
-        // every fragment of the chunk read first (the waits then retire them progressively under the
-        // MFMAs; reading each MFMA's operands just before it left the MFMA pipe waiting on LDS latency)
-        constexpr int KS = GL_BK / 16;
-        gh8_t af[KS][MT], bf[KS][4];
+        // every fragment of a 32-deep half-chunk read first (the waits then retire them progressively
+        // under the MFMAs; reading each MFMA's operands just before it left the MFMA pipe waiting on LDS
+        // latency); BK = 64 takes two such halves
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int qq = 2 * s + fh;
+        for (int h = 0; h < BK / 32; ++h) {
+            constexpr int KS = 2;
+            gh8_t af[KS][MT], bf[KS][4];
 #pragma unroll
-            for (int i = 0; i < MT; ++i) af[s][i] = *reinterpret_cast<const gh8_t *>(As + gl_swz(64 * i + 32 * wm + fr, qq));
-#pragma unroll
-            for (int b = 0; b < 4; ++b) bf[s][b] = *reinterpret_cast<const gh8_t *>(Bs + gl_swz(128 * wn + 32 * b + fr, qq));
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int s = 0; s < KS; ++s) {
+                const int qq = 2 * (2 * h + s) + fh;
 #pragma unroll
                 for (int i = 0; i < MT; ++i)
-                    acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][i], bf[s][b], acc[i][b], 0, 0, 0);
-        // pin that order against the scheduler's register-saving interleave (read, wait, MFMA)
-        __builtin_amdgcn_sched_group_barrier(0x100, KS * (MT + 4), 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, KS * 4 * MT, 0);
+                    af[s][i] = *reinterpret_cast<const gh8_t *>(As + gl_swz<BK>(64 * i + 32 * wm + fr, qq));
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    bf[s][b] = *reinterpret_cast<const gh8_t *>(Bs + gl_swz<BK>(128 * wn + 32 * b + fr, qq));
+            }
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+                        acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][i], bf[s][b], acc[i][b], 0, 0, 0);
+            // pin that order against the scheduler's register-saving interleave (read, wait, MFMA)
+            __builtin_amdgcn_sched_group_barrier(0x100, KS * (MT + 4), 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, KS * 4 * MT, 0);
+        }
     }
-    static_assert(S <= 4, "the waits above count at most two chunks ahead");
+    static_assert(S <= 4 && 2 * DA <= 63, "the waits above count at most two chunks ahead (6-bit vmcnt)");
     __builtin_amdgcn_s_waitcnt(0xC07F);                        // every wave done reading the last chunk
     __builtin_amdgcn_s_barrier();
     // the 64-row tiles one after the other through one LDS tile
@@ -1065,26 +1110,31 @@ __global__ __launch_bounds__(512) void linear512_kernel(const uint16_t *__restri
 // (tools/bench_lin_impl.py, profiles/r05_lin_forms.jsonl): 64-row, 2-stage workgroups -- two per CU --
 // are the fastest or within 1 % for the GELU, rows and tokens forms; deeper rings cost the second
 // workgroup per CU and lose 10-25 %.
-static int g_lin_mt = 0, g_lin_stages = 0;
+static int g_lin_mt = 0, g_lin_stages = 0, g_lin_kdepth = 0;
 #ifndef MAPF_LIN_DEBUG
 #define MAPF_LIN_DEBUG 0     // diagnostic builds: make variant V=lindbg1 VFLAGS=-DMAPF_LIN_DEBUG=1
 #endif
 static constexpr int lin_debug() { return MAPF_LIN_DEBUG; }
-template <int EPI, int MT, int S, class... Args>
+template <int EPI, int MT, int S, int BK = 32, class... Args>
 static void launch_linear512_form(long rows, hipStream_t s, Args... args) {
-    constexpr int lds = GL<MT, S>::LDS;
+    constexpr int lds = GL<MT, S, BK>::LDS;
     const dim3 grid((unsigned)((rows + MT * GL_BM - 1) / (MT * GL_BM)));
     if (S == 2 && lin_debug() == 1)
-        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 1>), grid, dim3(512), lds, s, args...);
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 1, BK>), grid, dim3(512), lds, s, args...);
     else if (S == 2 && lin_debug() == 2)
-        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 2>), grid, dim3(512), lds, s, args...);
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 2, BK>), grid, dim3(512), lds, s, args...);
     else
-        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S>), grid, dim3(512), lds, s, args...);
+        hipLaunchKernelGGL((linear512_kernel<EPI, MT, S, 0, BK>), grid, dim3(512), lds, s, args...);
 }
 template <int EPI, class... Args>
 static void launch_linear512(long rows, hipStream_t s, Args... args) {
     const int mt = g_lin_mt ? g_lin_mt : 1;
     const int st = g_lin_stages ? g_lin_stages : 2;
+    if (g_lin_kdepth == 64) {           // full-line K chunks: two stages (the LDS holds no more at MT = 2)
+        if (mt == 2) launch_linear512_form<EPI, 2, 2, 64>(rows, s, args...);
+        else launch_linear512_form<EPI, 1, 2, 64>(rows, s, args...);
+        return;
+    }
     if (mt == 2) {
         if (st == 4) launch_linear512_form<EPI, 2, 4>(rows, s, args...);
         else if (st == 3) launch_linear512_form<EPI, 2, 3>(rows, s, args...);
@@ -1402,6 +1452,12 @@ int mapf_linear512_select(int32_t row_tiles) {
 int mapf_linear512_stages(int32_t stages) {
     if (stages != 0 && (stages < 2 || stages > 4)) return MAPF_EINVAL;
     pol::g_lin_stages = stages;
+    return MAPF_OK;
+}
+
+int mapf_linear512_kdepth(int32_t k) {
+    if (k != 0 && k != 32 && k != 64) return MAPF_EINVAL;
+    pol::g_lin_kdepth = k;
     return MAPF_OK;
 }
 

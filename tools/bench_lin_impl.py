@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--stages", default="2,3,4", help="K-ring stages to time")
     ap.add_argument("--only", default=None, help="comma-separated kernels (default: all)")
+    ap.add_argument("--forms", default=None,
+                    help="comma-separated row_tiles:stages:kdepth forms, e.g. 1:2:32,2:2:64 (default: row tiles 2 "
+                         "and 1 x --stages at kdepth 32)")
     args = ap.parse_args()
     L = _lib.lib()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -51,9 +54,12 @@ def main():
         for name, fn in kern.items():
             if args.only and name not in args.only.split(","):
                 continue
-            for mt, stages in [(m, s_) for m in (2, 1) for s_ in map(int, args.stages.split(","))]:
+            forms = ([tuple(map(int, f.split(":"))) for f in args.forms.split(",")] if args.forms else
+                     [(m, s_, 32) for m in (2, 1) for s_ in map(int, args.stages.split(","))])
+            for mt, stages, kd in forms:
                 _lib.check(L.mapf_linear512_select(mt))
                 _lib.check(L.mapf_linear512_stages(stages))
+                _lib.check(L.mapf_linear512_kdepth(kd))
                 for _ in range(2):
                     _lib.check(fn())
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,10 +69,11 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / args.iters
-                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "stages": stages, "lib": os.path.basename(os.environ.get("MAPF_LIB", "libmapf.so")), "us": round(us, 1),
+                print(json.dumps({"round": rnd, "kernel": name, "row_tiles": mt, "stages": stages, "kdepth": kd, "lib": os.path.basename(os.environ.get("MAPF_LIB", "libmapf.so")), "us": round(us, 1),
                                   "pflops": round(flop / us / 1e9, 3)}), flush=True)
     _lib.check(L.mapf_linear512_select(0))
     _lib.check(L.mapf_linear512_stages(0))
+    _lib.check(L.mapf_linear512_kdepth(0))
 
 
 if __name__ == "__main__":
