@@ -498,7 +498,8 @@ int mapf_ppo_loss(const float *new_ps, const float *old_ps, const int64_t *actio
                   float *grad_sig, void *stream);
 
 /* SCRIMPNet's 128- and 256-channel convolutions (net.py:104-111: conv1a / conv1b 3x3 128->128,
- * conv2 2x2 128->256, conv2a / conv2b 2x2 256->256, stride 1, zero padding `pad`) as an MFMA
+ * conv2 2x2 128->256, conv2a / conv2b 2x2 256->256; and 2x2 256->128, conv2's data gradient over the
+ * flipped weight in the training backward; stride 1, zero padding `pad`) as an MFMA
  * implicit GEMM (csrc/mapf_conv.hip).  x: fp16 NHWC [nimg][H][W][Cin]; w_packed: fp16
  * [Cout][ks][ks][Cin] (torch's weight permuted); y: fp16 NHWC [nimg][Ho][Wo][Cout], Ho = H + 2 pad -
  * ks + 1.  fp32 accumulation, output rounded to fp16; relu = 1: then + bias (fp16, rounded again)

@@ -752,6 +752,9 @@ int mapf_conv_nhwc_f16(const uint16_t *x, const uint16_t *w_packed, const uint16
     else if (Cin == 128 && Cout == 128 && ks == 3) conv::launch<128, 128, 3, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 128 && Cout == 256 && ks == 2) conv::launch<128, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else if (Cin == 256 && Cout == 256 && ks == 2) conv::launch<256, 256, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
+    // the data gradient of conv2 (128 -> 256, 2x2): 256 -> 128 over the flipped weight (net._HipConv;
+    // MIOpen's backward-data kernel took 174 us for it at 2,048 images, profiles/r06f_update_profile.txt)
+    else if (Cin == 256 && Cout == 128 && ks == 2) conv::launch<256, 128, 2, 8>(x, w_packed, bias, y, M, H, W, Ho, Wo, pad, epi, s);
     else return MAPF_EINVAL;
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }

@@ -211,6 +211,57 @@ class _BiasReLUPool(torch.autograd.Function):
         return dr, db
 
 
+class _HipConv(torch.autograd.Function):
+    """conv2d(x, w) without bias (stride 1, fp16 NHWC, net.py:104-112) for the TRAINING forward's
+    128- / 256-channel layers on the acting path's MFMA implicit GEMM (mapf_conv_nhwc_f16, raw fp16
+    output: fp32 accumulation, one rounding, as MIOpen's); the bias + ReLU (+ pool) follow in _BiasReLU /
+    _BiasReLUPool.  Backward: the data gradient is the same kernel run over dy with the flipped,
+    transposed weight (dx = conv(dy, w[:, :, ::-1, ::-1]^T), padding ks - 1 - pad) wherever that
+    shape is one the kernel has (SCRIMPNet._OWN_CONV: every layer from conv1a to conv2b), else MIOpen's;
+    the weight gradient is MIOpen's (aten.convolution_backward).  In place of MIOpen's forward and data
+    gradient (0.28 + 0.48 ms of a 256 x 8-row update, profiles/r06_update_profile_c3.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, w, pad):
+        from . import _lib
+        B, Cin, H, W = x.shape
+        Cout, _, ks, _ = w.shape
+        y = torch.empty((B, Cout, H + 2 * pad - ks + 1, W + 2 * pad - ks + 1), dtype=torch.float16, device=x.device,
+                        memory_format=torch.channels_last)
+        st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        # a channels_last [Cout][Cin][ks][ks] weight is [Cout][ks][ks][Cin] in memory: the kernel's packed form
+        _lib.check(_lib.lib().mapf_conv_nhwc_f16(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()), None,
+                                                 ctypes.c_void_p(y.data_ptr()), B, H, W, Cin, Cout, ks, pad, 0, st))
+        ctx.save_for_backward(x, w)
+        ctx.pad = pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        x, w = ctx.saved_tensors
+        pad = ctx.pad
+        B, Cin, H, W = x.shape
+        Cout, _, ks, _ = w.shape
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        own_dx = ctx.needs_input_grad[0] and (Cout, Cin, ks) in SCRIMPNet._OWN_CONV
+        mask = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], False]
+        dx = dw = None
+        if any(mask):
+            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                            mask)
+            dx = gx if mask[0] else None
+            dw = gw if mask[1] else None
+        if own_dx:
+            wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)   # [Cin][ks][ks][Cout]
+            dx = torch.empty(x.shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
+            st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+            _lib.check(_lib.lib().mapf_conv_nhwc_f16(ctypes.c_void_p(dy.data_ptr()), ctypes.c_void_p(wt.data_ptr()), None,
+                                                     ctypes.c_void_p(dx.data_ptr()), B, dy.shape[2], dy.shape[3], Cout,
+                                                     Cin, ks, ks - 1 - pad, 0, st))
+        return dx, dw, None
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
 
@@ -506,11 +557,24 @@ class SCRIMPNet(nn.Module):
         self.fused_linear = True       # 512x512 linears + their dropout/residual/LayerNorm or GELU epilogue, one launch
         self._h16 = {}                 # fp16 weights of the acting forward (_half)
 
-    _OWN_CONV = {(128, 128, 3), (128, 256, 2), (256, 256, 2)}    # (Cin, Cout, kernel) of mapf_conv_nhwc_f16
+    # (Cin, Cout, kernel) of mapf_conv_nhwc_f16; (256, 128, 2) is conv2's data gradient (_HipConv)
+    _OWN_CONV = {(128, 128, 3), (128, 256, 2), (256, 256, 2), (256, 128, 2)}
     cast_params = True             # training forward: conv / linear weights to fp16 in one launch (_CastParams)
     _in_cast = False
 
     hip_bias_relu = True           # training forward: conv bias + ReLU on _BiasReLU (GPU, autocast)
+    hip_conv = True                # training forward: the _OWN_CONV layers' convolutions on _HipConv (MFMA)
+
+    def _conv_nobias(self, x, m):
+        """conv2d(x, m.weight) without the bias, fp16 NHWC: _HipConv for the MFMA kernel's shapes, else MIOpen"""
+        w = m.weight
+        co, ci, ks, _ = w.shape
+        if (self.hip_conv and (ci, co, ks) in self._OWN_CONV and w.dtype == torch.float16 and x.dtype == torch.float16
+                and m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding[0] == m.padding[1]
+                and m.padding[0] < ks and x.is_contiguous(memory_format=torch.channels_last)
+                and w.is_contiguous(memory_format=torch.channels_last) and x.shape[0] > 0):
+            return _HipConv.apply(x, w, m.padding[0])
+        return F.conv2d(x, w, None, m.stride, m.padding)
 
     def _conv_relu(self, x, m):
         """F.relu(m(x)) under autocast; on the GPU with grad, the convolution without its bias and
@@ -518,7 +582,7 @@ class SCRIMPNet(nn.Module):
         if (self.hip_bias_relu and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
                 m.bias is not None and m.out_channels % 4 == 0 and m.out_channels <= 1024 and
                 m.weight.is_contiguous(memory_format=torch.channels_last)):
-            y = F.conv2d(x, m.weight, None, m.stride, m.padding)
+            y = self._conv_nobias(x, m)
             if y.dtype == torch.float16 and y.is_contiguous(memory_format=torch.channels_last) and y.numel() > 0:
                 b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
                 return _BiasReLU.apply(y, b)
@@ -534,7 +598,7 @@ class SCRIMPNet(nn.Module):
                 not pool.ceil_mode and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
                 m.bias is not None and m.out_channels % 4 == 0 and m.out_channels <= 1024 and
                 m.weight.is_contiguous(memory_format=torch.channels_last)):
-            r = F.conv2d(x, m.weight, None, m.stride, m.padding)
+            r = self._conv_nobias(x, m)
             if (r.dtype == torch.float16 and r.is_contiguous(memory_format=torch.channels_last) and r.numel() > 0 and
                     r.shape[2] >= 2 and r.shape[3] >= 2):
                 b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)

@@ -180,3 +180,60 @@ def test_conv_bias_relu_pool_matches_autocast(cin, cout, ks, pad, hw):
         for k, (a, b) in enumerate(zip(res["hip"][1:], res[ref][1:])):
             rel = ((a - b).norm() / b.norm()).item()
             assert rel < tol, (ref, k, rel)
+
+
+@pytest.mark.parametrize("cin,cout,ks,pad,hw,b", [(128, 128, 3, 1, 9, 96), (128, 256, 2, 1, 4, 64),
+                                                  (256, 128, 2, 0, 5, 40), (256, 256, 2, 1, 5, 64),
+                                                  (256, 256, 2, 1, 6, 33)])
+def test_hip_conv_matches_miopen_conv(cin, cout, ks, pad, hw, b):
+    """net._HipConv (the training forward's conv on mapf_conv_nhwc_f16; data gradient by the same kernel
+    over the flipped, transposed weight -- conv2's is the 256 -> 128 2x2 form, also run forward here --
+    weight gradient MIOpen's) against F.conv2d on the same fp16 NHWC tensors, MIOpen's
+    deterministic algorithms: output and data gradient to fp16 rounding of another fp32 summation order
+    (2e-3 relative in norm, elementwise 1e-2 of the tensor's scale), weight gradient equal (the same call)."""
+    from mapf_amd.net import SCRIMPNet, _HipConv
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(cin + cout + hw)
+    cl = torch.channels_last
+    x0 = torch.randn(b, cin, hw, hw, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    w0 = (torch.randn(cout, cin, ks, ks, device="cuda", generator=g) / (cin * ks * ks) ** 0.5).half().contiguous(
+        memory_format=cl)
+    ho = hw + 2 * pad - ks + 1
+    gy = torch.randn(b, cout, ho, ho, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    res = []
+    try:
+        for hip in (True, False):
+            x, w = x0.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+            y = _HipConv.apply(x, w, pad) if hip else torch.nn.functional.conv2d(x, w, None, 1, pad)
+            y.backward(gy)
+            res.append((y.detach().float(), x.grad.float(), w.grad.float()))
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    for k, (a, r) in enumerate(zip(*res)):
+        rel = ((a - r).norm() / r.norm()).item()
+        err = (a - r).abs().max().item() / r.abs().max().item()
+        print(f"conv {cin}->{cout} k{ks} {hw}x{hw}: {('y', 'dx', 'dw')[k]} relative {rel:.2e}, max {err:.2e}"
+              f"{'' if k != 1 else (' (own kernel)' if (cout, cin, ks) in SCRIMPNet._OWN_CONV else ' (MIOpen)')}")
+        assert rel < 2e-3 and err < 1e-2, (k, rel, err)
+
+
+def test_training_forward_convs_take_hip_conv():
+    """SCRIMPNet's training forward (GPU, autocast, grad) runs conv1a .. conv2b through _HipConv
+    (conv1 from the 6-channel observation and conv3 stay MIOpen's: shapes the kernel does not have)"""
+    from mapf_amd.net import SCRIMPNet, _HipConv
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9).cuda().to(memory_format=torch.channels_last)
+    calls = []
+    orig = _HipConv.forward
+    try:
+        _HipConv.forward = staticmethod(lambda ctx, x, w, pad: calls.append(tuple(w.shape)) or orig(ctx, x, w, pad))
+        obs = (torch.rand(4, 8, 6, 9, 9, device="cuda") < 0.3).float()
+        out = net(obs, torch.randn(4, 8, 4, device="cuda"))
+        out[1].float().sum().backward()
+    finally:
+        _HipConv.forward = orig
+    assert calls == [(128, 128, 3, 3), (128, 128, 3, 3), (256, 128, 2, 2), (256, 256, 2, 2), (256, 256, 2, 2)], calls
