@@ -480,6 +480,10 @@ int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t 
                            int32_t q_rows, int64_t q_token_stride, int64_t q_seq_stride, int64_t kv_token_stride,
                            int64_t kv_seq_stride, int64_t out_token_stride, int64_t out_seq_stride, int32_t heads,
                            int32_t head_dim, float scale, void *stream);
+/* Which kernel mapf_attention_bwd_f16 launches (process-wide): 1 (default, round 6) the MFMA form, one
+ * wave per (sequence, head), P and dS rounded to fp16 as MFMA operands; 0 the VALU form, one wave per
+ * three heads, P and dS in fp32.  MAPF_EINVAL otherwise. */
+int mapf_attention_bwd_select(int32_t form);
 
 /* ---- PPO loss (model.py:115-175) ------------------------------------------
  * All loss terms of one minibatch update over R = rows x agents elements with A actions each,

@@ -1308,6 +1308,184 @@ __global__ __launch_bounds__(64) void attention_bwd_f16(const uint16_t *__restri
     }
 }
 
+// ---- attention backward on the MFMA (round 6) ------------------------------------------------
+// One wave per (sequence, head); the 16 x 16 x 32 f16 MFMA with one contraction step = the head's 32
+// dims or 32 (padded) tokens.  Two register layouts of the score matrix, as the forward kernel:
+//   T (keys x queries): S^T = K Q^T and dP^T = V dO^T; the softmax over keys per query column (4 lanes
+//     l, l^16, l^32, l^48), its max / sum and D_q = rowsum(dO o O) kept in LDS;
+//     dS^T = P^T (dP^T - D); dQ^T = K^T dS^T: the accumulators are the B operand as they are (their k
+//     order (j >> 2) * 16 + 4 (l >> 4) + (j & 3)), K^T read in that order from an LDS image of K with
+//     ds_read_b64_tr_b16 -- attention_f16's O^T = V^T P^T;
+//   N (queries x keys): S = Q K^T and dP = dO V^T recomputed, P from the stored max / sum, dS;
+//     dV^T = dO^T P and dK^T = Q^T dS, dO^T and Q^T from their LDS images.
+// P and dS are rounded to fp16 as MFMA operands (flash SDPA's backward does the same); sums in fp32.
+// 28 MFMAs per (sequence, head); the kernel moves K, V, Q, dO, O in and dQ, dK, dV out (HBM-bound).
+// QT = query tiles of 16: 2 (rows <= 32) or 1 (rows <= 16: the token-0 query).
+constexpr int ABM_WAVES = 4;
+constexpr int ABM_LDS_WAVE = 3 * 2048 + 3 * 32 * 4;        // K, Q, dO images + max, sum, D per query
+template <int QT>
+__global__ __launch_bounds__(256) void attention_bwd_mfma(const uint16_t *__restrict__ q, const uint16_t *__restrict__ k,
+                                                          const uint16_t *__restrict__ v, const uint16_t *__restrict__ o,
+                                                          const uint16_t *__restrict__ dout, uint16_t *__restrict__ dq,
+                                                          uint16_t *__restrict__ dk, uint16_t *__restrict__ dv, int n,
+                                                          int rows, long q_ts, long q_ss, long kv_ts, long kv_ss,
+                                                          long o_ts, long o_ss, float scale) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ABM_WAVES][ABM_LDS_WAVE];
+    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+    const int g = lane >> 4, i = lane & 15;
+    const int h = (int)blockIdx.y * ABM_WAVES + w;             // head
+    const long b = blockIdx.x;
+    uint8_t *Kimg = lds[w], *Qimg = Kimg + 2048, *Gimg = Qimg + 2048;
+    float *Mq = reinterpret_cast<float *>(Gimg + 2048), *Lq = Mq + 32, *Dq = Lq + 32;
+    const uint16_t *qb = q + b * q_ss + h * 32 + 8 * g, *kb = k + b * kv_ss + h * 32 + 8 * g;
+    const uint16_t *vb = v + b * kv_ss + h * 32 + 8 * g, *ob = o + b * o_ss + h * 32 + 8 * g;
+    const uint16_t *gb = dout + b * o_ss + h * 32 + 8 * g;
+    // fragments: lane (i, g) holds token row 16 t + i, dims 8 g .. 8 g + 7 (zeros past n / rows)
+    uint4 kf[2], vf[2], qf[QT], gf[QT], of[QT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        kf[t] = ld16(kb + (16 * t + i) * kv_ts, 16 * t + i < n);
+        vf[t] = ld16(vb + (16 * t + i) * kv_ts, 16 * t + i < n);
+    }
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+        const bool ok = 16 * t + i < rows;
+        qf[t] = ld16(qb + (16 * t + i) * q_ts, ok);
+        gf[t] = ld16(gb + (16 * t + i) * o_ts, ok);
+        of[t] = ld16(ob + (16 * t + i) * o_ts, ok);
+    }
+    // LDS images (32 token rows x 64 B, vimg_off's swizzle), zero rows where no token is
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        *reinterpret_cast<uint4 *>(Kimg + vimg_off(16 * t + i, g)) = kf[t];
+        *reinterpret_cast<uint4 *>(Qimg + vimg_off(16 * t + i, g)) = t < QT ? qf[t < QT ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4 *>(Gimg + vimg_off(16 * t + i, g)) = t < QT ? gf[t < QT ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    // D_q = sum_d dO o O for query 16 qt + i (all four lanes of the column get it)
+    float Dv[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+        const h8_t a = as_h8(gf[t]), c = as_h8(of[t]);
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)a[e] * (float)c[e];
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        Dv[t] = d;
+    }
+    // ---- layout T: rows = keys (16 kt + 4 g + e), columns = queries (16 qt + i)
+    const f4_t zero4 = {0.f, 0.f, 0.f, 0.f};
+    h8_t dsT[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        f4_t s[2], dp[2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+            s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(kf[kt]), as_h8(qf[qt]), zero4, 0, 0, 0);
+            dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(vf[kt]), as_h8(gf[qt]), zero4, 0, 0, 0);
+        }
+        float x[8], m = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int key = (e >> 2) * 16 + 4 * g + (e & 3);
+            x[e] = key < n ? s[e >> 2][e & 3] * scale : -INFINITY;
+            m = fmaxf(m, x[e]);
+        }
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        float l = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[e] = __expf(x[e] - m);
+            l += x[e];
+        }
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float rl = 1.f / l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsT[qt][e] = (_Float16)(x[e] * rl * (dp[e >> 2][e & 3] - Dv[qt]));
+        if (g == 0) {
+            Mq[16 * qt + i] = m;
+            Lq[16 * qt + i] = rl;
+            Dq[16 * qt + i] = Dv[qt];
+        }
+    }
+    if (QT == 1 && g == 0) {                                   // queries 16..31 do not exist: P = dS = 0 there
+        Mq[16 + i] = 0.f;
+        Lq[16 + i] = 0.f;
+        Dq[16 + i] = 0.f;
+    }
+    __syncthreads();                                           // the images and the per-query stats are written
+    // the transposed A operand X^T (row = dim 16 dt + i, k = token in the accumulators' order) from image X
+    auto trX = [&](const uint8_t *img, int dt) {
+        const int rq = i >> 2, cp = i & 3;
+        const int c = 2 * dt + (cp >> 1), hb = 8 * (cp & 1);
+        const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t *)(img + vimg_off(4 * g + rq, c) + hb));
+        const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t *)(img + vimg_off(16 + 4 * g + rq, c) + hb));
+        return __builtin_bit_cast(h8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    // dQ^T = scale K^T dS^T: lane -> dims 16 dt + 4 g + e of query 16 qt + i
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const h8_t kt_ = trX(Kimg, dt);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const f4_t r = __builtin_amdgcn_mfma_f32_16x16x32_f16(kt_, dsT[qt], zero4, 0, 0, 0);
+            const int qr = 16 * qt + i;
+            if (qr < rows)
+                *reinterpret_cast<uint2 *>(dq + b * q_ss + qr * q_ts + h * 32 + 16 * dt + 4 * g) =
+                    pack4(f2h(r[0] * scale), f2h(r[1] * scale), f2h(r[2] * scale), f2h(r[3] * scale));
+        }
+    }
+    // ---- layout N: rows = queries (16 qt + 4 g + e), columns = keys (16 kt + i)
+    h8_t pN[2], dsN[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+        const int key = 16 * kt + i;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            if (qt < QT) {
+                const f4_t s = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(qf[qt < QT ? qt : 0]), as_h8(kf[kt]), zero4, 0, 0, 0);
+                const f4_t dp = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(gf[qt < QT ? qt : 0]), as_h8(vf[kt]), zero4, 0, 0, 0);
+                const float4 mq = *reinterpret_cast<const float4 *>(Mq + 16 * qt + 4 * g);
+                const float4 lq = *reinterpret_cast<const float4 *>(Lq + 16 * qt + 4 * g);
+                const float4 dq4 = *reinterpret_cast<const float4 *>(Dq + 16 * qt + 4 * g);
+                const float mm[4] = {mq.x, mq.y, mq.z, mq.w}, ll[4] = {lq.x, lq.y, lq.z, lq.w};
+                const float dd[4] = {dq4.x, dq4.y, dq4.z, dq4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float p = key < n ? __expf(s[e] * scale - mm[e]) * ll[e] : 0.f;
+                    pN[kt][4 * qt + e] = (_Float16)p;
+                    dsN[kt][4 * qt + e] = (_Float16)(p * (dp[e] - dd[e]));
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pN[kt][4 * qt + e] = dsN[kt][4 * qt + e] = (_Float16)0.f;
+            }
+        }
+    }
+    // dV^T = dO^T P, dK^T = scale Q^T dS: lane -> dims 16 dt + 4 g + e of key 16 kt + i
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const h8_t gt = trX(Gimg, dt), qt_ = trX(Qimg, dt);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+            const int key = 16 * kt + i;
+            const f4_t rv = __builtin_amdgcn_mfma_f32_16x16x32_f16(gt, pN[kt], zero4, 0, 0, 0);
+            const f4_t rk = __builtin_amdgcn_mfma_f32_16x16x32_f16(qt_, dsN[kt], zero4, 0, 0, 0);
+            if (key < n) {
+                *reinterpret_cast<uint2 *>(dv + b * kv_ss + key * kv_ts + h * 32 + 16 * dt + 4 * g) =
+                    pack4(f2h(rv[0]), f2h(rv[1]), f2h(rv[2]), f2h(rv[3]));
+                *reinterpret_cast<uint2 *>(dk + b * kv_ss + key * kv_ts + h * 32 + 16 * dt + 4 * g) =
+                    pack4(f2h(rk[0] * scale), f2h(rk[1] * scale), f2h(rk[2] * scale), f2h(rk[3] * scale));
+            }
+        }
+    }
+}
+
+// 1 (default): attention_bwd_mfma; 0: the VALU kernel above (attention_bwd_f16)
+static int g_attn_bwd_form = 1;
+
 }  // namespace pol
 }  // namespace mapf
 
@@ -1567,6 +1745,19 @@ int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t 
           (uintptr_t)dk | (uintptr_t)dv) & 15))
         return MAPF_EINVAL;
     if (B == 0) return MAPF_OK;
+    if (pol::g_attn_bwd_form == 1) {   // one wave per (sequence, head), four heads per workgroup
+        if (q_rows <= 16)
+            hipLaunchKernelGGL((pol::attention_bwd_mfma<1>), dim3((unsigned)B, 4), dim3(256), 0, (hipStream_t)stream, q, k,
+                               v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride,
+                               (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride, (long)out_seq_stride,
+                               scale);
+        else
+            hipLaunchKernelGGL((pol::attention_bwd_mfma<2>), dim3((unsigned)B, 4), dim3(256), 0, (hipStream_t)stream, q, k,
+                               v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride, (long)q_seq_stride,
+                               (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride, (long)out_seq_stride,
+                               scale);
+        return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+    }
     if (n <= 20)        // three heads per wave (21 lanes each), six workgroups per sequence
         hipLaunchKernelGGL((pol::attention_bwd_f16<20, 3>), dim3((unsigned)B, 6), dim3(64), 3 * pol::AB<20>::LDS,
                            (hipStream_t)stream, q, k, v, out, dout, dq, dk, dv, (int)n, (int)q_rows, (long)q_token_stride,
@@ -1578,6 +1769,12 @@ int mapf_attention_bwd_f16(const uint16_t *q, const uint16_t *k, const uint16_t 
                            (long)q_seq_stride, (long)kv_token_stride, (long)kv_seq_stride, (long)out_token_stride,
                            (long)out_seq_stride, scale);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_attention_bwd_select(int32_t form) {
+    if (form < 0 || form > 1) return MAPF_EINVAL;
+    pol::g_attn_bwd_form = form;
+    return MAPF_OK;
 }
 
 }  // extern "C"

@@ -132,6 +132,7 @@ SIGNATURES = {
     "mapf_attention_f16": (ctypes.c_int, [P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I32, I32, ctypes.c_float, P]),
     "mapf_attention_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, I32, I32, I64, I64, I64, I64, I64, I64, I32,
                                               I32, ctypes.c_float, P]),
+    "mapf_attention_bwd_select": (ctypes.c_int, [I32]),
 }
 
 _lib = None

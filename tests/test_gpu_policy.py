@@ -428,11 +428,22 @@ def test_conv_first_kernel_vs_torch(C, H, B):
         torch.testing.assert_close(y.float(), ref.float(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("bwd_form", [1, 0])
 @pytest.mark.parametrize("n,first", [(17, False), (17, True), (5, False), (32, False), (9, True)])
-def test_hip_attention_autograd_vs_sdpa(n, first):
+def test_hip_attention_autograd_vs_sdpa(n, first, bwd_form):
     """_HipAttention (mapf_attention_f16 + mapf_attention_bwd_f16) == SDPA on the same fp16 q, k, v
     in fp32: output and dq / dk / dv, for the fused qkv tensor (one gradient) and for token 0's
-    query against separate k / v (forward_first)."""
+    query against separate k / v (forward_first); both backward forms (mapf_attention_bwd_select:
+    1 MFMA, the default; 0 VALU)."""
+    from mapf_amd import _lib
+    _lib.check(_lib.lib().mapf_attention_bwd_select(bwd_form))
+    try:
+        _attention_vs_sdpa(n, first)
+    finally:
+        _lib.check(_lib.lib().mapf_attention_bwd_select(1))
+
+
+def _attention_vs_sdpa(n, first):
     from mapf_amd.net import _HipAttention
     g = torch.Generator(device="cuda").manual_seed(n + 100 * first)
     b, d, scale = 37, 512, 512 ** -0.5
