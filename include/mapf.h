@@ -406,6 +406,27 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
 int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *gamma, const uint16_t *dz,
                            const float *dres, float *dx, float *dgamma, float *dbeta, float *work, int64_t rows,
                            int32_t dim, float eps, void *stream);
+
+/* The TRAINING forward's dropout + residual + next LayerNorm (round 6; net._DropResLN), one pass:
+ * x_out = res + dropout(y) (fp32; res rows res_row_stride floats apart, y fp16 contiguous), z =
+ * fp16(LayerNorm(x_out)) -- mapf_dropout_residual_layernorm's arithmetic, out of place.  The dropout's
+ * seed is read from DEVICE memory (seed_dev[0], a counter the training forward increments, mixed with
+ * the site's salt), so a captured update draws new masks on every replay.  dim 512, p in [0, 1). */
+int mapf_dropout_residual_layernorm_train(const float *res, int64_t res_row_stride, const uint16_t *y, float *x_out,
+                                          const float *gamma, const float *beta, uint16_t *z, int64_t rows, int32_t dim,
+                                          float eps, float p, const uint64_t *seed_dev, uint32_t salt, void *stream);
+/* Its backward: mapf_layernorm_bwd_f16 over x_out (contiguous) with dres, plus dy (fp16) = the
+ * gradient of the dropped branch: fp16(fp16(dx) * 1 / (1 - p)) where the forward kept, 0 elsewhere. */
+int mapf_layernorm_dropout_bwd_f16(const float *x, const float *gamma, const uint16_t *dz, const float *dres, float *dx,
+                                   uint16_t *dy, float *dgamma, float *dbeta, float *work, int64_t rows, int32_t dim,
+                                   float eps, float p, const uint64_t *seed_dev, uint32_t salt, void *stream);
+/* The training forward's MLP GELU + dropout (net._GeluDropout): out = dropout(gelu(h)) fp16 (h kept), and
+ * its backward dh = fp16(gelu'(h) * fp16(dout / (1 - p)) where kept) -- torch's masked_scale then its exact
+ * GeluBackward; the seed in device memory as above.  n % 4 == 0. */
+int mapf_gelu_dropout_train_f16(const uint16_t *h, uint16_t *out, int64_t n, float p, const uint64_t *seed_dev,
+                                uint32_t salt, void *stream);
+int mapf_gelu_dropout_bwd_f16(const uint16_t *h, const uint16_t *dout, uint16_t *dh, int64_t n, float p,
+                              const uint64_t *seed_dev, uint32_t salt, void *stream);
 int mapf_dropout_residual(float *x, const uint16_t *y, int64_t n, float p, uint64_t seed, void *stream);
 /* mapf_dropout_residual on rows x 512 contiguous x, y, then z = LayerNorm(x) as fp16 (like
  * mapf_layernorm_f16) in one pass; bit-identical to the two calls with the same seed. */

@@ -56,6 +56,10 @@ __device__ inline unsigned keep4(uint64_t seed, uint64_t i, uint32_t thr) {
     return (fmix32(c) >= thr ? 1u : 0u) | (fmix32(c ^ 1u) >= thr ? 2u : 0u) | (fmix32(c ^ 2u) >= thr ? 4u : 0u) |
            (fmix32(c ^ 3u) >= thr ? 8u : 0u);
 }
+// the training forward's dropout seed: a counter in device memory (SCRIMPNet._train_seed) and a per-site salt
+__device__ inline uint64_t dev_seed(const uint64_t *__restrict__ p, uint32_t salt) {
+    return p[0] * 0x9E3779B97F4A7C15ull + (uint64_t)salt * 0xD1B54A32D192ED03ull;
+}
 inline uint32_t drop_threshold(float p) {
     const double t = (double)p * 4294967296.0;
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
@@ -208,11 +212,16 @@ __global__ __launch_bounds__(256) void layernorm_f16(const float *__restrict__ x
 //   dx = rstd (g - mean_k(g) - xhat mean_k(g xhat))       (fp32, one wave per row)
 //   dgamma = sum_rows dz xhat, dbeta = sum_rows dz        (per-workgroup partials, then ln_bwd_colsum)
 constexpr int LNB_WG = 512;                                 // partial rows of the gamma / beta gradients
+// dy16 (training dropout + residual + LayerNorm, drln_fwd): also the gradient of the dropped branch,
+// dy = fp16(fp16(dx) * scale) where drln_fwd kept the element, 0 where it dropped it -- autograd's fp16
+// cast at the mixed-precision add, then torch's dropout backward (masked_scale)
 __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict__ x, long xstride,
                                                          const float *__restrict__ gamma,
                                                          const uint16_t *__restrict__ dz,
                                                          const float *__restrict__ dres, float *__restrict__ dx,
-                                                         float *__restrict__ part, long rows, float eps) {
+                                                         float *__restrict__ part, long rows, float eps,
+                                                         uint16_t *__restrict__ dy16, uint32_t thr, float scale,
+                                                         const uint64_t *__restrict__ seedp, uint32_t salt) {
     constexpr int D = 512;
     __shared__ float red[2][4][D];
     const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
@@ -267,6 +276,18 @@ __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict
         float4 *dr = reinterpret_cast<float4 *>(dx + row * D);
         dr[lane] = make_float4(o[0], o[1], o[2], o[3]);
         dr[64 + lane] = make_float4(o[4], o[5], o[6], o[7]);
+        if (dy16) {
+            const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+            const unsigned k0 = thr ? keep4(seed, (uint64_t)(row * 128 + lane), thr) : 15u;
+            const unsigned k1 = thr ? keep4(seed, (uint64_t)(row * 128 + 64 + lane), thr) : 15u;
+            uint32_t h[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                h[e] = (((e < 4 ? k0 : k1) >> (e & 3)) & 1u) ? f2h(h2f(f2h(o[e])) * scale) : 0u;
+            uint2 *yr = reinterpret_cast<uint2 *>(dy16 + row * D);
+            yr[lane] = pack4(h[0], h[1], h[2], h[3]);
+            yr[64 + lane] = pack4(h[4], h[5], h[6], h[7]);
+        }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -613,6 +634,75 @@ __global__ __launch_bounds__(256) void gelu_dropout_f16(uint16_t *__restrict__ h
             o[q] = ((k >> q) & 1u) ? f2h(g * scale) : 0u;
         }
         *p = pack4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// ---- the TRAINING forward's dropout (round 6): the same hash masks, the seed in device memory ------
+// A captured update replays its kernels with the arguments they were captured with, so a seed passed
+// by value would drop the same elements in every replay.  These kernels read a counter the training
+// forward increments on the device (SCRIMPNet._train_seed, captured with the update) and mix in a
+// per-site salt: every replay, and every dropout site, draws its own mask.
+
+// x_out = res + dropout(y) (fp32; res may be a strided view: rstride floats per row), z = LayerNorm(x_out)
+// fp16: dropout_residual_layernorm's arithmetic without writing over the residual (autograd keeps it)
+__global__ __launch_bounds__(256) void drln_fwd(const float *__restrict__ res, long rstride, const uint16_t *__restrict__ y,
+                                                float *__restrict__ xo, const float *__restrict__ gamma,
+                                                const float *__restrict__ beta, uint16_t *__restrict__ z, long rows,
+                                                uint32_t thr, float scale, float eps, const uint64_t *__restrict__ seedp,
+                                                uint32_t salt) {
+    const int lane = (int)(threadIdx.x & 63);
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+    const long i0 = row * 128 + lane, i1 = i0 + 64;
+    const float4 *rr = reinterpret_cast<const float4 *>(res + row * rstride);
+    const uint2 *yr = reinterpret_cast<const uint2 *>(y);
+    const float4 a = add_dropped(rr[lane], yr[i0], thr ? keep4(seed, (uint64_t)i0, thr) : 15u, scale);
+    const float4 c = add_dropped(rr[64 + lane], yr[i1], thr ? keep4(seed, (uint64_t)i1, thr) : 15u, scale);
+    float4 *xr = reinterpret_cast<float4 *>(xo);
+    xr[i0] = a;
+    xr[i1] = c;
+    ln_row(a, c, lane, gamma, beta, eps, z + row * 512);
+}
+
+__device__ inline float gelu_exact(float a) { return 0.5f * a * (1.f + erff(a * 0.70710678118654752f)); }
+
+// out = dropout(gelu(h)) (h kept for the backward): gelu_dropout_f16's arithmetic, out of place
+__global__ __launch_bounds__(256) void gelu_dropout_train(const uint16_t *__restrict__ h, uint16_t *__restrict__ out, long n4,
+                                                          uint32_t thr, float scale, const uint64_t *__restrict__ seedp,
+                                                          uint32_t salt) {
+    const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const unsigned k = thr ? keep4(seed, (uint64_t)i, thr) : 15u;
+        const uint2 v = reinterpret_cast<const uint2 *>(h)[i];
+        const uint32_t in[4] = {v.x, v.x >> 16, v.y, v.y >> 16};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = ((k >> q) & 1u) ? f2h(h2f(f2h(gelu_exact(h2f(in[q])))) * scale) : 0u;
+        reinterpret_cast<uint2 *>(out)[i] = pack4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// dh = gelu'(h) * dropout_backward(dout): torch's masked_scale (fp16(dout * scale) where kept) then its
+// exact GeluBackward in fp32 (0.5 (1 + erf(x / sqrt 2)) + x exp(-x^2 / 2) / sqrt(2 pi)), rounded to fp16
+__global__ __launch_bounds__(256) void gelu_dropout_bwd(const uint16_t *__restrict__ h, const uint16_t *__restrict__ dout,
+                                                        uint16_t *__restrict__ dh, long n4, uint32_t thr, float scale,
+                                                        const uint64_t *__restrict__ seedp, uint32_t salt) {
+    const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const unsigned k = thr ? keep4(seed, (uint64_t)i, thr) : 15u;
+        const uint2 v = reinterpret_cast<const uint2 *>(h)[i], gv = reinterpret_cast<const uint2 *>(dout)[i];
+        const uint32_t in[4] = {v.x, v.x >> 16, v.y, v.y >> 16}, gi[4] = {gv.x, gv.x >> 16, gv.y, gv.y >> 16};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float t = ((k >> q) & 1u) ? h2f(f2h(h2f(gi[q]) * scale)) : 0.f;
+            const float x = h2f(in[q]);
+            const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+            const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
+            o[q] = f2h(t * __builtin_fmaf(x, pdf, cdf));     // torch's kernel, compiled with contraction
+        }
+        reinterpret_cast<uint2 *>(dh)[i] = pack4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -1590,8 +1680,59 @@ int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *ga
     const int G = (int)(rows < 4 * pol::LNB_WG ? (rows + 3) / 4 : pol::LNB_WG);
     if (G > 0)
         hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x,
-                           (long)x_row_stride, gamma, dz, dres, dx, work, (long)rows, eps);
+                           (long)x_row_stride, gamma, dz, dres, dx, work, (long)rows, eps, nullptr, 0u, 1.f, nullptr, 0u);
     hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_layernorm_dropout_bwd_f16(const float *x, const float *gamma, const uint16_t *dz, const float *dres, float *dx,
+                                   uint16_t *dy, float *dgamma, float *dbeta, float *work, int64_t rows, int32_t dim,
+                                   float eps, float p, const uint64_t *seed_dev, uint32_t salt, void *stream) {
+    if (!x || !gamma || !dz || !dx || !dy || !dgamma || !dbeta || !work || !seed_dev || rows < 0 || dim != 512 ||
+        !(p >= 0.f && p < 1.f) ||
+        (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)dx | (uintptr_t)dres) & 15) || (((uintptr_t)dz | (uintptr_t)dy) & 7))
+        return MAPF_EINVAL;
+    const int G = (int)(rows < 4 * pol::LNB_WG ? (rows + 3) / 4 : pol::LNB_WG);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x, (long)512,
+                           gamma, dz, dres, dx, work, (long)rows, eps, dy, pol::drop_threshold(p), 1.f / (1.f - p),
+                           seed_dev, salt);
+    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_dropout_residual_layernorm_train(const float *res, int64_t res_row_stride, const uint16_t *y, float *x_out,
+                                          const float *gamma, const float *beta, uint16_t *z, int64_t rows, int32_t dim,
+                                          float eps, float p, const uint64_t *seed_dev, uint32_t salt, void *stream) {
+    if (!res || !y || !x_out || !gamma || !beta || !z || !seed_dev || rows < 0 || dim != 512 || (res_row_stride & 3) ||
+        !(p >= 0.f && p < 1.f) ||
+        (((uintptr_t)res | (uintptr_t)x_out | (uintptr_t)gamma | (uintptr_t)beta) & 15) || (((uintptr_t)y | (uintptr_t)z) & 7))
+        return MAPF_EINVAL;
+    if (rows == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::drln_fwd, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, res,
+                       (long)res_row_stride, y, x_out, gamma, beta, z, (long)rows, pol::drop_threshold(p),
+                       1.f / (1.f - p), eps, seed_dev, salt);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_gelu_dropout_train_f16(const uint16_t *h, uint16_t *out, int64_t n, float p, const uint64_t *seed_dev,
+                                uint32_t salt, void *stream) {
+    if (!h || !out || !seed_dev || n < 0 || (n & 3) || !(p >= 0.f && p < 1.f) || (((uintptr_t)h | (uintptr_t)out) & 7))
+        return MAPF_EINVAL;
+    if (n == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::gelu_dropout_train, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, h, out,
+                       (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed_dev, salt);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_gelu_dropout_bwd_f16(const uint16_t *h, const uint16_t *dout, uint16_t *dh, int64_t n, float p,
+                              const uint64_t *seed_dev, uint32_t salt, void *stream) {
+    if (!h || !dout || !dh || !seed_dev || n < 0 || (n & 3) || !(p >= 0.f && p < 1.f) ||
+        (((uintptr_t)h | (uintptr_t)dout | (uintptr_t)dh) & 7))
+        return MAPF_EINVAL;
+    if (n == 0) return MAPF_OK;
+    hipLaunchKernelGGL(pol::gelu_dropout_bwd, dim3(pol::grid_for(n / 4, 256)), dim3(256), 0, (hipStream_t)stream, h, dout,
+                       dh, (long)(n / 4), pol::drop_threshold(p), 1.f / (1.f - p), seed_dev, salt);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

@@ -16,6 +16,7 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int32
 U32 = ctypes.c_uint32
 I64 = ctypes.c_int64
+F32 = ctypes.c_float
 
 
 class ResetSpec(ctypes.Structure):
@@ -102,6 +103,10 @@ SIGNATURES = {
     "mapf_cast_f32_to_f16_multi": (ctypes.c_int, [P, P, P, I32, P]),
     "mapf_cast_f16_to_f32_multi": (ctypes.c_int, [P, P, P, I32, P]),
     "mapf_layernorm_bwd_f16": (ctypes.c_int, [P, I64, P, P, P, P, P, P, P, I64, I32, ctypes.c_float, P]),
+    "mapf_layernorm_dropout_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64, I32, F32, F32, P, U32, P]),
+    "mapf_dropout_residual_layernorm_train": (ctypes.c_int, [P, I64, P, P, P, P, P, I64, I32, F32, F32, P, U32, P]),
+    "mapf_gelu_dropout_train_f16": (ctypes.c_int, [P, P, I64, F32, P, U32, P]),
+    "mapf_gelu_dropout_bwd_f16": (ctypes.c_int, [P, P, P, I64, F32, P, U32, P]),
     "mapf_dropout_residual": (ctypes.c_int, [P, P, I64, ctypes.c_float, ctypes.c_uint64, P]),
     "mapf_dropout_residual_layernorm": (ctypes.c_int, [P, P, P, P, P, I64, I32, ctypes.c_float, ctypes.c_float,
                                                         ctypes.c_uint64, P]),

@@ -505,11 +505,17 @@ class _DeviceUpdate:
 
     @staticmethod
     def _capture(fn):
+        """fn captured into a hipGraph on a side stream.  thread_local capture mode: the process group's
+        watchdog thread keeps querying the events of earlier RCCL work while the capture runs, which the
+        default (global) mode forbids -- it killed the process (hipErrorStreamCaptureUnsupported) in the
+        c4-shaped distributed update on a 1-rank RCCL group.  The eager collectives are also drained
+        (synchronize) before the capture begins."""
+        torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 fn()
         torch.cuda.current_stream().wait_stream(s)
         return g

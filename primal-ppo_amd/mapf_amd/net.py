@@ -262,6 +262,97 @@ class _HipConv(torch.autograd.Function):
         return dx, dw, None
 
 
+def _drop_p(m):
+    """a Dropout module's probability as the forward applies it (0 in eval mode)"""
+    return float(m.p) if m.training else 0.0
+
+
+class _DropResLN(torch.autograd.Function):
+    """The TRAINING forward's residual + next PreNorm in one pass (round 6): x_out = res + dropout(y),
+    z = fp16(LayerNorm(x_out)) -- mapf_dropout_residual_layernorm_train; backward
+    mapf_layernorm_dropout_bwd_f16: LayerNorm's backward with the residual gradient (as _HipLayerNorm),
+    the dropped branch's fp16 gradient and dgamma / dbeta in one pass.  In place of torch's dropout
+    forward / backward, the fp32 add and a separate LayerNorm launch at every residual that feeds a
+    LayerNorm (transformer.py:7-24, 64-85).  The dropout mask is the kernels' counter hash seeded from
+    `seed` (SCRIMPNet._train_seed, int64 [1] in device memory, incremented by every training forward --
+    also inside a captured update) and the site's salt.  res: fp32 [.., 512] (a strided view allowed),
+    y: fp16 [.., 512]."""
+
+    @staticmethod
+    def forward(ctx, res, y, weight, bias, eps, p, seed, salt):
+        from . import _lib
+        ctx.set_materialize_grads(False)
+        rows = res.numel() // 512
+        r2 = res.reshape(rows, 512)
+        if r2.stride(1) != 1 or r2.stride(0) % 4:
+            r2 = r2.contiguous()
+        y2 = y.reshape(rows, 512).contiguous()
+        xo = torch.empty(rows, 512, dtype=torch.float32, device=res.device)
+        z = torch.empty(rows, 512, dtype=torch.float16, device=res.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(res.device).cuda_stream)
+        q = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_dropout_residual_layernorm_train(q(r2), r2.stride(0), q(y2), q(xo), q(weight), q(bias),
+                                                                     q(z), rows, 512, float(eps), float(p), q(seed),
+                                                                     int(salt), st))
+        ctx.save_for_backward(xo, weight, seed)
+        ctx.meta = (float(eps), float(p), int(salt), res.shape, y.shape)
+        out_shape = tuple(res.shape[:-1]) + (512,)
+        return z.view(out_shape), xo.view(out_shape)
+
+    @staticmethod
+    def backward(ctx, dz, dxo):
+        from . import _lib
+        xo, weight, seed = ctx.saved_tensors
+        eps, p, salt, res_shape, y_shape = ctx.meta
+        rows = xo.shape[0]
+        dz = (torch.zeros(rows, 512, dtype=torch.float16, device=xo.device) if dz is None else
+              dz.reshape(rows, 512).to(torch.float16).contiguous())
+        if dxo is not None:
+            dxo = dxo.reshape(rows, 512).to(torch.float32).contiguous()
+        dx = torch.empty(rows, 512, dtype=torch.float32, device=xo.device)
+        dy = torch.empty(rows, 512, dtype=torch.float16, device=xo.device)
+        dg = torch.empty(512, dtype=torch.float32, device=xo.device)
+        db = torch.empty(512, dtype=torch.float32, device=xo.device)
+        work = torch.empty(2 * 512 * 512, dtype=torch.float32, device=xo.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(xo.device).cuda_stream)
+        q = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_layernorm_dropout_bwd_f16(q(xo), q(weight), q(dz), None if dxo is None else q(dxo),
+                                                             q(dx), q(dy), q(dg), q(db), q(work), rows, 512, eps, p,
+                                                             q(seed), salt, st))
+        return dx.view(res_shape), dy.view(y_shape), dg, db, None, None, None, None
+
+
+class _GeluDropout(torch.autograd.Function):
+    """dropout(gelu(h)) of the TRAINING forward's MLP (transformer.py:27-45, af1 + do1) in one pass each
+    way (round 6): mapf_gelu_dropout_train_f16 / mapf_gelu_dropout_bwd_f16 -- torch's fp16 GELU, dropout,
+    masked_scale and GeluBackward kernels in two launches; the mask as _DropResLN's.  h: fp16."""
+
+    @staticmethod
+    def forward(ctx, h, p, seed, salt):
+        from . import _lib
+        h = h.contiguous()
+        out = torch.empty_like(h)
+        st = ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream)
+        _lib.check(_lib.lib().mapf_gelu_dropout_train_f16(ctypes.c_void_p(h.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                                          h.numel(), float(p), ctypes.c_void_p(seed.data_ptr()),
+                                                          int(salt), st))
+        ctx.save_for_backward(h, seed)
+        ctx.meta = (float(p), int(salt))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import _lib
+        h, seed = ctx.saved_tensors
+        p, salt = ctx.meta
+        dout = dout.to(torch.float16).contiguous()
+        dh = torch.empty_like(h)
+        st = ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream)
+        q = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_gelu_dropout_bwd_f16(q(h), q(dout), q(dh), h.numel(), p, q(seed), salt, st))
+        return dh, None, None, None
+
+
 class _PreNorm(nn.Module):
     """Residual(LayerNormalize(dim, fn)) of transformer.py:7-24 (state_dict path `.fn.norm` / `.fn.fn`)."""
 
@@ -446,19 +537,26 @@ class _SelfAttention(nn.Module):
                 x.shape[-1] == 512 and x.shape[1] <= 32 and torch.is_grad_enabled())
 
     def forward(self, x):
+        return self.do1(self.forward_core(x))
+
+    def forward_core(self, x):
+        """forward(x) before its dropout (the fused training residual applies it)"""
         b, n, d = x.shape
         h = self.heads
         qkv = _train_linear(x, self.to_qkv.weight, self.to_qkv.bias)
         if self._hip(x, qkv):
             att = _HipAttention.apply(qkv.contiguous(), qkv.contiguous(), n, 0, d, 2 * d, self.scale)
-            return self.do1(_train_linear(att, self.nn1.weight, self.nn1.bias))
+            return _train_linear(att, self.nn1.weight, self.nn1.bias)
         qkv = qkv.view(b, n, 3, h, d // h).permute(2, 0, 3, 1, 4)   # 3, b, h, n, dh
         q, k, v = qkv[0], qkv[1], qkv[2]
         out = F.scaled_dot_product_attention(q, k, v, scale=self.scale).transpose(1, 2).reshape(b, n, d)
-        return self.do1(self.nn1(out))
+        return self.nn1(out)
 
     def forward_first(self, x):
         """Token 0 of forward(x) only: keys and values of every token, the query of token 0."""
+        return self.do1(self.forward_first_core(x))
+
+    def forward_first_core(self, x):
         b, n, d = x.shape
         h = self.heads
         w, bias = self.to_qkv.weight, self.to_qkv.bias
@@ -466,11 +564,11 @@ class _SelfAttention(nn.Module):
         q = F.linear(x[:, 0], w[:d], bias[:d])
         kv = _train_linear(x, w[d:], bias[d:])
         if self._hip(x, q):
-            return self.do1(self.nn1(_HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale)))
+            return self.nn1(_HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale))
         q = q.view(b, 1, h, d // h).transpose(1, 2)                                             # b, h, 1, dh
         kv = kv.view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)                                 # 2, b, h, n, dh
         out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=self.scale).transpose(1, 2).reshape(b, 1, d)
-        return self.do1(self.nn1(out))
+        return self.nn1(out)
 
 
 class _FeedForward(nn.Module):
@@ -489,8 +587,17 @@ class _FeedForward(nn.Module):
         self.do2 = nn.Dropout(dropout)
 
     def forward(self, x):
-        h = self.do1(self.af1(_train_linear(x, self.nn1.weight, self.nn1.bias)))
-        return self.do2(_train_linear(h, self.nn2.weight, self.nn2.bias))
+        return self.do2(self.forward_core(x))
+
+    def forward_core(self, x, seed=None, salt=0):
+        """forward(x) before its last dropout; with the training seed, GELU + dropout as _GeluDropout"""
+        h = _train_linear(x, self.nn1.weight, self.nn1.bias)
+        if (seed is not None and h.is_cuda and h.dtype == torch.float16 and h.numel() % 4 == 0 and
+                getattr(self.af1, "approximate", None) == "none"):
+            h = _GeluDropout.apply(h, _drop_p(self.do1), seed, salt)
+        else:
+            h = self.do1(self.af1(h))
+        return _train_linear(h, self.nn2.weight, self.nn2.bias)
 
 
 class _Encoder(nn.Module):
@@ -501,10 +608,43 @@ class _Encoder(nn.Module):
                            _PreNorm(dim, _FeedForward(dim, mlp_dim, dropout))])
             for _ in range(depth)])
 
-    def forward(self, x, first_only=False):
+    fused_train = True      # training forward (GPU): _DropResLN residuals and _GeluDropout (with a seed)
+
+    def _train_fused_ok(self, x):
+        return (self.fused_train and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
+                x.dtype == torch.float32 and x.shape[-1] == 512 and _PreNorm.hip_layernorm and
+                all(pn.fn.norm.elementwise_affine for blk in self.layers for pn in blk))
+
+    def _forward_train_fused(self, x, first_only, seed):
+        """forward() of the training pass with every residual that feeds a LayerNorm as one _DropResLN
+        (the residual add, its dropout and the next PreNorm's LayerNorm) and the MLP's GELU + dropout as
+        _GeluDropout; the same operations and rounding points, the dropout masks from the kernels'
+        hash (sites salted 2 li, 2 li + 1, 16 + li)"""
+        L = len(self.layers)
+        z, res = self.layers[0][0]._norm(x)
+        for li, (att, ff) in enumerate(self.layers):
+            a, f = att.fn.fn, ff.fn.fn
+            if first_only and li == L - 1:
+                y = a.forward_first_core(z)
+                res = res[:, :1]
+            else:
+                y = a.forward_core(z)
+            nrm = ff.fn.norm
+            z, res = _DropResLN.apply(res, y, nrm.weight, nrm.bias, nrm.eps, _drop_p(a.do1), seed, 2 * li)
+            y = f.forward_core(z, seed, 16 + li)
+            if li + 1 < L:
+                nrm = self.layers[li + 1][0].fn.norm
+                z, res = _DropResLN.apply(res, y, nrm.weight, nrm.bias, nrm.eps, _drop_p(f.do2), seed, 2 * li + 1)
+            else:
+                return res + f.do2(y)
+
+    def forward(self, x, first_only=False, seed=None):
         """first_only: return token 0 of the last block's output only ([b, 1, d]).  SCRIMPNet reads
         nothing else (net.py:140-141 takes x[:, 0]), so the last block's queries, output
-        projection and MLP of tokens 1..16 are skipped; keys/values still see every token."""
+        projection and MLP of tokens 1..16 are skipped; keys/values still see every token.
+        seed: the training forward's device dropout seed (SCRIMPNet._train_seed): the fused training path."""
+        if seed is not None and self._train_fused_ok(x):
+            return self._forward_train_fused(x, first_only, seed)
         for li, (att, ff) in enumerate(self.layers):
             if first_only and li == len(self.layers) - 1:
                 return ff(att.forward_first(x))
@@ -616,6 +756,20 @@ class SCRIMPNet(nn.Module):
             self._cast_names_cache = names
         return names
 
+    def _next_train_seed(self, x):
+        """The training forward's dropout seed for the fused kernels (_DropResLN, _GeluDropout): an int64
+        counter in device memory, incremented on the device by every training forward (so a captured
+        update draws new masks on every replay; two models built from the same torch seed, or copies,
+        draw the same).  None off the GPU training path."""
+        if not (x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda")):
+            return None
+        t = self.__dict__.get("_train_seed")
+        if t is None or t.device != x.device:
+            t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(x.device)
+            self.__dict__["_train_seed"] = t
+        t.add_(1)
+        return t
+
     def weights_updated(self):
         """Forget the acting path's fp16 weight copies: an update replayed from a captured graph
         changes the parameters without bumping their version counters (_half's key)."""
@@ -663,7 +817,7 @@ class SCRIMPNet(nn.Module):
             VV = torch.matmul(h, self.token_wV.sum(0))                        # [b, 1, 512]
             T = A * VV                       # [b, 16, 512]: matmul(A, VV) over a length-1 axis
             x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
-            x = self.transformer(self.dropout(x), first_only=True)
+            x = self.transformer(self.dropout(x), first_only=True, seed=self._next_train_seed(x))
             x = self.nn_same(self.nn_same(x[:, 0]))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)

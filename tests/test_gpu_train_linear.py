@@ -237,3 +237,129 @@ def test_training_forward_convs_take_hip_conv():
     finally:
         _HipConv.forward = orig
     assert calls == [(128, 128, 3, 3), (128, 128, 3, 3), (256, 128, 2, 2), (256, 256, 2, 2), (256, 256, 2, 2)], calls
+
+
+def _seed(v=12345):
+    return torch.tensor([v], dtype=torch.int64, device="cuda")
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("strided", [False, True])
+def test_drop_res_ln_matches_torch_chain(p, strided):
+    """net._DropResLN (x = res + dropout(y), z = fp16(LN(x)); backward: LN's with the residual gradient and
+    the dropped branch's fp16 gradient) against the unfused chain -- torch add of the (masked, scaled)
+    fp16 branch, then _HipLayerNorm -- given the SAME mask: p = 0 bit-identical forward and gradients;
+    p = 0.2: the mask the kernel drew is read back from its output (x - res == 0 exactly where dropped)
+    and fed to the chain; keep rate 0.8 +- 0.01.  strided: res is token 0 of a [b, 17, 512] stream."""
+    from mapf_amd.net import _DropResLN, _HipLayerNorm
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    b = 640
+    base = torch.randn(b, 17, 512, device="cuda", generator=g) * 2
+    res0 = base[:, :1] if strided else base[:, :5]
+    y0 = torch.randn(res0.shape, device="cuda", generator=g).half()
+    w0, b0 = 1 + 0.1 * torch.randn(512, device="cuda", generator=g), 0.1 * torch.randn(512, device="cuda", generator=g)
+    dz = torch.randn(res0.shape, device="cuda", generator=g).half()
+    dx_down = torch.randn(res0.shape, device="cuda", generator=g)
+    out = {}
+    for fused in (True, False):
+        res, y, w, bb = (t.detach().clone().requires_grad_(True) for t in (res0, y0, w0, b0))
+        if fused:
+            z, x = _DropResLN.apply(res, y, w, bb, 1e-5, p, _seed(), 3)
+            keep = (x.detach() - res0) != 0
+            keep |= y0.float() == 0
+            out["keep"] = keep
+        else:
+            k = out["keep"]
+            ydrop = torch.where(k, y * (1.0 / (1.0 - p)), torch.zeros_like(y)) if p > 0 else y
+            x = res + ydrop
+            z, x = _HipLayerNorm.apply(x, w, bb, 1e-5)
+        torch.autograd.backward([z, x], [dz, dx_down])
+        out[fused] = (z.detach().float(), x.detach(), res.grad, y.grad.float(), w.grad, bb.grad)
+    if p > 0:
+        rate = out["keep"].float().mean().item()
+        assert abs(rate - (1 - p)) < 0.01, rate
+    for k, (a, r) in enumerate(zip(out[True], out[False])):
+        if p == 0:
+            assert torch.equal(a, r), k
+        else:
+            torch.testing.assert_close(a, r, rtol=2e-3, atol=2e-3, msg=str(k))
+    assert torch.equal(out[True][3] == 0, out[False][3] == 0) or p == 0     # the gradient dropped where the forward did
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_gelu_dropout_matches_torch(p):
+    """net._GeluDropout against F.gelu then the same mask (read back from the output) on fp16: p = 0
+    bit-identical forward and gradient (torch's fp16 GELU and GeluBackward compute in fp32); p = 0.2
+    to fp16 rounding (torch scales after the GELU's rounding the same way), keep rate 0.8 +- 0.01."""
+    from mapf_amd.net import _GeluDropout
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    h0 = (torch.randn(4096, 512, device="cuda", generator=g) * 2).half()
+    gy = torch.randn(4096, 512, device="cuda", generator=g).half()
+    h = h0.clone().requires_grad_(True)
+    y = _GeluDropout.apply(h, p, _seed(77), 5)
+    y.backward(gy)
+    h2 = h0.clone().requires_grad_(True)
+    ref = torch.nn.functional.gelu(h2)
+    keep = (y.detach() != 0) | (ref.detach() == 0)
+    if p > 0:
+        assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+        ref = torch.where(keep, ref * (1.0 / (1.0 - p)), torch.zeros_like(ref))
+    ref.backward(gy)
+    if p == 0:
+        same_y = (y == ref.detach()).float().mean().item()
+        same_g = (h.grad == h2.grad).float().mean().item()
+        print(f"gelu: forward {same_y:.5%} bit-identical to torch's, gradient {same_g:.5%}")
+        # torch's exp / erf builds may round differently in the last bit: within one fp16 ulp
+        torch.testing.assert_close(y.float(), ref.detach().float(), rtol=1e-3, atol=1e-5)
+        torch.testing.assert_close(h.grad.float(), h2.grad.float(), rtol=1e-3, atol=1e-5)
+    else:
+        torch.testing.assert_close(y.float(), ref.detach().float(), rtol=2e-3, atol=2e-3)
+        torch.testing.assert_close(h.grad.float(), h2.grad.float(), rtol=2e-3, atol=2e-3)
+
+
+def test_training_forward_fused_residuals_equal_unfused():
+    """SCRIMPNet's training forward with _Encoder.fused_train (every LayerNorm-feeding residual a
+    _DropResLN, the MLP's GELU + dropout a _GeluDropout) == the unfused forward, dropout off: outputs
+    within fp16 rounding (1e-2 relative) and every parameter's gradient within 2e-2 (relative norm); and with
+    dropout on, two forwards draw different masks (the device seed counter moves)."""
+    from mapf_amd.net import SCRIMPNet, _Encoder
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(0)
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9).cuda().to(memory_format=torch.channels_last)
+    obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.3).float()
+    vec = torch.randn(16, 8, 4, device="cuda")
+    net.eval()
+    res = []
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False   # conv1 / conv3: MIOpen's
+    try:
+        for fused in (True, False):
+            _Encoder.fused_train = fused
+            net.zero_grad()
+            out = net(obs, vec)
+            (out[1].float().sum() + out[0].float().pow(2).sum()).backward()
+            res.append(([o.detach().float() for o in out], [p.grad.detach().clone() for p in net.parameters()
+                                                              if p.grad is not None]))
+    finally:
+        _Encoder.fused_train = True
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    # the same operations and rounding points; torch's GELU kernels may round their exp / erf in the last
+    # bit differently (test_gelu_dropout_matches_torch), which moves the outputs by fp16 ulps
+    for a, r in zip(res[0][0], res[1][0]):
+        print(f"output: max |diff| {(a - r).abs().max().item():.3e}, bit-identical {(a == r).float().mean().item():.4%}")
+        torch.testing.assert_close(a, r, rtol=1e-2, atol=2e-3)
+    assert len(res[0][1]) == len(res[1][1])
+    for a, r in zip(res[0][1], res[1][1]):
+        rel = ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
+        assert rel < 2e-2, rel
+    net.train()
+    with torch.no_grad():
+        net.dropout.p = 0.0                                  # torch's own dropout sites off: only the fused ones draw
+        net.transformer.layers[-1][1].fn.fn.do2.p = 0.0
+    outs = [net(obs, vec)[1].detach() for _ in range(2)]
+    assert not torch.equal(outs[0], outs[1])

@@ -130,3 +130,39 @@ def test_update_shapes_get_their_own_graphs():
         s = m.train(*b[:8], None, b[8], 0.5)
         assert all(np.isfinite(float(x)) or (k == 8 and np.isinf(float(x))) for k, x in enumerate(s))
     assert len(m._updates) == 2 and all(u.graph is not None for u in m._updates.values())
+
+
+def test_graphed_updates_draw_dropout_masks_like_eager(deterministic_convs):
+    """Dropout ON (train mode) at the fused training sites (_DropResLN, _GeluDropout: the counter-hash
+    masks seeded from SCRIMPNet._train_seed in device memory, incremented by every forward -- a captured
+    increment in the graph): the graphed updates equal an eager twin's, update by update, so every replay
+    drew the mask the eager forward drew; and consecutive updates draw different masks (the same
+    minibatch twice gives different losses).  torch's own dropout sites (the tokens' and the last
+    residual's, torch's RNG) are set to 0 so only the fused ones draw."""
+    from mapf_amd.model import Model
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(0)
+    m1 = Model(0, "cuda", global_model=True, numChannel=6, num_agents=8, fov=9)
+    with torch.no_grad():
+        m1.network.dropout.p = 0.0
+        m1.network.transformer.layers[-1][1].fn.fn.do2.p = 0.0
+    m1.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    m2 = copy.deepcopy(m1)
+    m2.graph_update = False
+    m2.net_scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    for m in (m1, m2):                                       # the same starting count (each its own tensor)
+        m.network.__dict__["_train_seed"] = torch.tensor([42], dtype=torch.int64, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    b = _batch(g)
+    s1 = [m1.train(*b[:8], None, b[8], 1.0) for _ in range(6)]
+    s2 = [m2.train(*b[:8], None, b[8], 1.0) for _ in range(6)]
+    upd = next(iter(m1._updates.values()))
+    assert upd.graph is not None and upd.eager_runs == upd.WARMUP
+    for k in range(6):
+        for i, (a, c) in enumerate(zip(s1[k], s2[k])):
+            assert float(a) == float(c) or (np.isnan(float(a)) and np.isnan(float(c))), (k, i, float(a), float(c))
+    # the same minibatch, new masks: the loss terms move from update to update (the weights move by ~lr only)
+    assert len({round(float(s[0]), 6) for s in s1}) == 6, [float(s[0]) for s in s1]
+    for p1, p2 in zip(m1.network.parameters(), m2.network.parameters()):
+        assert torch.equal(p1, p2)
