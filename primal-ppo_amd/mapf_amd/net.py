@@ -704,11 +704,24 @@ class SCRIMPNet(nn.Module):
 
     hip_bias_relu = True           # training forward: conv bias + ReLU on _BiasReLU (GPU, autocast)
     hip_conv = True                # training forward: the _OWN_CONV layers' convolutions on _HipConv (MFMA)
+    conv3_gemm = True              # training forward: a conv whose kernel covers its unpadded input as one GEMM
 
     def _conv_nobias(self, x, m):
-        """conv2d(x, m.weight) without the bias, fp16 NHWC: _HipConv for the MFMA kernel's shapes, else MIOpen"""
+        """conv2d(x, m.weight) without the bias, fp16 NHWC: a plain GEMM where the kernel covers its whole
+        unpadded input (conv3: 3x3 on 3x3 -> 1x1, as the acting path runs it; MIOpen's backward-data kernel
+        took ~160 us for it in a 256 x 8-row update, profiles/r06h_update_profile_c3.txt), _HipConv for the
+        MFMA kernel's shapes, else MIOpen"""
         w = m.weight
         co, ci, ks, _ = w.shape
+        if (self.conv3_gemm and m.padding == (0, 0) and m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1
+                and x.shape[2] == ks and x.shape[3] == ks and x.dtype == torch.float16 and w.dtype == torch.float16
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and w.is_contiguous(memory_format=torch.channels_last)):
+            # [B, ks*ks*ci] x [co, ks*ks*ci]^T with K ordered (ky, kx, c): both operands are views of the
+            # channels_last storage; autograd's GEMMs give the data and weight gradients
+            B = x.shape[0]
+            y = F.linear(x.permute(0, 2, 3, 1).reshape(B, -1), w.permute(0, 2, 3, 1).reshape(co, -1))
+            return y.view(B, co, 1, 1)
         if (self.hip_conv and (ci, co, ks) in self._OWN_CONV and w.dtype == torch.float16 and x.dtype == torch.float16
                 and m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding[0] == m.padding[1]
                 and m.padding[0] < ks and x.is_contiguous(memory_format=torch.channels_last)

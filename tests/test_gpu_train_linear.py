@@ -239,6 +239,32 @@ def test_training_forward_convs_take_hip_conv():
     assert calls == [(128, 128, 3, 3), (128, 128, 3, 3), (256, 128, 2, 2), (256, 256, 2, 2), (256, 256, 2, 2)], calls
 
 
+def test_conv3_as_gemm_matches_conv():
+    """SCRIMPNet._conv_nobias on conv3 (3x3 over a 3x3 input, no padding: one output pixel) is a GEMM over
+    the channels_last views, K ordered (ky, kx, c): output, data and weight gradients match F.conv2d's
+    to fp16 rounding of another summation order"""
+    from mapf_amd.net import SCRIMPNet
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(9)
+    cl = torch.channels_last
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9)
+    x0 = torch.randn(96, 256, 3, 3, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    w0 = (torch.randn(500, 256, 3, 3, device="cuda", generator=g) / 48).half().contiguous(memory_format=cl)
+    gy = torch.randn(96, 500, 1, 1, device="cuda", generator=g).half()
+    res = []
+    for gemm in (True, False):
+        x, w = x0.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+        mm = type("M", (), {"weight": w, "padding": (0, 0), "stride": (1, 1), "dilation": (1, 1), "groups": 1})()
+        y = net._conv_nobias(x, mm) if gemm else torch.nn.functional.conv2d(x, w, None, 1, 0)
+        y.backward(gy)
+        res.append((y.detach().float().reshape(96, 500), x.grad.float(), w.grad.float()))
+    for k, (a, r) in enumerate(zip(*res)):
+        rel = ((a - r).norm() / r.norm()).item()
+        print(f"conv3 as GEMM: {('y', 'dx', 'dw')[k]} relative {rel:.2e}")
+        assert rel < 2e-3, (k, rel)
+
+
 def _seed(v=12345):
     return torch.tensor([v], dtype=torch.int64, device="cuda")
 
@@ -349,10 +375,15 @@ def test_training_forward_fused_residuals_equal_unfused():
         _Encoder.fused_train = True
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
     # the same operations and rounding points; torch's GELU kernels may round their exp / erf in the last
-    # bit differently (test_gelu_dropout_matches_torch), which moves the outputs by fp16 ulps
+    # bit differently (test_gelu_dropout_matches_torch), which moves the outputs by fp16 ulps; those ulps pass
+    # through two transformer layers and the LSTM, so a near-zero output can sit 2-4 ulps (of 1.0) away:
+    # elementwise 4e-3 absolute, and the whole output within 5e-3 relative norm
     for a, r in zip(res[0][0], res[1][0]):
-        print(f"output: max |diff| {(a - r).abs().max().item():.3e}, bit-identical {(a == r).float().mean().item():.4%}")
-        torch.testing.assert_close(a, r, rtol=1e-2, atol=2e-3)
+        rel = ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
+        print(f"output: max |diff| {(a - r).abs().max().item():.3e}, bit-identical {(a == r).float().mean().item():.4%}, "
+              f"rel norm {rel:.2e}")
+        torch.testing.assert_close(a, r, rtol=1e-2, atol=4e-3)
+        assert rel < 5e-3, rel
     assert len(res[0][1]) == len(res[1][1])
     for a, r in zip(res[0][1], res[1][1]):
         rel = ((a - r).norm() / r.norm().clamp_min(1e-30)).item()

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--split", type=int, default=None, help="net._SplitKLinear.SPLIT (row chunks)")
     ap.add_argument("--fp16-partials", action="store_true", help="split weight gradients with fp16 partials")
+    ap.add_argument("--ab", default=None,
+                    help="A/B a SCRIMPNet class switch (e.g. conv3_gemm, hip_conv): captured updates with it on / off, "
+                         "alternating, each a fresh capture; prints one JSON line and exits")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from mapf_amd.config import EnvParameters, make_config
@@ -50,6 +53,26 @@ def main():
     def upd():
         return model.train(sl("observations"), sl("vectors"), sl("returns"), sl("costReturns"), sl("values"),
                            sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
+    import json
+    if args.ab:
+        from mapf_amd.net import SCRIMPNet
+        assert isinstance(getattr(SCRIMPNet, args.ab), bool), args.ab
+        ab = {}
+        for on in (True, False, True, False, True, False):
+            setattr(SCRIMPNet, args.ab, on)
+            model._updates.clear()                 # a fresh capture with the switch in its new position
+            for _ in range(3):
+                upd()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(args.updates):
+                t0 = time.perf_counter()
+                upd()
+                ts.append(time.perf_counter() - t0)
+            ab.setdefault(str(on), []).append(round(float(np.median(ts)) * 1e3, 3))
+            print(f"{args.ab}={on}: median {np.median(ts) * 1e3:.3f} ms", flush=True)
+        print(json.dumps({"rows": args.rows, "agents": N, "ab": args.ab, "median_ms": ab}), flush=True)
+        return
     res = {}
     for mode in ("graph", "eager", "graph"):      # Model.graph_update: one captured hipGraph per update
         model.graph_update = mode == "graph"
@@ -64,7 +87,6 @@ def main():
         res.setdefault(mode, []).append(float(np.median(ts)) * 1e3)
         print(f"update ({mode}): median {np.median(ts) * 1e3:.2f} ms, mean {np.mean(ts) * 1e3:.2f} ms for "
               f"{args.rows} x {N} rows", flush=True)
-    import json
     print(json.dumps({"rows": args.rows, "agents": N, "median_ms": res}), flush=True)
     if args.no_profile:
         return
