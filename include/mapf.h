@@ -396,6 +396,14 @@ int mapf_cast_f32_to_f16_multi(const float *const *src, uint16_t *const *dst, co
                                void *stream);
 int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, const int64_t *n, int32_t count,
                                void *stream);
+/* mapf_cast_f32_to_f16_multi where entry i with cout[i] > 0 is a conv weight stored [Cout][ks][ks][Cin]
+ * (channels_last [Cout][Cin][ks][ks], Cout = cout[i], ks = ks[i], Cin = n[i] / (Cout ks ks)) written as
+ * its flipped, transposed copy [Cin][ks][ks][Cout]: dst[ci][ky][kx][co] = src[co][ks-1-ky][ks-1-kx][ci]
+ * -- the weight of the data gradient dx = conv(dy, w flipped, transposed) (_HipConv) -- in the same launch
+ * as the plain casts (cout[i] == 0).  cout / ks: HOST int32 arrays.  MAPF_EINVAL as above or when n[i]
+ * is not a multiple of Cout ks ks. */
+int mapf_cast_f32_to_f16_multi_flip(const float *const *src, uint16_t *const *dst, const int64_t *n,
+                                    const int32_t *cout, const int32_t *ks, int32_t count, void *stream);
 /* Backward of z = fp16(LayerNorm(x)) (mapf_layernorm_f16; the training forward's PreNorm,
  * transformer.py:7-24 under autocast): given dz fp16 [rows][512], dx fp32 [rows][512] (contiguous),
  * dgamma / dbeta fp32 [512] (sums over the rows, fixed order).  mean / rstd are recomputed from x as
@@ -441,6 +449,21 @@ int mapf_tokens(float *x, const float *A, const uint16_t *VV, const float *cls, 
 int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos, int64_t B,
                           int32_t L, int32_t D, float p, uint64_t seed, const float *gamma, const float *beta,
                           float eps, uint16_t *z, void *stream);
+/* The TRAINING forward's tokens and the first PreNorm (net._TokensLN; SCRIMPNet.forward, net.py:124-130):
+ * x = dropout(cat(cls, A * VV) + pos) fp32 [B][L + 1][512] -- torch's ops and roundings (the product and
+ * the sum rounded separately), dropout x * 1 / (1 - p) where kept, the mask from the device seed (graph-safe,
+ * as mapf_dropout_residual_layernorm_train) -- and z = fp16(LayerNorm(x)) in one pass.  A: fp32 [B][L]
+ * (the tokeniser's softmax), VV: fp16 [B][512], cls: fp32 [512], pos: fp32 [L + 1][512].  L == 16. */
+int mapf_tokens_layernorm_train(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos,
+                                int64_t B, int32_t L, float p, const uint64_t *seed_dev, uint32_t salt, const float *gamma,
+                                const float *beta, float eps, uint16_t *z, void *stream);
+/* Its backward after LayerNorm's (mapf_layernorm_bwd_f16 with the residual's gradient as dres): given
+ * dx fp32 [B][L + 1][512], the same mask: g = dx / (1 - p) where kept; dA fp32 [B][L] = sum over the
+ * columns of g[.][t + 1] VV; dVV fp16 [B][512] = sum over t of g[.][t + 1] A[.][t]; dpos fp32 [L + 1][512]
+ * and dcls fp32 [512] the sums of g over B (fixed order).  work: 256 * (L + 1) * 512 floats. */
+int mapf_tokens_train_bwd(const float *dx, const float *A, const uint16_t *VV, float *dA, uint16_t *dVV, float *dpos,
+                          float *dcls, float *work, int64_t B, int32_t L, float p, const uint64_t *seed_dev,
+                          uint32_t salt, void *stream);
 /* Row tiles per workgroup of the mapf_linear512_* kernels (process-wide; bit-identical results
  * either way, for A/B timing): 2 (128 rows share each staged 512 x 32 weight chunk), 1 (64 rows),
  * or 0 (default: 1, the faster or within 1 % for every form at the c3 shape, round 5).  MAPF_EINVAL

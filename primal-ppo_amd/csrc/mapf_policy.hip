@@ -537,6 +537,7 @@ struct CastList {
     void *dst[CAST_MAX];
     long n[CAST_MAX];
     int blk0[CAST_MAX + 1];                                 // first block of tensor i; blk0[count] = grid
+    int cout[CAST_MAX], ks[CAST_MAX];                       // cout > 0: the flipped, transposed conv weight
     int count;
 };
 template <bool TO_F16>
@@ -545,23 +546,39 @@ __global__ __launch_bounds__(256) void cast_multi(CastList L) {
     int t = 0;
     while (t + 1 < L.count && L.blk0[t + 1] <= b) ++t;      // uniform scan over <= 64 entries
     const long base = (long)(b - L.blk0[t]) * CAST_PER_BLOCK, n = L.n[t];
+    const int co = TO_F16 ? L.cout[t] : 0, ks = TO_F16 ? L.ks[t] : 1;
     for (int e = (int)threadIdx.x; e < CAST_PER_BLOCK; e += 256) {
         const long i = base + e;
         if (i >= n) break;
-        if (TO_F16)
-            static_cast<uint16_t *>(L.dst[t])[i] = (uint16_t)f2h(static_cast<const float *>(L.src[t])[i]);
-        else
+        if (TO_F16) {
+            long j = i;
+            if (co > 0) {       // dst [Cin][ky][kx][Cout] = src [Cout][ks-1-ky][ks-1-kx][Cin] (channels_last storage)
+                const int cin = (int)(n / ((long)co * ks * ks));
+                const int o = (int)(i % co);
+                long r = i / co;
+                const int kx = (int)(r % ks);
+                r /= ks;
+                const int ky = (int)(r % ks), ci = (int)(r / ks);
+                j = (((long)o * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)) * cin + ci;
+            }
+            static_cast<uint16_t *>(L.dst[t])[i] = (uint16_t)f2h(static_cast<const float *>(L.src[t])[j]);
+        } else {
             static_cast<float *>(L.dst[t])[i] = h2f(static_cast<const uint16_t *>(L.src[t])[i]);
+        }
     }
 }
 
 template <bool TO_F16>
-static int cast_multi_api(const void *const *src, void *const *dst, const int64_t *n, int32_t count, void *stream) {
-    if (!src || !dst || !n || count < 0 || count > CAST_MAX) return MAPF_EINVAL;
+static int cast_multi_api(const void *const *src, void *const *dst, const int64_t *n, int32_t count, void *stream,
+                          const int32_t *cout = nullptr, const int32_t *ks = nullptr) {
+    if (!src || !dst || !n || count < 0 || count > CAST_MAX || (!cout) != (!ks)) return MAPF_EINVAL;
     CastList L{};
     long blocks = 0;
     for (int i = 0; i < count; ++i) {
         if (n[i] < 0 || (n[i] > 0 && (!src[i] || !dst[i]))) return MAPF_EINVAL;
+        if (cout && cout[i] > 0 && (ks[i] <= 0 || n[i] % ((int64_t)cout[i] * ks[i] * ks[i]))) return MAPF_EINVAL;
+        L.cout[i] = cout && cout[i] > 0 ? cout[i] : 0;
+        L.ks[i] = cout && cout[i] > 0 ? ks[i] : 1;
         L.src[i] = src[i];
         L.dst[i] = dst[i];
         L.n[i] = (long)n[i];
@@ -784,6 +801,187 @@ __global__ __launch_bounds__(256) void tokens_layernorm(float *__restrict__ x, c
         }
     }
     ln_rows<R>(av, cv, live, lane, gamma, beta, eps, zr);
+}
+
+// ---- the TRAINING forward's tokens (net._TokensLN; SCRIMPNet.forward's tokeniser, net.py:124-130) ----
+// x = dropout(cat(cls, A * VV) + pos) fp32 as torch's ops compute it -- the product and the sum rounded
+// separately (no contraction), the dropout as x * scale where kept -- with the mask from the device seed
+// (dev_seed: graph-safe), and z = fp16(LayerNorm(x)).  A: [B][16] fp32, VV: [B][512] fp16.
+constexpr int TOK_L = 16, TOK_T = TOK_L + 1;
+__device__ inline float4 token4_train(const float *__restrict__ A, const uint16_t *__restrict__ VV,
+                                      const float *__restrict__ cls, const float *__restrict__ pos, long b, int t,
+                                      int d4, long i, uint32_t thr, float scale, uint64_t seed) {
+    const float4 pp = reinterpret_cast<const float4 *>(pos + (long)t * 512)[d4];
+    float4 v;
+    if (t == 0) {
+        const float4 c = reinterpret_cast<const float4 *>(cls)[d4];
+        v = make_float4(__fadd_rn(c.x, pp.x), __fadd_rn(c.y, pp.y), __fadd_rn(c.z, pp.z), __fadd_rn(c.w, pp.w));
+    } else {
+        const float a = A[b * TOK_L + t - 1];
+        const uint2 w = reinterpret_cast<const uint2 *>(VV + b * 512)[d4];
+        v = make_float4(__fadd_rn(__fmul_rn(a, h2f(w.x)), pp.x), __fadd_rn(__fmul_rn(a, h2f(w.x >> 16)), pp.y),
+                        __fadd_rn(__fmul_rn(a, h2f(w.y)), pp.z), __fadd_rn(__fmul_rn(a, h2f(w.y >> 16)), pp.w));
+    }
+    if (thr) {
+        const unsigned k = keep4(seed, (uint64_t)i, thr);
+        v.x = (k & 1u) ? __fmul_rn(v.x, scale) : 0.f;
+        v.y = (k & 2u) ? __fmul_rn(v.y, scale) : 0.f;
+        v.z = (k & 4u) ? __fmul_rn(v.z, scale) : 0.f;
+        v.w = (k & 8u) ? __fmul_rn(v.w, scale) : 0.f;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void tokens_ln_train(float *__restrict__ x, const float *__restrict__ A,
+                                                       const uint16_t *__restrict__ VV, const float *__restrict__ cls,
+                                                       const float *__restrict__ pos, long B, uint32_t thr, float scale,
+                                                       const uint64_t *__restrict__ seedp, uint32_t salt,
+                                                       const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                       float eps, uint16_t *__restrict__ z) {
+    constexpr int R = 4;                                    // four rows per wave, 16 per block (tokens_layernorm)
+    const int lane = (int)(threadIdx.x & 63);
+    const long rows = B * TOK_T;
+    const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+    if (row0 >= rows) return;
+    const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+    float4 av[R], cv[R];
+    bool live[R];
+    uint16_t *zr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const long row = row0 + r;
+        live[r] = row < rows;
+        zr[r] = z + (live[r] ? row : 0) * 512;
+        if (!live[r]) {
+            av[r] = cv[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            continue;
+        }
+        const long b = row / TOK_T;
+        const int t = (int)(row - b * TOK_T);
+        av[r] = token4_train(A, VV, cls, pos, b, t, lane, row * 128 + lane, thr, scale, seed);
+        cv[r] = token4_train(A, VV, cls, pos, b, t, 64 + lane, row * 128 + 64 + lane, thr, scale, seed);
+        float4 *xr = reinterpret_cast<float4 *>(x) + row * 128;
+        xr[lane] = av[r];
+        xr[64 + lane] = cv[r];
+    }
+    ln_rows<R>(av, cv, live, lane, gamma, beta, eps, zr);
+}
+
+// backward of tokens_ln_train's tokens, given dx = dL/dx fp32 [B][17][512] (LayerNorm's backward with the
+// residual's gradient already added): g = dx * scale where the forward kept, else 0 (torch's dropout
+// backward); dA[b][t] = sum_c g[b][t+1][c] VV[b][c] (fp32); dVV[b][c] = fp16(sum_t g[b][t+1][c] A[b][t]), the
+// products rounded before the sums as torch's mul then sum; and per-block partial sums of g over the block's
+// sequences (dpos; its token-0 row is dcls) for tokens_bwd_colsum, in a fixed order.  256 threads per block,
+// 2 columns each; sequences two at a time (both rows' 34 loads in flight).
+__device__ inline void tok_bwd_row(const float *__restrict__ dx, long b, int c0, uint32_t thr, float scale,
+                                   uint64_t seed, float2 (&g)[TOK_T]) {
+#pragma unroll
+    for (int t = 0; t < TOK_T; ++t) g[t] = *reinterpret_cast<const float2 *>(dx + (b * TOK_T + t) * 512 + c0);
+    if (thr) {
+#pragma unroll
+        for (int t = 0; t < TOK_T; ++t) {
+            const long i = (b * TOK_T + t) * 512 + c0;
+            const unsigned k = keep4(seed, (uint64_t)(i >> 2), thr) >> (c0 & 3);
+            g[t].x = (k & 1u) ? __fmul_rn(g[t].x, scale) : 0.f;
+            g[t].y = (k & 2u) ? __fmul_rn(g[t].y, scale) : 0.f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void tokens_train_bwd(const float *__restrict__ dx, const float *__restrict__ A,
+                                                        const uint16_t *__restrict__ VV, long B, int per, uint32_t thr,
+                                                        float scale, const uint64_t *__restrict__ seedp, uint32_t salt,
+                                                        float *__restrict__ dA, uint16_t *__restrict__ dVV,
+                                                        float *__restrict__ part) {
+    __shared__ float red[2][4][TOK_L];
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6, c0 = 2 * tid;
+    const uint64_t seed = thr ? dev_seed(seedp, salt) : 0;
+    float2 acc[TOK_T];
+#pragma unroll
+    for (int t = 0; t < TOK_T; ++t) acc[t] = make_float2(0.f, 0.f);
+    const long b0 = (long)blockIdx.x * per, b1 = b0 + per < B ? b0 + per : B;
+    for (long b = b0; b < b1; b += 2) {
+        const int nb = b + 1 < b1 ? 2 : 1;
+        float2 g[2][TOK_T];
+        tok_bwd_row(dx, b, c0, thr, scale, seed, g[0]);
+        if (nb == 2) tok_bwd_row(dx, b + 1, c0, thr, scale, seed, g[1]);
+        float pa[2][TOK_L];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (q >= nb) {
+#pragma unroll
+                for (int t = 0; t < TOK_L; ++t) pa[q][t] = 0.f;
+                continue;
+            }
+            const long bb = b + q;
+#pragma unroll
+            for (int t = 0; t < TOK_T; ++t) {               // dpos partials in sequence order
+                acc[t].x += g[q][t].x;
+                acc[t].y += g[q][t].y;
+            }
+            const uint32_t vv = *reinterpret_cast<const uint32_t *>(VV + bb * 512 + c0);
+            const float v0 = h2f(vv & 0xFFFFu), v1 = h2f(vv >> 16);
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TOK_L; ++t) {
+                const float a = A[bb * TOK_L + t];
+                s0 = __fadd_rn(s0, __fmul_rn(g[q][t + 1].x, a));
+                s1 = __fadd_rn(s1, __fmul_rn(g[q][t + 1].y, a));
+                pa[q][t] = __fadd_rn(__fmul_rn(g[q][t + 1].x, v0), __fmul_rn(g[q][t + 1].y, v1));
+            }
+            *reinterpret_cast<uint32_t *>(dVV + bb * 512 + c0) = (uint32_t)f2h(s0) | ((uint32_t)f2h(s1) << 16);
+        }
+        // dA: 2 x 16 sums over the 512 columns -- interleaved wave reductions, then the 4 waves in order
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int t = 0; t < TOK_L; ++t) pa[q][t] += __shfl_xor(pa[q][t], s, 64);
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int t = 0; t < TOK_L; ++t) red[q][wv][t] = pa[q][t];
+        }
+        __syncthreads();
+        if (tid < 2 * TOK_L && tid / TOK_L < nb) {
+            const int q = tid / TOK_L, t = tid % TOK_L;
+            dA[(b + q) * TOK_L + t] = (red[q][0][t] + red[q][1][t]) + (red[q][2][t] + red[q][3][t]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int t = 0; t < TOK_T; ++t)
+        *reinterpret_cast<float2 *>(part + ((long)blockIdx.x * TOK_T + t) * 512 + c0) = acc[t];
+}
+
+// dpos[c] = sum_g part[g][c] over G partial rows in a fixed order (colsum_to_f16's, fp32 out); dcls = its
+// first 512 columns (the cls token's gradient: token 0's)
+__global__ __launch_bounds__(256) void tokens_bwd_colsum(const float *__restrict__ part, int G, int C,
+                                                         float *__restrict__ dpos, float *__restrict__ dcls) {
+    __shared__ float sl[8][32];
+    const int t = (int)threadIdx.x, cl = t & 31, slice = t >> 5;
+    const int c = (int)blockIdx.x * 32 + cl;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
+        const int per = (G + 7) / 8, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
+        int gi = g0;
+        for (; gi + 4 <= g1; gi += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += part[(long)(gi + u) * C + c];
+        }
+        for (; gi < g1; ++gi) acc[0] += part[(long)gi * C + c];
+    }
+    sl[slice][cl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (slice == 0 && c < C) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v += sl[k][cl];
+        dpos[c] = v;
+        if (c < 512) dcls[c] = v;
+    }
 }
 
 // ---- attention over a short token axis (transformer.py:48-85; n <= 32 tokens) -----
@@ -1618,6 +1816,13 @@ int mapf_cast_f32_to_f16_multi(const float *const *src, uint16_t *const *dst, co
                                      n, count, stream);
 }
 
+int mapf_cast_f32_to_f16_multi_flip(const float *const *src, uint16_t *const *dst, const int64_t *n,
+                                    const int32_t *cout, const int32_t *ks, int32_t count, void *stream) {
+    if (!cout || !ks) return MAPF_EINVAL;
+    return pol::cast_multi_api<true>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst),
+                                     n, count, stream, cout, ks);
+}
+
 int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, const int64_t *n, int32_t count,
                                void *stream) {
     return pol::cast_multi_api<false>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst), n,
@@ -1850,6 +2055,39 @@ int mapf_tokens_layernorm(float *x, const float *A, const uint16_t *VV, const fl
     hipLaunchKernelGGL(pol::tokens_layernorm, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, (hipStream_t)stream, x, A,
                        VV, cls, pos, (long)B, (int)L, pol::drop_threshold(p), 1.f / (1.f - p), seed, gamma, beta, eps,
                        z);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_tokens_layernorm_train(float *x, const float *A, const uint16_t *VV, const float *cls, const float *pos,
+                                int64_t B, int32_t L, float p, const uint64_t *seed_dev, uint32_t salt, const float *gamma,
+                                const float *beta, float eps, uint16_t *z, void *stream) {
+    if (!x || !A || !VV || !cls || !pos || !seed_dev || !gamma || !beta || !z || B < 0 || L != pol::TOK_L ||
+        !(p >= 0.f && p < 1.f) ||
+        (((uintptr_t)x | (uintptr_t)cls | (uintptr_t)pos | (uintptr_t)gamma | (uintptr_t)beta) & 15) ||
+        (((uintptr_t)VV | (uintptr_t)z) & 7))
+        return MAPF_EINVAL;
+    if (B == 0) return MAPF_OK;
+    const long rows = (long)B * pol::TOK_T;
+    hipLaunchKernelGGL(pol::tokens_ln_train, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, (hipStream_t)stream, x,
+                       A, VV, cls, pos, (long)B, pol::drop_threshold(p), 1.f / (1.f - p), seed_dev, salt, gamma, beta,
+                       eps, z);
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+int mapf_tokens_train_bwd(const float *dx, const float *A, const uint16_t *VV, float *dA, uint16_t *dVV, float *dpos,
+                          float *dcls, float *work, int64_t B, int32_t L, float p, const uint64_t *seed_dev,
+                          uint32_t salt, void *stream) {
+    if (!dx || !A || !VV || !dA || !dVV || !dpos || !dcls || !work || !seed_dev || B < 0 || L != pol::TOK_L ||
+        !(p >= 0.f && p < 1.f) || (((uintptr_t)dx | (uintptr_t)work) & 7) || (((uintptr_t)VV | (uintptr_t)dVV) & 3))
+        return MAPF_EINVAL;
+    constexpr int C = pol::TOK_T * 512;
+    const long per = B > 0 ? (B + 255) / 256 : 1;
+    const int G = (int)((B + per - 1) / per);
+    if (G > 0)
+        hipLaunchKernelGGL(pol::tokens_train_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, dx, A, VV,
+                           (long)B, (int)per, pol::drop_threshold(p), 1.f / (1.f - p), seed_dev, salt, dA, dVV, work);
+    hipLaunchKernelGGL(pol::tokens_bwd_colsum, dim3((unsigned)(C / 32)), dim3(256), 0, (hipStream_t)stream, work, G, C,
+                       dpos, dcls);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 

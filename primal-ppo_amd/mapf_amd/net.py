@@ -111,19 +111,39 @@ class _CastParams(torch.autograd.Function):
         return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 
     @staticmethod
-    def forward(ctx, *params):
+    def forward(ctx, flips, *params):
+        """flips: indices of channels_last conv weights whose flipped, transposed fp16 copy ([Cin][Cout][ks][ks],
+        channels_last: _HipConv's data-gradient weight) is returned too, after the plain copies, from the
+        same launch (mapf_cast_f32_to_f16_multi_flip); those copies carry no gradient"""
         from . import _lib
         ctx.set_materialize_grads(False)
         assert all(_CastParams.dense(p) for p in params)
         ctx.layouts = [(p.shape, p.stride()) for p in params]
         outs = [torch.empty_strided(p.shape, p.stride(), dtype=torch.float16, device=p.device) for p in params]
         st = ctypes.c_void_p(torch.cuda.current_stream(params[0].device).cuda_stream)
-        _cast_multi(_lib.lib().mapf_cast_f32_to_f16_multi, params, outs, st)
-        return tuple(outs)
+        if not flips:
+            _cast_multi(_lib.lib().mapf_cast_f32_to_f16_multi, params, outs, st)
+            return tuple(outs)
+        fl = [params[i] for i in flips]
+        assert all(w.dim() == 4 and w.shape[2] == w.shape[3] and w.is_contiguous(memory_format=torch.channels_last)
+                   for w in fl)
+        wts = [torch.empty((w.shape[1], w.shape[0], w.shape[2], w.shape[3]), dtype=torch.float16, device=w.device,
+                           memory_format=torch.channels_last) for w in fl]
+        src, dst = list(params) + fl, outs + wts
+        k = len(src)
+        arr = lambda ts: (ctypes.c_void_p * k)(*[t.data_ptr() for t in ts])  # noqa: E731
+        co = (ctypes.c_int32 * k)(*([0] * len(params) + [w.shape[0] for w in fl]))
+        kk = (ctypes.c_int32 * k)(*([0] * len(params) + [w.shape[2] for w in fl]))
+        _lib.check(_lib.lib().mapf_cast_f32_to_f16_multi_flip(arr(src), arr(dst),
+                                                              (ctypes.c_int64 * k)(*[t.numel() for t in src]),
+                                                              co, kk, k, st))
+        ctx.mark_non_differentiable(*wts)
+        return tuple(outs + wts)
 
     @staticmethod
     def backward(ctx, *grads):
         from . import _lib
+        grads = grads[:len(ctx.layouts)]                 # the flipped copies carry none
         live = [i for i, g in enumerate(grads) if g is not None]
         outs = [None] * len(grads)
         if live:
@@ -139,7 +159,7 @@ class _CastParams(torch.autograd.Function):
             _cast_multi(_lib.lib().mapf_cast_f16_to_f32_multi, src, dst, st)
             for i, d in zip(live, dst):
                 outs[i] = d
-        return tuple(outs)
+        return (None,) + tuple(outs)
 
 
 class _BiasReLU(torch.autograd.Function):
@@ -222,28 +242,41 @@ class _HipConv(torch.autograd.Function):
     gradient (0.28 + 0.48 ms of a 256 x 8-row update, profiles/r06_update_profile_c3.txt)."""
 
     @staticmethod
-    def forward(ctx, x, w, pad):
+    def forward(ctx, x, w, pad, b=None, wt=None):
         from . import _lib
         B, Cin, H, W = x.shape
         Cout, _, ks, _ = w.shape
         y = torch.empty((B, Cout, H + 2 * pad - ks + 1, W + 2 * pad - ks + 1), dtype=torch.float16, device=x.device,
                         memory_format=torch.channels_last)
         st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-        # a channels_last [Cout][Cin][ks][ks] weight is [Cout][ks][ks][Cin] in memory: the kernel's packed form
-        _lib.check(_lib.lib().mapf_conv_nhwc_f16(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()), None,
-                                                 ctypes.c_void_p(y.data_ptr()), B, H, W, Cin, Cout, ks, pad, 0, st))
-        ctx.save_for_backward(x, w)
+        # a channels_last [Cout][Cin][ks][ks] weight is [Cout][ks][ks][Cin] in memory: the kernel's packed form;
+        # with b: relu(fp16(fp16(acc) + b)) in the epilogue, what _BiasReLU's pass writes
+        bp = None if b is None else ctypes.c_void_p(b.data_ptr())
+        _lib.check(_lib.lib().mapf_conv_nhwc_f16(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()), bp,
+                                                 ctypes.c_void_p(y.data_ptr()), B, H, W, Cin, Cout, ks, pad,
+                                                 0 if b is None else 1, st))
+        ctx.save_for_backward(x, w, None if b is None else y, wt)
         ctx.pad = pad
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from . import _lib
-        x, w = ctx.saved_tensors
+        x, w, y, wt = ctx.saved_tensors
         pad = ctx.pad
         B, Cin, H, W = x.shape
         Cout, _, ks, _ = w.shape
         dy = dy.contiguous(memory_format=torch.channels_last)
+        db = None
+        if y is not None:                       # the fused bias + ReLU: _BiasReLU's backward first
+            rows = y.numel() // Cout
+            dyr = torch.empty_like(y)
+            db = torch.empty(Cout, dtype=torch.float16, device=y.device)
+            work = torch.empty(512 * Cout, dtype=torch.float32, device=y.device)
+            st = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
+            p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+            _lib.check(_lib.lib().mapf_relu_bias_bwd_f16(p(y), p(dy), p(dyr), p(db), p(work), rows, Cout, st))
+            dy = dyr
         own_dx = ctx.needs_input_grad[0] and (Cout, Cin, ks) in SCRIMPNet._OWN_CONV
         mask = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], False]
         dx = dw = None
@@ -253,13 +286,72 @@ class _HipConv(torch.autograd.Function):
             dx = gx if mask[0] else None
             dw = gw if mask[1] else None
         if own_dx:
-            wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)   # [Cin][ks][ks][Cout]
+            if wt is None:                      # else _CastParams made it (SCRIMPNet._flip_names)
+                wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)  # [Cin][ks][ks][Cout]
             dx = torch.empty(x.shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
             st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
             _lib.check(_lib.lib().mapf_conv_nhwc_f16(ctypes.c_void_p(dy.data_ptr()), ctypes.c_void_p(wt.data_ptr()), None,
                                                      ctypes.c_void_p(dx.data_ptr()), B, dy.shape[2], dy.shape[3], Cout,
                                                      Cin, ks, ks - 1 - pad, 0, st))
-        return dx, dw, None
+        return dx, dw, None, db, None
+
+
+class _TokensLN(torch.autograd.Function):
+    """The TRAINING forward's tokeniser tail and the first PreNorm in one pass (round 6):
+    x = dropout(cat(cls, A * VV) + pos) fp32, z = fp16(LayerNorm(x)) -- mapf_tokens_layernorm_train, the
+    ops and roundings of SCRIMPNet.forward's torch chain (net.py:124-130, transformer.py:7-24; the mask is
+    the kernels' counter hash from the device seed, salt 32).  Backward: LayerNorm's with the residual's
+    gradient (mapf_layernorm_bwd_f16), then mapf_tokens_train_bwd: the dropout mask, dA, dVV (fp16) and the
+    sums over the batch for pos and cls.  In place of torch's mul, cat, add, dropout, LayerNorm launches and
+    their backward's mul / sum / masked-scale passes (~0.29 ms of a 256 x 8-row update,
+    profiles/r06n_update_shapes.txt).  A: fp32 [B, 16]; VV: fp16 [B, 512]; returns (z [B, 17, 512] fp16,
+    x [B, 17, 512] fp32: the first block's residual)."""
+
+    @staticmethod
+    def forward(ctx, A, VV, cls, pos, weight, bias, eps, p, seed, salt):
+        from . import _lib
+        ctx.set_materialize_grads(False)
+        B = A.shape[0]
+        x = torch.empty(B, 17, 512, dtype=torch.float32, device=A.device)
+        z = torch.empty(B, 17, 512, dtype=torch.float16, device=A.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_tokens_layernorm_train(ptr(x), ptr(A), ptr(VV), ptr(cls), ptr(pos), B, 16, float(p),
+                                                          ptr(seed), int(salt), ptr(weight), ptr(bias), float(eps),
+                                                          ptr(z), st))
+        ctx.save_for_backward(x, A, VV, weight, seed)
+        ctx.eps, ctx.p, ctx.salt, ctx.shapes = float(eps), float(p), int(salt), (cls.shape, pos.shape)
+        return z, x
+
+    @staticmethod
+    def backward(ctx, dz, dres):
+        from . import _lib
+        x, A, VV, weight, seed = ctx.saved_tensors
+        B = A.shape[0]
+        rows = B * 17
+        dev = x.device
+        if dz is None:
+            dz = torch.zeros(rows, 512, dtype=torch.float16, device=dev)
+        dz = dz.reshape(rows, 512).to(torch.float16).contiguous()
+        if dres is not None:
+            dres = dres.reshape(rows, 512).to(torch.float32).contiguous()
+        dx = torch.empty(rows, 512, dtype=torch.float32, device=dev)
+        dg = torch.empty(512, dtype=torch.float32, device=dev)
+        db = torch.empty(512, dtype=torch.float32, device=dev)
+        work = torch.empty(256 * 17 * 512, dtype=torch.float32, device=dev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mapf_layernorm_bwd_f16(ptr(x), 512, ptr(weight), ptr(dz),
+                                                     None if dres is None else ptr(dres), ptr(dx), ptr(dg), ptr(db),
+                                                     ptr(work), rows, 512, ctx.eps, st))
+        dA = torch.empty(B, 16, dtype=torch.float32, device=dev)
+        dVV = torch.empty(B, 512, dtype=torch.float16, device=dev)
+        dpos = torch.empty(17, 512, dtype=torch.float32, device=dev)
+        dcls = torch.empty(512, dtype=torch.float32, device=dev)
+        _lib.check(_lib.lib().mapf_tokens_train_bwd(ptr(dx), ptr(A), ptr(VV), ptr(dA), ptr(dVV), ptr(dpos), ptr(dcls),
+                                                    ptr(work), B, 16, ctx.p, ptr(seed), ctx.salt, st))
+        cs, ps = ctx.shapes
+        return dA, dVV, dcls.view(cs), dpos.view(ps), dg, db, None, None, None, None
 
 
 def _drop_p(m):
@@ -615,13 +707,14 @@ class _Encoder(nn.Module):
                 x.dtype == torch.float32 and x.shape[-1] == 512 and _PreNorm.hip_layernorm and
                 all(pn.fn.norm.elementwise_affine for blk in self.layers for pn in blk))
 
-    def _forward_train_fused(self, x, first_only, seed):
+    def _forward_train_fused(self, x, first_only, seed, start=None):
         """forward() of the training pass with every residual that feeds a LayerNorm as one _DropResLN
         (the residual add, its dropout and the next PreNorm's LayerNorm) and the MLP's GELU + dropout as
         _GeluDropout; the same operations and rounding points, the dropout masks from the kernels'
-        hash (sites salted 2 li, 2 li + 1, 16 + li)"""
+        hash (sites salted 2 li, 2 li + 1, 16 + li).  start: (z, x) -- the first PreNorm's output and its
+        residual made already (_TokensLN); x is then unused."""
         L = len(self.layers)
-        z, res = self.layers[0][0]._norm(x)
+        z, res = self.layers[0][0]._norm(x) if start is None else start
         for li, (att, ff) in enumerate(self.layers):
             a, f = att.fn.fn, ff.fn.fn
             if first_only and li == L - 1:
@@ -705,6 +798,9 @@ class SCRIMPNet(nn.Module):
     hip_bias_relu = True           # training forward: conv bias + ReLU on _BiasReLU (GPU, autocast)
     hip_conv = True                # training forward: the _OWN_CONV layers' convolutions on _HipConv (MFMA)
     conv3_gemm = True              # training forward: a conv whose kernel covers its unpadded input as one GEMM
+    conv_bias_relu = True          # training forward: _HipConv's epilogue adds the bias and applies the ReLU
+    cast_flips = True              # training forward: _HipConv's flipped weights made in _CastParams' launch
+    fused_tokens = True            # training forward: tokens + dropout + first LayerNorm as _TokensLN
 
     def _conv_nobias(self, x, m):
         """conv2d(x, m.weight) without the bias, fp16 NHWC: a plain GEMM where the kernel covers its whole
@@ -722,12 +818,23 @@ class SCRIMPNet(nn.Module):
             B = x.shape[0]
             y = F.linear(x.permute(0, 2, 3, 1).reshape(B, -1), w.permute(0, 2, 3, 1).reshape(co, -1))
             return y.view(B, co, 1, 1)
-        if (self.hip_conv and (ci, co, ks) in self._OWN_CONV and w.dtype == torch.float16 and x.dtype == torch.float16
-                and m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding[0] == m.padding[1]
-                and m.padding[0] < ks and x.is_contiguous(memory_format=torch.channels_last)
-                and w.is_contiguous(memory_format=torch.channels_last) and x.shape[0] > 0):
-            return _HipConv.apply(x, w, m.padding[0])
+        if self._own_conv_ok(x, m):
+            return _HipConv.apply(x, w, m.padding[0], None, self._wt(m))
         return F.conv2d(x, w, None, m.stride, m.padding)
+
+    def _wt(self, m):
+        """m's flipped, transposed fp16 weight from this forward's _CastParams launch, or None"""
+        return self.__dict__.get("_wt16", {}).get(m)
+
+    def _own_conv_ok(self, x, m):
+        """m's convolution of x runs on _HipConv (mapf_conv_nhwc_f16)"""
+        w = m.weight
+        co, ci, ks, _ = w.shape
+        return (self.hip_conv and (ci, co, ks) in self._OWN_CONV and w.dtype == torch.float16
+                and x.dtype == torch.float16 and m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1
+                and m.padding[0] == m.padding[1] and m.padding[0] < ks
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and w.is_contiguous(memory_format=torch.channels_last) and x.shape[0] > 0)
 
     def _conv_relu(self, x, m):
         """F.relu(m(x)) under autocast; on the GPU with grad, the convolution without its bias and
@@ -735,6 +842,9 @@ class SCRIMPNet(nn.Module):
         if (self.hip_bias_relu and x.is_cuda and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda") and
                 m.bias is not None and m.out_channels % 4 == 0 and m.out_channels <= 1024 and
                 m.weight.is_contiguous(memory_format=torch.channels_last)):
+            if self.conv_bias_relu and self._own_conv_ok(x, m):
+                b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
+                return _HipConv.apply(x, m.weight, m.padding[0], b, self._wt(m))
             y = self._conv_nobias(x, m)
             if y.dtype == torch.float16 and y.is_contiguous(memory_format=torch.channels_last) and y.numel() > 0:
                 b = m.bias if m.bias.dtype == torch.float16 else m.bias.to(torch.float16)
@@ -769,6 +879,29 @@ class SCRIMPNet(nn.Module):
             self._cast_names_cache = names
         return names
 
+    def _flip_names(self, names, own):
+        """{conv module name: index in names of its weight} for the layers whose data gradient _HipConv runs
+        on its own kernel (SCRIMPNet._OWN_CONV, channels_last weights): their flipped, transposed fp16 copies
+        come from _CastParams' launch instead of a flip + copy per backward"""
+        if not self.hip_conv:
+            return {}
+        key = tuple(names)
+        cache = self.__dict__.get("_flip_cache")
+        if cache is None or cache[0] != key:
+            out = {}
+            for mn, m in self.named_modules():
+                if isinstance(m, nn.Conv2d) and f"{mn}.weight" in names:
+                    co, ci, ks, ks2 = m.weight.shape
+                    if (ks == ks2 and (ci, co, ks) in self._OWN_CONV and m.stride == (1, 1) and m.groups == 1
+                            and m.dilation == (1, 1)):
+                        out[mn] = names.index(f"{mn}.weight")
+            cache = (key, out)
+            self.__dict__["_flip_cache"] = cache
+        out = cache[1]
+        if not all(own[names[i]].is_contiguous(memory_format=torch.channels_last) for i in out.values()):
+            return {}
+        return out
+
     def _next_train_seed(self, x):
         """The training forward's dropout seed for the fused kernels (_DropResLN, _GeluDropout): an int64
         counter in device memory, incremented on the device by every training forward (so a captured
@@ -799,12 +932,16 @@ class SCRIMPNet(nn.Module):
             # (autocast would cast each weight on use and its ToCopyBackward each gradient)
             names = self._cast_names()
             own = dict(self.named_parameters())
-            p16 = _CastParams.apply(*[own[n] for n in names])
+            flips = self._flip_names(names, own) if self.cast_flips else ()
+            p16 = _CastParams.apply(tuple(flips.values()) if flips else (), *[own[n] for n in names])
             self._in_cast = True
+            # the flipped weights of _HipConv's data gradients, by module (read in _conv_relu / _conv_nobias)
+            self.__dict__["_wt16"] = {self.get_submodule(mn): wt for mn, wt in zip(flips, p16[len(names):])}
             try:
-                return torch.func.functional_call(self, dict(zip(names, p16)), (obs, vector, input_state))
+                return torch.func.functional_call(self, dict(zip(names, p16[:len(names)])), (obs, vector, input_state))
             finally:
                 self._in_cast = False
+                self.__dict__["_wt16"] = {}
         with torch.autocast(device_type=obs.device.type, enabled=obs.device.type == "cuda"):
             n_agents = self.num_agents or EnvParameters.N_AGENTS
             F_ = self.fov or obs.shape[-1]
@@ -828,9 +965,23 @@ class SCRIMPNet(nn.Module):
             A = torch.matmul(h, self.token_wA.sum(0).transpose(0, 1))         # [b, 1, 16]
             A = A.transpose(1, 2).softmax(dim=-1)                             # [b, 16, 1]
             VV = torch.matmul(h, self.token_wV.sum(0))                        # [b, 1, 512]
-            T = A * VV                       # [b, 16, 512]: matmul(A, VV) over a length-1 axis
-            x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
-            x = self.transformer(self.dropout(x), first_only=True, seed=self._next_train_seed(x))
+            seed = self._next_train_seed(h)
+            enc = self.transformer
+            if (seed is not None and self.fused_tokens and enc._train_fused_ok(self.pos_embedding) and
+                    A.dtype == torch.float32 and VV.dtype == torch.float16 and A.shape[1:] == (16, 1) and
+                    VV.shape[1:] == (1, 512) and tuple(self.pos_embedding.shape) == (1, 17, 512) and
+                    self.cls_token.numel() == 512 and self.cls_token.is_contiguous() and
+                    self.pos_embedding.is_contiguous()):
+                # tokens + dropout + the first PreNorm in one launch (_TokensLN)
+                ln = enc.layers[0][0].fn.norm
+                start = _TokensLN.apply(A.reshape(-1, 16).contiguous(), VV.reshape(-1, 512).contiguous(),
+                                        self.cls_token, self.pos_embedding, ln.weight, ln.bias, ln.eps,
+                                        _drop_p(self.dropout), seed, 32)
+                x = enc._forward_train_fused(None, True, seed, start=start)
+            else:
+                T = A * VV                       # [b, 16, 512]: matmul(A, VV) over a length-1 axis
+                x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
+                x = enc(self.dropout(x), first_only=True, seed=seed)
             x = self.nn_same(self.nn_same(x[:, 0]))
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)

@@ -227,16 +227,56 @@ def test_training_forward_convs_take_hip_conv():
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
     net = SCRIMPNet(numChannel=6, num_agents=8, fov=9).cuda().to(memory_format=torch.channels_last)
-    calls = []
+    calls, flipped = [], []
     orig = _HipConv.forward
     try:
-        _HipConv.forward = staticmethod(lambda ctx, x, w, pad: calls.append(tuple(w.shape)) or orig(ctx, x, w, pad))
+        _HipConv.forward = staticmethod(
+            lambda ctx, x, w, pad, b=None, wt=None: calls.append((tuple(w.shape), b is not None))
+            or flipped.append(wt is not None and torch.equal(wt, w.flip(2, 3).transpose(0, 1)))
+            or orig(ctx, x, w, pad, b, wt))
         obs = (torch.rand(4, 8, 6, 9, 9, device="cuda") < 0.3).float()
         out = net(obs, torch.randn(4, 8, 4, device="cuda"))
         out[1].float().sum().backward()
     finally:
         _HipConv.forward = orig
-    assert calls == [(128, 128, 3, 3), (128, 128, 3, 3), (256, 128, 2, 2), (256, 256, 2, 2), (256, 256, 2, 2)], calls
+    # the un-pooled layers take the bias + ReLU in the conv's epilogue (SCRIMPNet.conv_bias_relu)
+    assert calls == [((128, 128, 3, 3), True), ((128, 128, 3, 3), False), ((256, 128, 2, 2), True),
+                     ((256, 256, 2, 2), True), ((256, 256, 2, 2), False)], calls
+    # each carries its flipped, transposed weight from _CastParams' launch (mapf_cast_f32_to_f16_multi_flip)
+    assert flipped == [True] * 5, flipped
+
+
+@pytest.mark.parametrize("cin,cout,ks,pad,hw,b", [(128, 128, 3, 1, 9, 96), (128, 256, 2, 1, 4, 64),
+                                                  (256, 256, 2, 1, 5, 64)])
+def test_hip_conv_bias_relu_epilogue_equals_two_passes(cin, cout, ks, pad, hw, b):
+    """_HipConv with the bias (bias + ReLU in the conv kernel's epilogue; backward: mapf_relu_bias_bwd_f16
+    then the conv's own gradients) == _BiasReLU over _HipConv's raw output: output, data, weight and bias
+    gradients bit-identical (the same roundings: fp16(fp16(acc) + b), the same backward kernels)"""
+    from mapf_amd.net import _BiasReLU, _HipConv
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(3 * cin + cout)
+    cl = torch.channels_last
+    x0 = torch.randn(b, cin, hw, hw, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    w0 = (torch.randn(cout, cin, ks, ks, device="cuda", generator=g) / (cin * ks * ks) ** 0.5).half().contiguous(
+        memory_format=cl)
+    b0 = (torch.randn(cout, device="cuda", generator=g) * 0.3).half()
+    ho = hw + 2 * pad - ks + 1
+    gy = torch.randn(b, cout, ho, ho, device="cuda", generator=g).half().contiguous(memory_format=cl)
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    res = []
+    try:
+        for fused in (True, False):
+            x, w, bb = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+            y = _HipConv.apply(x, w, pad, bb) if fused else _BiasReLU.apply(_HipConv.apply(x, w, pad), bb)
+            y.backward(gy)
+            res.append((y.detach(), x.grad, w.grad, bb.grad))
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    assert (res[0][0] == 0).float().mean().item() > 0.2          # the ReLU clamps a good share
+    for k, (a, r) in enumerate(zip(*res)):
+        assert torch.equal(a, r), ("y", "dx", "dw", "db")[k]
 
 
 def test_conv3_as_gemm_matches_conv():
@@ -312,6 +352,86 @@ def test_drop_res_ln_matches_torch_chain(p, strided):
         else:
             torch.testing.assert_close(a, r, rtol=2e-3, atol=2e-3, msg=str(k))
     assert torch.equal(out[True][3] == 0, out[False][3] == 0) or p == 0     # the gradient dropped where the forward did
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("B", [96, 2048, 301])
+def test_tokens_ln_matches_torch_chain(p, B):
+    """net._TokensLN (tokens + dropout + the first PreNorm, mapf_tokens_layernorm_train; backward
+    mapf_layernorm_bwd_f16 + mapf_tokens_train_bwd) against SCRIMPNet.forward's torch chain -- A * VV, cat
+    with cls, + pos, dropout, then _HipLayerNorm -- given the SAME mask (read back from the kernel's x:
+    exactly 0 where dropped): x and z bit-identical; gradients of A, VV, cls, pos, gamma, beta within fp32
+    summation order (1e-5 relative in norm; dVV, fp16, within 1e-3); keep rate 1 - p +- 0.01.  B = 301: a
+    ragged last block of the backward's per-block sums."""
+    from mapf_amd.net import _HipLayerNorm, _TokensLN
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(B + int(10 * p))
+    A0 = torch.rand(B, 16, device="cuda", generator=g) + 0.5
+    VV0 = torch.randn(B, 512, device="cuda", generator=g).half()
+    cls0 = torch.randn(1, 1, 512, device="cuda", generator=g)
+    pos0 = torch.randn(1, 17, 512, device="cuda", generator=g)
+    w0 = 1 + 0.1 * torch.randn(512, device="cuda", generator=g)
+    b0 = 0.1 * torch.randn(512, device="cuda", generator=g)
+    dz = torch.randn(B, 17, 512, device="cuda", generator=g).half()
+    dres = torch.randn(B, 17, 512, device="cuda", generator=g)
+    res = []
+    for fused in (True, False):
+        A, VV, cls, pos, w, b = (t.clone().requires_grad_(True) for t in (A0, VV0, cls0, pos0, w0, b0))
+        if fused:
+            z, x = _TokensLN.apply(A, VV, cls, pos, w, b, 1e-5, p, _seed(7), 32)
+            keep = x != 0
+        else:
+            T = A.unsqueeze(2) * VV.unsqueeze(1)
+            xt = torch.cat((cls.expand(B, -1, -1), T), dim=1) + pos
+            xt = xt * keep * (1.0 / (1.0 - p)) if p > 0 else xt
+            z, x = _HipLayerNorm.apply(xt, w, b, 1e-5)
+        (z.float() * dz.float()).sum().add_((x * dres).sum()).backward()
+        res.append((x.detach(), z.detach(), A.grad, VV.grad, cls.grad, pos.grad, w.grad, b.grad))
+    if p > 0:
+        assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for k, (a, r) in enumerate(zip(res[0][2:], res[1][2:])):
+        rel = ((a.float() - r.float()).norm() / r.float().norm()).item()
+        assert rel < (1e-3 if k == 1 else 1e-5), (("A", "VV", "cls", "pos", "gamma", "beta")[k], rel)
+
+
+def test_training_forward_takes_tokens_ln():
+    """SCRIMPNet's training forward (GPU, autocast, grad) builds the tokens through _TokensLN, and with
+    SCRIMPNet.fused_tokens off through torch's chain: outputs within fp16 rounding, every gradient within
+    2e-2 (relative norm) -- dropout off (eval), deterministic convolutions"""
+    from mapf_amd.net import SCRIMPNet, _TokensLN
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.manual_seed(1)
+    net = SCRIMPNet(numChannel=6, num_agents=8, fov=9).cuda().to(memory_format=torch.channels_last)
+    net.eval()
+    obs = (torch.rand(16, 8, 6, 9, 9, device="cuda") < 0.3).float()
+    vec = torch.randn(16, 8, 4, device="cuda")
+    calls, res = [], []
+    orig = _TokensLN.forward
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        _TokensLN.forward = staticmethod(lambda ctx, *a: calls.append(a[0].shape) or orig(ctx, *a))
+        for fused in (True, False):
+            SCRIMPNet.fused_tokens = fused
+            net.zero_grad()
+            out = net(obs, vec)
+            (out[1].float().sum() + out[0].float().pow(2).sum()).backward()
+            res.append(([o.detach().float() for o in out], [p.grad.detach().clone() for p in net.parameters()
+                                                              if p.grad is not None]))
+    finally:
+        SCRIMPNet.fused_tokens = True
+        _TokensLN.forward = orig
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    assert calls == [torch.Size([128, 16])], calls
+    for a, r in zip(res[0][0], res[1][0]):
+        torch.testing.assert_close(a, r, rtol=1e-2, atol=4e-3)
+    assert len(res[0][1]) == len(res[1][1])
+    for a, r in zip(res[0][1], res[1][1]):
+        rel = ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
+        assert rel < 2e-2, rel
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ab", default=None,
                     help="A/B a SCRIMPNet class switch (e.g. conv3_gemm, hip_conv): captured updates with it on / off, "
                          "alternating, each a fresh capture; prints one JSON line and exits")
+    ap.add_argument("--shapes", action="store_true", help="profile eager updates grouped by aten op + input shapes")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from mapf_amd.config import EnvParameters, make_config
@@ -91,6 +92,24 @@ def main():
     if args.no_profile:
         return
     from torch.profiler import ProfilerActivity, profile
+    if args.shapes:                                # eager updates: which aten op (and input shapes) runs which kernel
+        model.graph_update = False
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            for _ in range(args.updates):
+                upd()
+            torch.cuda.synchronize()
+        print(prof.key_averages(group_by_input_shape=True).table(
+            sort_by="self_cuda_time_total", row_limit=80, max_name_column_width=40, max_shapes_column_width=110),
+            flush=True)
+        # the small torch ops, every shape: calls per update and device time
+        small = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::sum", "aten::cat",
+                 "aten::mul", "aten::mul_", "aten::div_", "aten::index", "aten::flip", "aten::clone", "aten::zeros",
+                 "aten::relu", "aten::threshold_backward", "aten::sub", "aten::masked_fill_", "aten::where")
+        for e in sorted(prof.key_averages(group_by_input_shape=True), key=lambda e: -e.self_device_time_total):
+            if e.key in small and e.count >= args.updates:
+                print(f"{e.key:24s} {e.count / args.updates:5.1f}/upd {e.self_device_time_total / args.updates:8.1f} us"
+                      f"  {str(e.input_shapes)[:150]}", flush=True)
+        return
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
         for _ in range(args.updates):
             upd()
