@@ -370,8 +370,10 @@ int mapf_nhwc_bias_relu_pool2(const uint16_t *x, const uint16_t *bias, uint16_t 
 int mapf_layernorm_f16(const float *x, int64_t x_row_stride, const float *gamma, const float *beta, uint16_t *y,
                        int64_t rows, int32_t dim, float eps, void *stream);
 /* out[c] = fp16 of the fp32 sum over the rows of g fp16 [rows][C] (fixed order): a linear's bias
- * gradient (the training forward's 17-token linears, net._SplitKLinear).  C % 4 == 0, C <= 4096;
- * work: 512 * C floats of scratch.  rows == 0 zeroes out.  Capturable. */
+ * gradient (the training forward's 17-token linears, net._SplitKLinear; its short 2-D ones,
+ * net._LinearBG).  C % 4 == 0, C <= 4096; work: 512 * C floats of scratch.  rows <= 8192 with C % 8 == 0
+ * and g 16-B aligned: one launch (a block per 32 columns), else per-block partials then their sum.
+ * rows == 0 zeroes out (g may then be NULL).  Capturable. */
 int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows, int32_t C, void *stream);
 /* Backward of p = maxpool2x2(relu(fp16(r + bias))) (mapf_nhwc_bias_relu_pool2's forward from the raw
  * conv output r fp16 NHWC [B][H][W][C]; the training forward's pooled conv layers, net.py:106-111):

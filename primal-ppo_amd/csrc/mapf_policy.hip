@@ -504,6 +504,54 @@ __global__ __launch_bounds__(256) void colsum_partial_f16(const uint16_t *__rest
     }
 }
 
+// column sums of a short fp16 [rows][C] matrix in ONE launch (the bias gradient of the training forward's
+// 2-D linears, rows <= COLSUM_SHORT_ROWS): a block takes 32 columns -- 4 groups of 8 (16-B loads) x 64 row
+// lanes, each lane its rows in order, then the 64 lanes in order (a fixed order: deterministic); fp16 out.
+constexpr long COLSUM_SHORT_ROWS = 8192;
+__global__ __launch_bounds__(256) void colsum_short_f16(const uint16_t *__restrict__ g, long rows, int C,
+                                                        uint16_t *__restrict__ out) {
+    __shared__ float sl[64][33];
+    const int t = (int)threadIdx.x, cg = t & 3, rl = t >> 2;
+    const int c0 = (int)blockIdx.x * 32 + cg * 8;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c0 < C) {
+        long r = rl;
+        constexpr int U = 8;                                // eight rows' loads in flight
+        for (; r + (U - 1) * 64 < rows; r += U * 64) {
+            uint4 v[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) v[q] = *reinterpret_cast<const uint4 *>(g + (r + q * 64) * C + c0);
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a[2 * k] += h2f(w[k] & 0xFFFFu);
+                    a[2 * k + 1] += h2f(w[k] >> 16);
+                }
+            }
+        }
+        for (; r < rows; r += 64) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(g + r * C + c0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[2 * k] += h2f(w[k] & 0xFFFFu);
+                a[2 * k + 1] += h2f(w[k] >> 16);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sl[rl][cg * 8 + k] = a[k];
+    __syncthreads();
+    const int c = (int)blockIdx.x * 32 + t;
+    if (t < 32 && c < C) {
+        float v = 0.f;
+        for (int l = 0; l < 64; ++l) v += sl[l][t];
+        out[c] = (uint16_t)f2h(v);
+    }
+}
+
 // out[c] = fp16(sum_g part[g][c]) over G partial rows in a fixed order (8 slices x 4 chains each)
 __global__ __launch_bounds__(256) void colsum_to_f16(const float *__restrict__ part, int G, int C,
                                                      uint16_t *__restrict__ out) {
@@ -1830,7 +1878,13 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
 }
 
 int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows, int32_t C, void *stream) {
-    if (!g || !out || !work || rows < 0 || C <= 0 || (C & 3) || C > 4096 || ((uintptr_t)g & 7)) return MAPF_EINVAL;
+    if ((!g && rows > 0) || !out || !work || rows < 0 || C <= 0 || (C & 3) || C > 4096 || ((uintptr_t)g & 7))
+        return MAPF_EINVAL;
+    if (rows <= pol::COLSUM_SHORT_ROWS && !(C & 7) && !((uintptr_t)g & 15)) {
+        hipLaunchKernelGGL(pol::colsum_short_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, g,
+                           (long)rows, (int)C, out);
+        return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+    }
     const int per = 256 / ((C < 1024 ? C : 1024) / 4);
     const long need = (rows + per - 1) / per;
     const int G = (int)(need < pol::RB_WG ? need : pol::RB_WG);

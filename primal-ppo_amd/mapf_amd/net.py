@@ -593,14 +593,51 @@ class _SplitKLinear(torch.autograd.Function):
         return gx, gw, gb
 
 
+class _LinearBG(torch.autograd.Function):
+    """F.linear(x, w, b) on fp16 operands for the training forward's short linears (token 0's and the
+    fully connected layers: 2-D, rows < _SplitKLinear.MIN_ROWS): the same addmm forward and the same
+    two GEMMs backward as torch's AddmmBackward, the bias gradient from mapf_colsum_f16's one-launch
+    column sum (fp32, fixed order, rounded to fp16) in place of torch's fp16 reduction (~15 us per layer,
+    8 layers per update: profiles/r06n_update_shapes.txt).  x: fp16 [rows, in] (strided rows allowed)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _lib
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gy.mm(w) if ctx.needs_input_grad[0] else None
+        gw = x.t().mm(gy).t() if ctx.needs_input_grad[1] else None
+        gb = None
+        if ctx.needs_input_grad[2]:
+            n_out = gy.shape[1]
+            gb = torch.empty(n_out, dtype=torch.float16, device=gy.device)
+            work = torch.empty(1 if gy.shape[0] <= 8192 else 512 * n_out, dtype=torch.float32, device=gy.device)
+            st = ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream)
+            _lib.check(_lib.lib().mapf_colsum_f16(ctypes.c_void_p(gy.data_ptr()), ctypes.c_void_p(gb.data_ptr()),
+                                                  ctypes.c_void_p(work.data_ptr()), gy.shape[0], n_out, st))
+        return gx, gw, gb
+
+
 def _train_linear(x, w, b):
     """F.linear(x, w, b) of the training forward: the split weight gradient (_SplitKLinear) when x
-    has many rows (grad enabled, on the GPU), plain autocast F.linear otherwise."""
+    has many rows (grad enabled, on the GPU), _LinearBG for short 2-D fp16 ones, plain autocast F.linear
+    otherwise."""
     rows = x.numel() // x.shape[-1]
-    if (torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda") and
-            rows >= _SplitKLinear.MIN_ROWS and rows % _SplitKLinear.SPLIT == 0 and w.requires_grad):
-        return _SplitKLinear.apply(x, w, b)
+    if torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda"):
+        if rows >= _SplitKLinear.MIN_ROWS and rows % _SplitKLinear.SPLIT == 0 and w.requires_grad:
+            return _SplitKLinear.apply(x, w, b)
+        if (_LinearBG.enabled and x.dim() == 2 and x.dtype == w.dtype == torch.float16 and b is not None and
+                b.dtype == torch.float16 and w.shape[0] % 8 == 0 and 0 < rows <= 8192 and x.stride(1) == 1):
+            return _LinearBG.apply(x, w, b)
     return F.linear(x, w, b)
+
+
+_LinearBG.enabled = True
 
 
 class _SelfAttention(nn.Module):
@@ -653,10 +690,11 @@ class _SelfAttention(nn.Module):
         h = self.heads
         w, bias = self.to_qkv.weight, self.to_qkv.bias
         # x[:, 0] is a 2-D strided view: one GEMM with lda = n*d ([b, 1, d] would run as a slow bmm)
-        q = F.linear(x[:, 0], w[:d], bias[:d])
+        q = _train_linear(x[:, 0], w[:d], bias[:d])
         kv = _train_linear(x, w[d:], bias[d:])
         if self._hip(x, q):
-            return self.nn1(_HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale))
+            att = _HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale)
+            return _train_linear(att.reshape(b, d), self.nn1.weight, self.nn1.bias).view(b, 1, d)
         q = q.view(b, 1, h, d // h).transpose(1, 2)                                             # b, h, 1, dh
         kv = kv.view(b, n, 2, h, d // h).permute(2, 0, 3, 1, 4)                                 # 2, b, h, n, dh
         out = F.scaled_dot_product_attention(q, kv[0], kv[1], scale=self.scale).transpose(1, 2).reshape(b, 1, d)
@@ -959,7 +997,8 @@ class SCRIMPNet(nn.Module):
             x = cr(x, self.conv3).flatten(1)
             g = F.relu(self.fully_connected_1(v))
             x3 = torch.cat((x, g), -1)
-            h = self.fully_connected_3(F.relu(self.fully_connected_2(x3)))
+            fc2, fc3 = self.fully_connected_2, self.fully_connected_3
+            h = _train_linear(F.relu(_train_linear(x3, fc2.weight, fc2.bias)), fc3.weight, fc3.bias)
             h = F.relu(h + x3).unsqueeze(1)                                   # [b, 1, 512]
             # tokeniser (net.py:124-130): sums over the 8 token matrices, softmax over a length-1 axis
             A = torch.matmul(h, self.token_wA.sum(0).transpose(0, 1))         # [b, 1, 16]
@@ -982,7 +1021,8 @@ class SCRIMPNet(nn.Module):
                 T = A * VV                       # [b, 16, 512]: matmul(A, VV) over a length-1 axis
                 x = torch.cat((self.cls_token.expand(T.shape[0], -1, -1), T), dim=1) + self.pos_embedding
                 x = enc(self.dropout(x), first_only=True, seed=seed)
-            x = self.nn_same(self.nn_same(x[:, 0]))
+            ns = self.nn_same
+            x = _train_linear(_train_linear(x[:, 0], ns.weight, ns.bias), ns.weight, ns.bias)
             x = x.reshape(-1, n_agents, NetParameters.NET_SIZE)
             logits = self.policy_layer(x)
             policy = logits.softmax(dim=-1)

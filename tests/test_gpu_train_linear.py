@@ -41,6 +41,65 @@ def test_split_weight_gradient_matches_autocast_linear(rows, n_in, n_out):
           f"{_SplitKLinear.out_dtype_ok}")
 
 
+@pytest.mark.parametrize("rows,strided", [(2048, False), (2048, True), (4095, False), (77, True), (1, False)])
+def test_short_linear_matches_autocast_linear(rows, strided):
+    """net._LinearBG (the training forward's short 2-D fp16 linears via _train_linear: torch's addmm and
+    backward GEMMs, the bias gradient from mapf_colsum_f16's one-launch column sum) against autocast
+    F.linear: output bit-identical, input / weight gradients equal (the same GEMMs), the bias gradient
+    within fp16 rounding of another fp32 summation order.  strided: x is token 0 of a [rows, 17, 512]."""
+    from mapf_amd.net import _LinearBG, _train_linear
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(rows + strided)
+    xs = torch.randn(rows, 17 if strided else 1, 512, device="cuda", generator=g).half()
+    w0 = (torch.randn(512, 512, device="cuda", generator=g) / 512 ** 0.5).half()
+    b0 = (torch.randn(512, device="cuda", generator=g) * 0.1).half()
+    gy = torch.randn(rows, 512, device="cuda", generator=g).half()
+    res, calls = [], []
+    orig = _LinearBG.forward
+    try:
+        _LinearBG.forward = staticmethod(lambda ctx, *a: calls.append(1) or orig(ctx, *a))
+        for own in (True, False):
+            x3, w, b = (t.clone().requires_grad_(True) for t in (xs, w0, b0))
+            x = x3[:, 0]
+            with torch.autocast(device_type="cuda"):
+                y = _train_linear(x, w, b) if own else F.linear(x, w, b)
+            y.backward(gy)
+            res.append((y.detach(), x3.grad, w.grad, b.grad))
+    finally:
+        _LinearBG.forward = orig
+    assert calls == [1]
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=0, atol=0)
+    torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-3, atol=1e-3)
+    ref = gy.double().sum(0)
+    err_own = (res[0][3].double() - ref).abs().max().item()
+    err_torch = (res[1][3].double() - ref).abs().max().item()
+    ulp = 2 ** -10 * ref.abs().max().item()
+    assert err_own <= max(err_torch, ulp), (err_own, err_torch, ulp)
+
+
+@pytest.mark.parametrize("rows,C", [(0, 512), (1, 512), (63, 8), (2048, 512), (8192, 1536), (8193, 512), (300, 12)])
+def test_colsum_f16_matches_fp64(rows, C):
+    """mapf_colsum_f16 (one launch for rows <= 8192 with C % 8 == 0, partials + sum otherwise) against an
+    fp64 column sum: within one fp16 rounding of the fp32 sum"""
+    import ctypes
+    from mapf_amd import _lib
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(rows + C)
+    x = torch.randn(max(rows, 1), C, device="cuda", generator=g).half()[:rows]
+    out = torch.full((C,), 7.0, dtype=torch.float16, device="cuda")
+    work = torch.empty(512 * C, dtype=torch.float32, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().mapf_colsum_f16(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                          ctypes.c_void_p(work.data_ptr()), rows, C, st))
+    torch.cuda.synchronize()
+    ref = x.double().sum(0)
+    tol = 2 ** -10 * ref.abs().clamp_min(1.0) + 1e-6 * rows
+    assert ((out.double() - ref).abs() <= tol).all(), (out.double() - ref).abs().max().item()
+
+
 @pytest.mark.parametrize("rows", [34816, 2048, 35, 1])
 def test_hip_layernorm_matches_autocast_layernorm(rows):
     """net._HipLayerNorm (mapf_layernorm_f16 forward, mapf_layernorm_bwd_f16 backward) against torch's

@@ -56,11 +56,13 @@ def main():
                            sl("costValues"), sl("actions"), sl("ps"), None, sl("trainValid"), 1.0)
     import json
     if args.ab:
-        from mapf_amd.net import SCRIMPNet
-        assert isinstance(getattr(SCRIMPNet, args.ab), bool), args.ab
+        from mapf_amd import net as netmod
+        owner, attr = ((getattr(netmod, args.ab.split(".")[0]), args.ab.split(".")[1]) if "." in args.ab
+                       else (netmod.SCRIMPNet, args.ab))     # "conv3_gemm" or "_LinearBG.enabled"
+        assert isinstance(getattr(owner, attr), bool), args.ab
         ab = {}
         for on in (True, False, True, False, True, False):
-            setattr(SCRIMPNet, args.ab, on)
+            setattr(owner, attr, on)
             model._updates.clear()                 # a fresh capture with the switch in its new position
             for _ in range(3):
                 upd()
