@@ -193,11 +193,11 @@ C2, C4, C5 = (4096, 8, 20, 20, 11, 6), (1024, 16, 40, 40, 9, 6), (2048, 64, 80, 
 PMC_REPORTS = {(C2, "observe_kernel", False): "r01_pmc_observe_c2.json",
                (C2, "step_observe_kernel", False): "r01_pmc_step_observe_c2.json",
                (C2, "rollout_random_kernel<false,4>", False): "r03c_pmc_rollout_c2.json",
-               (C2, "rollout_random_kernel<true,4>", True): "r04_pmc_rollout_c2_slots.json",
+               (C2, "rollout_random_kernel<true,4>", True): "r06u_pmc_rollout_c2_slots.json",
                (C4, "rollout_wide3_kernel<u64,1,false>", False): "r03b_pmc_rollout_wide3_c4.json",
-               (C4, "rollout_wide3_kernel<u64,1,true>", True): "r04_pmc_rollout_c4_slots.json",
+               (C4, "rollout_wide3_kernel<u64,1,true>", True): "r06u_pmc_rollout_c4_slots.json",
                (C5, "rollout_wide_kernel<Row2,2,true>", False): "r03b_pmc_rollout_wide_c5.json",
-               (C5, "rollout_wide_kernel<Row2,2,true>", True): "r04_pmc_rollout_c5_slots.json"}
+               (C5, "rollout_wide_kernel<Row2,2,true>", True): "r06u_pmc_rollout_c5_slots.json"}
 
 
 def pmc_traffic_per_step(B, N, H, W, F, C, kernel, slots=False):
