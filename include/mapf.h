@@ -462,7 +462,7 @@ int mapf_tokens_layernorm_train(float *x, const float *A, const uint16_t *VV, co
 /* Its backward after LayerNorm's (mapf_layernorm_bwd_f16 with the residual's gradient as dres): given
  * dx fp32 [B][L + 1][512], the same mask: g = dx / (1 - p) where kept; dA fp32 [B][L] = sum over the
  * columns of g[.][t + 1] VV; dVV fp16 [B][512] = sum over t of g[.][t + 1] A[.][t]; dpos fp32 [L + 1][512]
- * and dcls fp32 [512] the sums of g over B (fixed order).  work: 256 * (L + 1) * 512 floats. */
+ * and dcls fp32 [512] the sums of g over B (fixed order).  work: 512 * (L + 1) * 512 floats. */
 int mapf_tokens_train_bwd(const float *dx, const float *A, const uint16_t *VV, float *dA, uint16_t *dVV, float *dpos,
                           float *dcls, float *work, int64_t B, int32_t L, float p, const uint64_t *seed_dev,
                           uint32_t salt, void *stream);

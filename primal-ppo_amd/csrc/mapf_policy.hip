@@ -56,6 +56,12 @@ __device__ inline unsigned keep4(uint64_t seed, uint64_t i, uint32_t thr) {
     return (fmix32(c) >= thr ? 1u : 0u) | (fmix32(c ^ 1u) >= thr ? 2u : 0u) | (fmix32(c ^ 2u) >= thr ? 4u : 0u) |
            (fmix32(c ^ 3u) >= thr ? 8u : 0u);
 }
+// bits k0 and k0 + 1 of keep4(seed, i, thr) (k0 in 0..2), as bits 0 and 1: the same draws, two hashes
+__device__ inline unsigned keep2(uint64_t seed, uint64_t i, uint32_t thr, unsigned k0) {
+    const uint32_t key = fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x5EEDD0u));
+    const uint32_t c = ((uint32_t)i << 2) ^ key ^ ((uint32_t)(i >> 30) * 0x9E3779B9u);
+    return (fmix32(c ^ k0) >= thr ? 1u : 0u) | (fmix32(c ^ (k0 + 1u)) >= thr ? 2u : 0u);
+}
 // the training forward's dropout seed: a counter in device memory (SCRIMPNet._train_seed) and a per-site salt
 __device__ inline uint64_t dev_seed(const uint64_t *__restrict__ p, uint32_t salt) {
     return p[0] * 0x9E3779B97F4A7C15ull + (uint64_t)salt * 0xD1B54A32D192ED03ull;
@@ -856,6 +862,7 @@ __global__ __launch_bounds__(256) void tokens_layernorm(float *__restrict__ x, c
 // separately (no contraction), the dropout as x * scale where kept -- with the mask from the device seed
 // (dev_seed: graph-safe), and z = fp16(LayerNorm(x)).  A: [B][16] fp32, VV: [B][512] fp16.
 constexpr int TOK_L = 16, TOK_T = TOK_L + 1;
+constexpr long TOK_BWD_WG = 512;                            // tokens_train_bwd's blocks at most (2 per CU)
 __device__ inline float4 token4_train(const float *__restrict__ A, const uint16_t *__restrict__ VV,
                                       const float *__restrict__ cls, const float *__restrict__ pos, long b, int t,
                                       int d4, long i, uint32_t thr, float scale, uint64_t seed) {
@@ -929,7 +936,7 @@ __device__ inline void tok_bwd_row(const float *__restrict__ dx, long b, int c0,
 #pragma unroll
         for (int t = 0; t < TOK_T; ++t) {
             const long i = (b * TOK_T + t) * 512 + c0;
-            const unsigned k = keep4(seed, (uint64_t)(i >> 2), thr) >> (c0 & 3);
+            const unsigned k = keep2(seed, (uint64_t)(i >> 2), thr, (unsigned)(c0 & 3));
             g[t].x = (k & 1u) ? __fmul_rn(g[t].x, scale) : 0.f;
             g[t].y = (k & 2u) ? __fmul_rn(g[t].y, scale) : 0.f;
         }
@@ -2135,7 +2142,7 @@ int mapf_tokens_train_bwd(const float *dx, const float *A, const uint16_t *VV, f
         !(p >= 0.f && p < 1.f) || (((uintptr_t)dx | (uintptr_t)work) & 7) || (((uintptr_t)VV | (uintptr_t)dVV) & 3))
         return MAPF_EINVAL;
     constexpr int C = pol::TOK_T * 512;
-    const long per = B > 0 ? (B + 255) / 256 : 1;
+    const long per = B > 0 ? (B + pol::TOK_BWD_WG - 1) / pol::TOK_BWD_WG : 1;   // <= TOK_BWD_WG blocks
     const int G = (int)((B + per - 1) / per);
     if (G > 0)
         hipLaunchKernelGGL(pol::tokens_train_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, dx, A, VV,

@@ -338,7 +338,7 @@ class _TokensLN(torch.autograd.Function):
         dx = torch.empty(rows, 512, dtype=torch.float32, device=dev)
         dg = torch.empty(512, dtype=torch.float32, device=dev)
         db = torch.empty(512, dtype=torch.float32, device=dev)
-        work = torch.empty(256 * 17 * 512, dtype=torch.float32, device=dev)
+        work = torch.empty(512 * 17 * 512, dtype=torch.float32, device=dev)   # mapf_tokens_train_bwd's partials
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         _lib.check(_lib.lib().mapf_layernorm_bwd_f16(ptr(x), 512, ptr(weight), ptr(dz),
