@@ -558,15 +558,17 @@ __global__ __launch_bounds__(256) void colsum_short_f16(const uint16_t *__restri
     }
 }
 
-// out[c] = fp16(sum_g part[g][c]) over G partial rows in a fixed order (8 slices x 4 chains each)
+// out[c] = fp16(sum_g part[g][c]) over G partial rows in a fixed order: a block takes 8 columns, its
+// 32 slices of the rows 4 chains each, then the slices in order (C / 8 blocks: 16 at C = 128, where
+// 32-column blocks left 4 CUs to read the partials)
 __global__ __launch_bounds__(256) void colsum_to_f16(const float *__restrict__ part, int G, int C,
                                                      uint16_t *__restrict__ out) {
-    __shared__ float sl[8][32];
-    const int t = (int)threadIdx.x, cl = t & 31, slice = t >> 5;
-    const int c = (int)blockIdx.x * 32 + cl;
+    __shared__ float sl[32][9];
+    const int t = (int)threadIdx.x, cl = t & 7, slice = t >> 3;
+    const int c = (int)blockIdx.x * 8 + cl;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (c < C) {
-        const int per = (G + 7) / 8, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
+        const int per = (G + 31) / 32, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
         int gi = g0;
         for (; gi + 4 <= g1; gi += 4) {
 #pragma unroll
@@ -578,8 +580,7 @@ __global__ __launch_bounds__(256) void colsum_to_f16(const float *__restrict__ p
     __syncthreads();
     if (slice == 0 && c < C) {
         float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v += sl[k][cl];
+        for (int k = 0; k < 32; ++k) v += sl[k][cl];
         out[c] = (uint16_t)f2h(v);
     }
 }
@@ -1898,7 +1899,7 @@ int mapf_colsum_f16(const uint16_t *g, uint16_t *out, float *work, int64_t rows,
     if (G > 0)
         hipLaunchKernelGGL(pol::colsum_partial_f16, dim3((unsigned)G, (unsigned)((C + 1023) / 1024)), dim3(256), 0,
                            (hipStream_t)stream, g, work, (long)rows, (int)C);
-    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, (hipStream_t)stream, work, G,
                        (int)C, out);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
@@ -1916,7 +1917,7 @@ int mapf_relu_bias_pool_bwd_f16(const uint16_t *r, const uint16_t *bias, const u
     if (G > 0)
         hipLaunchKernelGGL(pol::relu_bias_pool_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, r, bias, dp,
                            dr, work, (int)B, (int)H, (int)W, (int)C);
-    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, (hipStream_t)stream, work, G,
                        (int)C, dbias);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
@@ -1932,7 +1933,7 @@ int mapf_relu_bias_bwd_f16(const uint16_t *y, const uint16_t *dy, uint16_t *dx, 
     if (G > 0)
         hipLaunchKernelGGL(pol::relu_bias_bwd, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, y, dy, dx, work,
                            (long)rows, (int)C);
-    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, (hipStream_t)stream, work, G,
+    hipLaunchKernelGGL(pol::colsum_to_f16, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, (hipStream_t)stream, work, G,
                        (int)C, dbias);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
