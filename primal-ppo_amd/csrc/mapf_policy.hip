@@ -310,16 +310,16 @@ __global__ __launch_bounds__(256) void layernorm_bwd_f16(const float *__restrict
 }
 
 // column sums of the [2][G][512] partials -> dgamma, dbeta (fixed order: deterministic).  A block
-// takes 32 of the 1,024 columns; its 8 x 32 threads sum 8 slices of the G rows (4 chains each), then
-// the 8 slices are added in order.
+// takes 8 of the 1,024 columns (128 blocks); its 32 x 8 threads sum 32 slices of the G rows (4 chains
+// each), then the 32 slices are added in order.
 __global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ part, int G, float *__restrict__ dgamma,
                                                      float *__restrict__ dbeta) {
-    __shared__ float sl[8][32];
-    const int t = (int)threadIdx.x, cl = t & 31, slice = t >> 5;
-    const int i = (int)blockIdx.x * 32 + cl;               // 0 .. 1023: [gamma | beta] x 512 columns
+    __shared__ float sl[32][9];
+    const int t = (int)threadIdx.x, cl = t & 7, slice = t >> 3;
+    const int i = (int)blockIdx.x * 8 + cl;                // 0 .. 1023: [gamma | beta] x 512 columns
     const int w = i >> 9, col = i & 511;
     const float *p = part + (long)w * G * 512 + col;
-    const int per = (G + 7) / 8, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
+    const int per = (G + 31) / 32, g0 = slice * per, g1 = g0 + per < G ? g0 + per : G;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     int gi = g0;
     for (; gi + 4 <= g1; gi += 4) {
@@ -331,8 +331,7 @@ __global__ __launch_bounds__(256) void ln_bwd_colsum(const float *__restrict__ p
     __syncthreads();
     if (slice == 0) {
         float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v += sl[k][cl];
+        for (int k = 0; k < 32; ++k) v += sl[k][cl];
         (w ? dbeta : dgamma)[col] = v;
     }
 }
@@ -1948,7 +1947,7 @@ int mapf_layernorm_bwd_f16(const float *x, int64_t x_row_stride, const float *ga
     if (G > 0)
         hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x,
                            (long)x_row_stride, gamma, dz, dres, dx, work, (long)rows, eps, nullptr, 0u, 1.f, nullptr, 0u);
-    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
+    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(128), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
@@ -1964,7 +1963,7 @@ int mapf_layernorm_dropout_bwd_f16(const float *x, const float *gamma, const uin
         hipLaunchKernelGGL(pol::layernorm_bwd_f16, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x, (long)512,
                            gamma, dz, dres, dx, work, (long)rows, eps, dy, pol::drop_threshold(p), 1.f / (1.f - p),
                            seed_dev, salt);
-    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(32), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
+    hipLaunchKernelGGL(pol::ln_bwd_colsum, dim3(128), dim3(256), 0, (hipStream_t)stream, work, G, dgamma, dbeta);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
