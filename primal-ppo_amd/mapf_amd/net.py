@@ -532,7 +532,7 @@ class _SplitKLinear(torch.autograd.Function):
     (out / 64) x (in / 128) output tiles for the 34,816-deep reduction -- 32 tiles on 256 CUs for a
     512 x 512 weight (tools/profile_update.py)."""
 
-    SPLIT = 8
+    SPLIT = 16                      # 8 -> 16: -0.06 / -0.11 ms per 256 x 8 / 256 x 16 update (profiles/r06ze_ab_split*)
     MIN_ROWS = 8192                 # _train_linear takes this form from this many rows on
     out_dtype_ok = None             # torch.bmm(..., out_dtype=float32) on this build (decided once, _fp32_bmm)
 

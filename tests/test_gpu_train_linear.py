@@ -1,6 +1,6 @@
 """The training forward's split weight-gradient linear (net._SplitKLinear, used by _train_linear for
 the 17-token layers): under fp16 autocast its output, input gradient and bias gradient equal plain
-F.linear's (the same GEMMs), and its weight gradient -- eight row chunks, fp32 partial products
+F.linear's (the same GEMMs), and its weight gradient -- SPLIT (16) row chunks, fp32 partial products
 summed in fp32, rounded to fp16 -- matches autograd's one-GEMM fp16 weight gradient to fp16
 rounding (relative 2e-3 in norm, elementwise within a few fp16 ulps of the gradient's scale)."""
 import pytest

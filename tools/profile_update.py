@@ -57,11 +57,16 @@ def main():
     import json
     if args.ab:
         from mapf_amd import net as netmod
-        owner, attr = ((getattr(netmod, args.ab.split(".")[0]), args.ab.split(".")[1]) if "." in args.ab
-                       else (netmod.SCRIMPNet, args.ab))     # "conv3_gemm" or "_LinearBG.enabled"
-        assert isinstance(getattr(owner, attr), bool), args.ab
+        spec, _, vals = args.ab.partition("=")   # "conv3_gemm", "_LinearBG.enabled" or "_SplitKLinear.SPLIT=8,16"
+        owner, attr = ((getattr(netmod, spec.split(".")[0]), spec.split(".")[1]) if "." in spec
+                       else (netmod.SCRIMPNet, spec))
+        if vals:
+            choices = [type(getattr(owner, attr))(v) for v in vals.split(",")]
+        else:
+            assert isinstance(getattr(owner, attr), bool), args.ab
+            choices = [True, False]
         ab = {}
-        for on in (True, False, True, False, True, False):
+        for on in choices * 3:
             setattr(owner, attr, on)
             model._updates.clear()                 # a fresh capture with the switch in its new position
             for _ in range(3):
