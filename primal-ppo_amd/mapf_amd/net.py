@@ -593,6 +593,62 @@ class _SplitKLinear(torch.autograd.Function):
         return gx, gw, gb
 
 
+class _QKVFirst(torch.autograd.Function):
+    """The last encoder block's projections (forward_first_core) from ONE to_qkv weight [3d, d]: token 0's
+    query q = x[:, 0] W_q^T + b_q and every token's keys / values kv = x W_kv^T + b_kv, with one backward:
+    the input gradient is kv's GEMM with token 0's query gradient accumulated into its rows (addmm_), so no
+    zero-filled [b, n, d] select gradient and no add; the weight and bias gradients are written into one
+    [3d, d] / [3d] tensor, so no zero-filled slice gradients and adds either.  kv's weight gradient is
+    _SplitKLinear's (split-K, fp32 partials, rounded to fp16), q's one GEMM; the bias gradients
+    mapf_colsum_f16.  x: fp16 [b, n, d] contiguous; w, b fp16 (the training forward's _CastParams copies)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        d = x.shape[-1]
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b[:d], x[:, 0], w[:d].t()), F.linear(x, w[d:], b[d:])
+
+    @staticmethod
+    def backward(ctx, dq, dkv):
+        from . import _lib
+        x, w = ctx.saved_tensors
+        B, n, d = x.shape
+        dev = x.device
+        x2 = x.reshape(-1, d)
+        dq = torch.zeros(B, d, dtype=x.dtype, device=dev) if dq is None else dq.contiguous()
+        dkv2 = (torch.zeros(B * n, 2 * d, dtype=x.dtype, device=dev) if dkv is None else dkv.reshape(-1, 2 * d)
+                .contiguous())
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (dkv2 @ w[d:]).view(B, n, d)
+            gx[:, 0].addmm_(dq, w[:d])
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty(3 * d, d, dtype=torch.float16, device=dev)
+            torch.mm(dq.t(), x[:, 0], out=gw[:d])
+            S = _SplitKLinear.SPLIT
+            R = dkv2.shape[0]
+            parts = None
+            if R % S == 0:
+                a, c = dkv2.view(S, R // S, 2 * d).transpose(1, 2), x2.view(S, R // S, d)
+                parts = _SplitKLinear._fp32_bmm(a, c)
+                if parts is None:
+                    parts = torch.bmm(a, c).float()
+            if parts is not None:
+                gw[d:].copy_(parts.sum(0))
+            else:
+                torch.mm(dkv2.t(), x2, out=gw[d:])
+            gw = gw.to(w.dtype)
+        if ctx.needs_input_grad[2]:
+            gb = torch.empty(3 * d, dtype=torch.float16, device=dev)
+            work = torch.empty(512 * 2 * d, dtype=torch.float32, device=dev)
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for g2, lo, C in ((dq, 0, d), (dkv2, d, 2 * d)):
+                _lib.check(_lib.lib().mapf_colsum_f16(ctypes.c_void_p(g2.data_ptr()),
+                                                      ctypes.c_void_p(gb.data_ptr() + 2 * lo),
+                                                      ctypes.c_void_p(work.data_ptr()), g2.shape[0], C, st))
+        return gx, gw, gb
+
+
 class _LinearBG(torch.autograd.Function):
     """F.linear(x, w, b) on fp16 operands for the training forward's short linears (token 0's and the
     fully connected layers: 2-D, rows < _SplitKLinear.MIN_ROWS): the same addmm forward and the same
@@ -660,6 +716,7 @@ class _SelfAttention(nn.Module):
         self.do1 = nn.Dropout(dropout)
 
     hip_attention = True               # the training forward's attention on _HipAttention (GPU, fp16)
+    qkv_first = True                   # the last block's q / kv projections and their backward as _QKVFirst
 
     def _hip(self, x, t):
         return (self.hip_attention and x.is_cuda and t.dtype == torch.float16 and self.heads == 16 and
@@ -690,8 +747,13 @@ class _SelfAttention(nn.Module):
         h = self.heads
         w, bias = self.to_qkv.weight, self.to_qkv.bias
         # x[:, 0] is a 2-D strided view: one GEMM with lda = n*d ([b, 1, d] would run as a slow bmm)
-        q = _train_linear(x[:, 0], w[:d], bias[:d])
-        kv = _train_linear(x, w[d:], bias[d:])
+        if (self.qkv_first and torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda") and
+                x.dtype == w.dtype == bias.dtype == torch.float16 and x.is_contiguous() and d % 8 == 0 and
+                w.requires_grad and b * n >= _SplitKLinear.MIN_ROWS):
+            q, kv = _QKVFirst.apply(x, w, bias)
+        else:
+            q = _train_linear(x[:, 0], w[:d], bias[:d])
+            kv = _train_linear(x, w[d:], bias[d:])
         if self._hip(x, q):
             att = _HipAttention.apply(q.contiguous(), kv.contiguous(), 1, 0, 0, d, self.scale)
             return _train_linear(att.reshape(b, d), self.nn1.weight, self.nn1.bias).view(b, 1, d)

@@ -79,6 +79,41 @@ def test_short_linear_matches_autocast_linear(rows, strided):
     assert err_own <= max(err_torch, ulp), (err_own, err_torch, ulp)
 
 
+@pytest.mark.parametrize("b", [512, 2048])
+def test_qkv_first_matches_two_linears(b):
+    """net._QKVFirst (the last block's token-0 query and all-token keys / values from one to_qkv weight, one
+    backward) against the two _train_linear calls it replaces (a _LinearBG on x[:, 0] and a _SplitKLinear on
+    x): q and kv bit-identical; kv's weight and both bias gradients equal (the same kernels); x's gradient and
+    q's weight gradient within fp16 rounding (token 0's rows: one fused accumulate instead of an fp16 add)"""
+    from mapf_amd.net import _QKVFirst, _train_linear
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    n, d = 17, 512
+    g = torch.Generator(device="cuda").manual_seed(b)
+    x0 = torch.randn(b, n, d, device="cuda", generator=g).half()
+    w0 = (torch.randn(3 * d, d, device="cuda", generator=g) / d ** 0.5).half()
+    b0 = (torch.randn(3 * d, device="cuda", generator=g) * 0.1).half()
+    dq = torch.randn(b, d, device="cuda", generator=g).half()
+    dkv = torch.randn(b, n, 2 * d, device="cuda", generator=g).half()
+    res = []
+    for fused in (True, False):
+        x, w, bb = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        with torch.autocast(device_type="cuda"):
+            if fused:
+                q, kv = _QKVFirst.apply(x, w, bb)
+            else:
+                q, kv = _train_linear(x[:, 0], w[:d], bb[:d]), _train_linear(x, w[d:], bb[d:])
+        torch.autograd.backward([q, kv], [dq, dkv])
+        res.append((q.detach(), kv.detach(), x.grad, w.grad, bb.grad))
+    (qf, kvf, gxf, gwf, gbf), (qr, kvr, gxr, gwr, gbr) = res
+    assert torch.equal(qf, qr) and torch.equal(kvf, kvr)
+    assert torch.equal(gwf[d:], gwr[d:]) and torch.equal(gbf, gbr)
+    for a, r in ((gxf, gxr), (gwf[:d], gwr[:d])):
+        rel = ((a.float() - r.float()).norm() / r.float().norm()).item()
+        assert rel < 2e-3, rel
+    assert torch.equal(gxf[:, 1:], gxr[:, 1:])
+
+
 @pytest.mark.parametrize("rows,C", [(0, 512), (1, 512), (63, 8), (2048, 512), (8192, 1536), (8193, 512), (300, 12)])
 def test_colsum_f16_matches_fp64(rows, C):
     """mapf_colsum_f16 (one launch for rows <= 8192 with C % 8 == 0, partials + sum otherwise) against an
