@@ -9,7 +9,8 @@ mkdir -p gpurun_out/tune
 export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1
 export PYTORCH_TUNABLEOP_FILENAME=$PWD/gpurun_out/tune/tunableop_results.csv
 # KEEP=1: start from the shipped results, so only shapes missing from them are benchmarked
-if [ -n "${KEEP:-}" ]; then cp primal-ppo_amd/mapf_amd/tunableop_gfx950.csv "$PYTORCH_TUNABLEOP_FILENAME"; fi
+# (TunableOp appends the device ordinal to the file name: results0.csv on device 0)
+if [ -n "${KEEP:-}" ]; then cp primal-ppo_amd/mapf_amd/tunableop_gfx950.csv "${PYTORCH_TUNABLEOP_FILENAME%.csv}0.csv"; fi
 timeout -k 10 500 python3 -u tools/bench_rollout.py --train --updates 4 --update-warmup 3 > gpurun_out/tune/c3.log 2>&1 \
   || { echo "c3 rc=$?"; tail -5 gpurun_out/tune/c3.log; exit 1; }
 timeout -k 10 500 python3 -u tools/bench_rollout.py --envs 1024 --agents 16 --size 40 --train --updates 4 --update-warmup 3 \
