@@ -406,6 +406,20 @@ int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, co
  * is not a multiple of Cout ks ks. */
 int mapf_cast_f32_to_f16_multi_flip(const float *const *src, uint16_t *const *dst, const int64_t *n,
                                     const int32_t *cout, const int32_t *ks, int32_t count, void *stream);
+/* The PPO update's optimizer tail (model._DeviceUpdate._back, model.py:177-185 of the reference: GradScaler
+ * unscale_, clip_grad_norm_(10), Adam step, for torch.optim.Adam(fused, capturable) state): for `count`
+ * fp32 tensors p[i], their gradients g[i], Adam moments m[i], v[i] (all four of one dense layout, n[i]
+ * elements) and step counters steps[i] (fp32 scalars, equal): found_inf = 1 if any gradient is non-finite
+ * (the caller zeroes it first); grad_norm = the 2-norm of g / scale over every tensor; unless found_inf:
+ * g' = (g / scale) * min(max_norm / (grad_norm + 1e-6), 1), Adam with step = steps + 1 (no weight decay,
+ * no amsgrad), steps += 1; g' is written back to g (found_inf or not: torch's unscale_ + clip leave it
+ * so).  scale: the loss scale, fp32 in device memory.  work:
+ * work_floats >= sum over tensors of ceil(n / 8192) floats of scratch.  Three kernel kinds, no host
+ * synchronisation, no memset: capturable.  Pointer arrays are host arrays of device pointers. */
+int mapf_optim_unscale_clip_adam(float *const *p, float *const *g, float *const *m, float *const *v,
+                                 const int64_t *n, float *const *steps, int32_t count, const float *scale,
+                                 float max_norm, float lr, float beta1, float beta2, float eps, float *found_inf,
+                                 float *grad_norm, float *work, int64_t work_floats, void *stream);
 /* Backward of z = fp16(LayerNorm(x)) (mapf_layernorm_f16; the training forward's PreNorm,
  * transformer.py:7-24 under autocast): given dz fp16 [rows][512], dx fp32 [rows][512] (contiguous),
  * dgamma / dbeta fp32 [512] (sums over the rows, fixed order).  mean / rstd are recomputed from x as

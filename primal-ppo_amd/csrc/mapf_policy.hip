@@ -23,6 +23,7 @@
 // inverted dropout); the mask bits come from a counter hash (keep4: murmur3's finaliser of
 // the element index, keyed by `seed`) -- a different stream than torch's own generator; the
 // reference's masks are random anyway (the net is never eval()-ed, net.py:50-51).
+#include <vector>
 #include <hip/hip_fp16.h>
 
 #include "mapf.h"
@@ -645,6 +646,116 @@ static int cast_multi_api(const void *const *src, void *const *dst, const int64_
     if (blocks == 0) return MAPF_OK;
     hipLaunchKernelGGL(cast_multi<TO_F16>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L);
     return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
+}
+
+// ---- the update's optimizer tail (model._DeviceUpdate._back): AMP unscale + found-inf, the grad-norm
+// clip and Adam in three launches over up to OPT_MAX fp32 tensors each, in place of torch's unscale,
+// foreach-norm, stack / norm / clamp, foreach-mul and fused-Adam passes.  p, g, m, v of a tensor share
+// one dense layout, so element k of each is the same parameter entry.
+constexpr int OPT_MAX = 64, OPT_PER_BLOCK = 8192;
+struct OptList {
+    float *p[OPT_MAX];
+    float *g[OPT_MAX];
+    float *m[OPT_MAX];
+    float *v[OPT_MAX];
+    long n[OPT_MAX];
+    int blk0[OPT_MAX + 1];                                  // first block of tensor i; blk0[count] = the chunk's grid
+    int count;
+};
+__device__ inline int opt_tensor(const OptList &L, int b) {
+    int t = 0;
+    while (t + 1 < L.count && L.blk0[t + 1] <= b) ++t;      // uniform scan over <= 64 entries
+    return t;
+}
+__device__ inline float opt_inv_scale(const float *scale) { return (float)(1.0 / (double)scale[0]); }
+
+// pass 1: per block, the sum of squares of the unscaled gradients (fp32, the block's elements in a
+// fixed order) -> part[part0 + block]; any non-finite gradient sets found_inf = 1
+__global__ __launch_bounds__(256) void optim_sumsq(OptList L, const float *__restrict__ scale, float *__restrict__ part,
+                                                   int part0, float *__restrict__ found_inf) {
+    __shared__ float red[4];
+    __shared__ int bad;
+    const int b = (int)blockIdx.x, t = opt_tensor(L, b);
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const float inv = opt_inv_scale(scale);
+    const long base = (long)(b - L.blk0[t]) * OPT_PER_BLOCK, n = L.n[t];
+    float acc = 0.f;
+    bool nf = false;
+    for (int e = (int)threadIdx.x; e < OPT_PER_BLOCK; e += 256) {
+        const long i = base + e;
+        if (i >= n) break;
+        const float g = L.g[t][i];
+        nf |= !isfinite(g);
+        const float u = g * inv;
+        acc += u * u;
+    }
+    if (nf) bad = 1;
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[part0 + b] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (bad) found_inf[0] = 1.f;
+    }
+}
+
+// the total gradient norm from the G partials, in one fixed order (every block computes the same value)
+__device__ inline float opt_total_norm(const float *__restrict__ part, int G) {
+    __shared__ float red[4];
+    float a = 0.f;
+    for (int k = (int)threadIdx.x; k < G; k += 256) a += part[k];
+    a = wave_sum(a);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return sqrtf(tot);
+}
+
+// pass 2: g' = (g / scale) * min(max_norm / (norm + 1e-6), 1) (torch's unscale_ then clip_grad_norm_'s
+// in-place scaling, two roundings), written back to g as torch leaves it; then, unless found_inf, torch's
+// fused Adam step (no weight decay, no amsgrad) with step = the stored step + 1.  Block 0 writes the norm.
+__global__ __launch_bounds__(256) void optim_adam(OptList L, const float *__restrict__ part, int G,
+                                                  const float *__restrict__ scale, const float *__restrict__ found_inf,
+                                                  const float *__restrict__ step, float max_norm, float lr, float beta1,
+                                                  float beta2, float eps, float *__restrict__ grad_norm) {
+    const int b = (int)blockIdx.x, t = opt_tensor(L, b);
+    const float norm = opt_total_norm(part, G);
+    if (b == 0 && threadIdx.x == 0 && grad_norm) grad_norm[0] = norm;
+    const float inv = opt_inv_scale(scale);
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+    const long base0 = (long)(b - L.blk0[t]) * OPT_PER_BLOCK, n0 = L.n[t];
+    if (found_inf[0] != 0.f) {                              // the step is skipped; g as torch leaves it
+        for (int e = (int)threadIdx.x; e < OPT_PER_BLOCK && base0 + e < n0; e += 256)
+            L.g[t][base0 + e] = (L.g[t][base0 + e] * inv) * coef;
+        return;
+    }
+    const float s = step[0] + 1.f;
+    const float bc1 = 1.f - powf(beta1, s), bc2s = sqrtf(1.f - powf(beta2, s));
+    const float step_size = lr / bc1;
+    const long base = (long)(b - L.blk0[t]) * OPT_PER_BLOCK, n = L.n[t];
+    for (int e = (int)threadIdx.x; e < OPT_PER_BLOCK; e += 256) {
+        const long i = base + e;
+        if (i >= n) break;
+        const float g = (L.g[t][i] * inv) * coef;
+        L.g[t][i] = g;
+        const float m = beta1 * L.m[t][i] + (1.f - beta1) * g;
+        const float v = beta2 * L.v[t][i] + (1.f - beta2) * g * g;
+        L.m[t][i] = m;
+        L.v[t][i] = v;
+        L.p[t][i] -= step_size * m / (sqrtf(v) / bc2s + eps);
+    }
+}
+
+// pass 3: every tensor's step += 1 unless found_inf (torch's capturable Adam keeps one per parameter)
+struct OptSteps {
+    float *s[OPT_MAX];
+    int count;
+};
+__global__ void optim_steps(OptSteps S, const float *__restrict__ found_inf) {
+    const int i = (int)threadIdx.x;
+    if (i < S.count && found_inf[0] == 0.f) S.s[i][0] += 1.f;
 }
 
 // ---- dropout epilogues -----------------------------------------------------------
@@ -1876,6 +1987,54 @@ int mapf_cast_f32_to_f16_multi_flip(const float *const *src, uint16_t *const *ds
     if (!cout || !ks) return MAPF_EINVAL;
     return pol::cast_multi_api<true>(reinterpret_cast<const void *const *>(src), reinterpret_cast<void *const *>(dst),
                                      n, count, stream, cout, ks);
+}
+
+int mapf_optim_unscale_clip_adam(float *const *p, float *const *g, float *const *m, float *const *v,
+                                 const int64_t *n, float *const *steps, int32_t count, const float *scale,
+                                 float max_norm, float lr, float beta1, float beta2, float eps, float *found_inf,
+                                 float *grad_norm, float *work, int64_t work_floats, void *stream) {
+    if (!p || !g || !m || !v || !n || !steps || !scale || !found_inf || !work || count <= 0) return MAPF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    // the chunks of <= OPT_MAX tensors and their blocks (partials for every chunk in one array)
+    std::vector<pol::OptList> chunks;
+    long G = 0;
+    for (int c0 = 0; c0 < count; c0 += pol::OPT_MAX) {
+        pol::OptList L{};
+        L.count = count - c0 < pol::OPT_MAX ? count - c0 : pol::OPT_MAX;
+        long blocks = 0;
+        for (int k = 0; k < L.count; ++k) {
+            const int i = c0 + k;
+            if (n[i] <= 0 || !p[i] || !g[i] || !m[i] || !v[i] || !steps[i]) return MAPF_EINVAL;
+            L.p[k] = p[i];
+            L.g[k] = g[i];
+            L.m[k] = m[i];
+            L.v[k] = v[i];
+            L.n[k] = (long)n[i];
+            L.blk0[k] = (int)blocks;
+            blocks += (n[i] + pol::OPT_PER_BLOCK - 1) / pol::OPT_PER_BLOCK;
+        }
+        L.blk0[L.count] = (int)blocks;
+        G += blocks;
+        chunks.push_back(L);
+    }
+    if (G > work_floats || G > (1L << 24)) return MAPF_EINVAL;
+    long off = 0;
+    for (const auto &L : chunks) {
+        hipLaunchKernelGGL(pol::optim_sumsq, dim3((unsigned)L.blk0[L.count]), dim3(256), 0, s, L, scale, work, (int)off,
+                           found_inf);
+        off += L.blk0[L.count];
+    }
+    for (size_t k = 0; k < chunks.size(); ++k)
+        hipLaunchKernelGGL(pol::optim_adam, dim3((unsigned)chunks[k].blk0[chunks[k].count]), dim3(256), 0, s,
+                           chunks[k], work, (int)G, scale, found_inf, steps[0], max_norm, lr, beta1, beta2, eps,
+                           k == 0 ? grad_norm : nullptr);
+    for (int c0 = 0; c0 < count; c0 += pol::OPT_MAX) {
+        pol::OptSteps S{};
+        S.count = count - c0 < pol::OPT_MAX ? count - c0 : pol::OPT_MAX;
+        for (int k = 0; k < S.count; ++k) S.s[k] = steps[c0 + k];
+        hipLaunchKernelGGL(pol::optim_steps, dim3(1), dim3(64), 0, s, S, found_inf);
+    }
+    return hipGetLastError() == hipSuccess ? MAPF_OK : MAPF_EDEVICE;
 }
 
 int mapf_cast_f16_to_f32_multi(const uint16_t *const *src, float *const *dst, const int64_t *n, int32_t count,

@@ -104,6 +104,8 @@ SIGNATURES = {
     "mapf_cast_f32_to_f16_multi_flip": (ctypes.c_int, [P, P, P, P, P, I32, P]),
     "mapf_tokens_layernorm_train": (ctypes.c_int, [P, P, P, P, P, I64, I32, F32, P, U32, P, P, F32, P, P]),
     "mapf_tokens_train_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, I32, F32, P, U32, P]),
+    "mapf_optim_unscale_clip_adam": (ctypes.c_int, [P, P, P, P, P, P, I32, P, F32, F32, F32, F32, F32, P, P, P,
+                                                    I64, P]),
     "mapf_cast_f16_to_f32_multi": (ctypes.c_int, [P, P, P, I32, P]),
     "mapf_layernorm_bwd_f16": (ctypes.c_int, [P, I64, P, P, P, P, P, P, P, I64, I32, ctypes.c_float, P]),
     "mapf_layernorm_dropout_bwd_f16": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64, I32, F32, F32, P, U32, P]),

@@ -146,6 +146,9 @@ class Model:
         self._flat = None
         self.fused_loss = True        # GPU: the loss terms + their gradient in one launch (_FusedPPOLoss)
         self.graph_update = True      # GPU: the update replayed from captured hipGraphs (_DeviceUpdate)
+        # GPU: unscale + clip + Adam as mapf_optim_unscale_clip_adam (_DeviceUpdate._fused_tail) instead of torch's
+        # passes: tested equal, but not faster in its current form (profiles/r06zk_ab_optim*.txt), so off
+        self.fused_optim = False
         self.distributed_update = None  # None: the all-reduced update when world size > 1; True / False: forced
         self._updates = {}
         if global_model:
@@ -465,17 +468,72 @@ class _DeviceUpdate:
                 off += p.numel()
         params = [p for p in net.parameters() if p.grad is not None]
         self.found_inf.zero_()
-        torch._amp_foreach_non_finite_check_and_unscale_([p.grad for p in params], self.found_inf,
-                                                         self.scale.double().reciprocal().float())
-        grad_norm = torch.nn.utils.clip_grad_norm_(params, T.MAX_GRAD_NORM)
-        opt.grad_scale, opt.found_inf = None, self.found_inf     # fused Adam: skipped on the device when inf
-        opt.step()
-        opt.grad_scale = opt.found_inf = None
+        if self._fused_tail_ok(opt, params):
+            grad_norm = self._fused_tail(opt, params)
+        else:
+            torch._amp_foreach_non_finite_check_and_unscale_([p.grad for p in params], self.found_inf,
+                                                             self.scale.double().reciprocal().float())
+            grad_norm = torch.nn.utils.clip_grad_norm_(params, T.MAX_GRAD_NORM)
+            opt.grad_scale, opt.found_inf = None, self.found_inf     # fused Adam: skipped on the device when inf
+            opt.step()
+            opt.grad_scale = opt.found_inf = None
         torch._amp_update_scale_(self.scale, self.growth, self.found_inf, *self.amp)
         all_loss, terms, adv, cadv = self.live
         self.stats.copy_(torch.stack([t.detach().float().reshape(()) for t in (
             all_loss, terms[0], terms[1], terms[2], terms[3], terms[4], terms[5], terms[6], grad_norm,
             torch.mean(adv), torch.mean(cadv))]))
+
+    def _fused_tail_ok(self, opt, params):
+        """the optimizer tail can run as mapf_optim_unscale_clip_adam: Model.fused_optim, one plain Adam group
+        (no weight decay / amsgrad / maximize), fp32 CUDA parameters whose gradients share their dense layout"""
+        if not (self.model.fused_optim and isinstance(opt, torch.optim.Adam) and len(opt.param_groups) == 1 and
+                params):
+            return False
+        grp = opt.param_groups[0]
+        if grp["weight_decay"] or grp["amsgrad"] or grp.get("maximize") or len(grp["params"]) != len(params):
+            return False
+        from .net import _CastParams
+
+        def state_ok(p):          # none yet, or torch's fused / capturable layout (device fp32 step, moments like p)
+            st = opt.state.get(p, {})
+            if not st:
+                return True
+            return (set(st) == {"step", "exp_avg", "exp_avg_sq"} and st["step"].is_cuda and
+                    st["step"].dtype == torch.float32 and st["step"].numel() == 1 and
+                    all(st[k].dtype == torch.float32 and st[k].stride() == p.stride() for k in ("exp_avg", "exp_avg_sq")))
+        return all(p.is_cuda and p.dtype == torch.float32 and p.grad is not None and p.grad.dtype == torch.float32
+                   and p.grad.stride() == p.stride() and _CastParams.dense(p) and state_ok(p) for p in params)
+
+    def _fused_tail(self, opt, params):
+        """unscale + found-inf, clip_grad_norm_(MAX_GRAD_NORM) and the Adam step in three launches
+        (mapf_optim_unscale_clip_adam) on the optimizer's own state, which it creates as torch's
+        fused / capturable Adam does (zero moments, a zero fp32 step per parameter); returns the grad norm
+        (a device scalar)"""
+        from . import _lib
+        grp = opt.param_groups[0]
+        for p in params:
+            st = opt.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        k = len(params)
+        arr = lambda ts: (ctypes.c_void_p * k)(*[t.data_ptr() for t in ts])  # noqa: E731
+        sts = [opt.state[p] for p in params]
+        blocks = sum((p.numel() + 8191) // 8192 for p in params)
+        if getattr(self, "_tail_work", None) is None or self._tail_work.numel() < blocks:
+            self._tail_work = torch.empty(blocks, dtype=torch.float32, device=params[0].device)
+            self._tail_norm = torch.empty((), dtype=torch.float32, device=params[0].device)
+        b1, b2 = grp["betas"]
+        st = ctypes.c_void_p(torch.cuda.current_stream(params[0].device).cuda_stream)
+        _lib.check(_lib.lib().mapf_optim_unscale_clip_adam(
+            arr(params), arr([p.grad for p in params]), arr([x["exp_avg"] for x in sts]),
+            arr([x["exp_avg_sq"] for x in sts]), (ctypes.c_int64 * k)(*[p.numel() for p in params]),
+            arr([x["step"] for x in sts]), k, ctypes.c_void_p(self.scale.data_ptr()),
+            float(TrainingParameters.MAX_GRAD_NORM), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+            ctypes.c_void_p(self.found_inf.data_ptr()), ctypes.c_void_p(self._tail_norm.data_ptr()),
+            ctypes.c_void_p(self._tail_work.data_ptr()), self._tail_work.numel(), st))
+        return self._tail_norm
 
     def _moments(self):
         """eager, before segment A: the global advantage statistics (two all-reduced moment passes)"""

@@ -4,6 +4,8 @@ restated in torch below), ties and clamp boundaries included, and a whole Model.
 update fused vs unfused from the same state."""
 import copy
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -124,3 +126,61 @@ def test_model_update_fused_equals_unfused():
     # there (2.04 % measured on one box, MIOpen's backward algorithm varies per box)
     for p1, p2 in pairs:
         assert ((p1.grad - p2.grad).norm() / p2.grad.norm().clamp_min(1e-30)).item() < 5e-2
+
+
+@pytest.mark.parametrize("inf", [False, True])
+def test_fused_optimizer_tail_matches_torch(inf):
+    """_DeviceUpdate._fused_tail (mapf_optim_unscale_clip_adam: unscale + found-inf, clip_grad_norm_(10),
+    Adam) against torch's path (_amp_foreach_non_finite_check_and_unscale_, clip_grad_norm_, fused
+    capturable Adam with found_inf) over three steps on the same tensors (a channels_last conv weight
+    among them): parameters, moments and the unscaled clipped gradients within fp32 rounding of a
+    different summation / contraction order, steps and the grad norm equal to fp32 rounding; with an inf
+    gradient in the second step, that step is skipped by both (parameters, moments, step unchanged)"""
+    import types
+    from mapf_amd.config import TrainingParameters
+    from mapf_amd.model import _DeviceUpdate
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    shapes = [(128, 6, 3, 3), (128,), (512, 512), (5, 512), (5,), (1536, 512), (7,)]
+    base = [torch.randn(s, device="cuda", generator=g) * 0.1 for s in shapes]
+    base[0] = base[0].contiguous(memory_format=torch.channels_last)
+    grads = [[torch.randn(s, device="cuda", generator=g).contiguous(memory_format=torch.channels_last
+             if len(s) == 4 else torch.contiguous_format) * (2.0 ** 8) * 0.02 for s in shapes] for _ in range(3)]
+    if inf:
+        grads[1][2][3, 4] = float("inf")
+    res = []
+    for fused in (True, False):
+        ps = [torch.nn.Parameter(b.clone()) for b in base]
+        opt = torch.optim.Adam(ps, lr=TrainingParameters.lr, fused=True, capturable=True)
+        scale = torch.full((1,), 2.0 ** 8, device="cuda")
+        found = torch.zeros((), device="cuda")
+        ns = types.SimpleNamespace(model=types.SimpleNamespace(fused_optim=True), scale=scale, found_inf=found)
+        norms, founds = [], []
+        for step in range(3):
+            for p, gr in zip(ps, grads[step]):
+                p.grad = gr.clone()
+            found.zero_()
+            if fused:
+                assert _DeviceUpdate._fused_tail_ok(ns, opt, ps)
+                norm = _DeviceUpdate._fused_tail(ns, opt, ps).clone()
+            else:
+                torch._amp_foreach_non_finite_check_and_unscale_([p.grad for p in ps], found,
+                                                                 scale.double().reciprocal().float())
+                norm = torch.nn.utils.clip_grad_norm_(ps, TrainingParameters.MAX_GRAD_NORM)
+                opt.grad_scale, opt.found_inf = None, found
+                opt.step()
+                opt.grad_scale = opt.found_inf = None
+            norms.append(norm.item())
+            founds.append(found.item())
+        st = [opt.state[p] for p in ps]
+        res.append(([p.detach() for p in ps], [x["exp_avg"] for x in st], [x["exp_avg_sq"] for x in st],
+                    [x["step"].item() for x in st], [p.grad for p in ps], norms, founds))
+    (pf, mf, vf, sf, gf, nf, ff), (pt, mt, vt, stt, gt, nt, ft) = res
+    assert ff == ft == ([0.0, 1.0, 0.0] if inf else [0.0, 0.0, 0.0])
+    assert sf == stt == [2.0 if inf else 3.0] * len(shapes)
+    np.testing.assert_allclose(nf, nt, rtol=1e-5)
+    for a, b in zip(pf + mf + vf, pt + mt + vt):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=1e-9)
+    for a, b in zip(gf, gt):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=1e-9, equal_nan=True)

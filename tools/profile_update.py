@@ -58,8 +58,9 @@ def main():
     if args.ab:
         from mapf_amd import net as netmod
         spec, _, vals = args.ab.partition("=")   # "conv3_gemm", "_LinearBG.enabled" or "_SplitKLinear.SPLIT=8,16"
-        owner, attr = ((getattr(netmod, spec.split(".")[0]), spec.split(".")[1]) if "." in spec
-                       else (netmod.SCRIMPNet, spec))
+        head, _, tail = spec.partition(".")
+        owner, attr = ((model, tail) if head == "model" else      # "model.fused_optim": the Model instance's
+                       (getattr(netmod, head), tail) if tail else (netmod.SCRIMPNet, spec))
         if vals:
             choices = [type(getattr(owner, attr))(v) for v in vals.split(",")]
         else:
