@@ -682,13 +682,19 @@ __global__ __launch_bounds__(256) void optim_sumsq(OptList L, const float *__res
     const long base = (long)(b - L.blk0[t]) * OPT_PER_BLOCK, n = L.n[t];
     float acc = 0.f;
     bool nf = false;
-    for (int e = (int)threadIdx.x; e < OPT_PER_BLOCK; e += 256) {
-        const long i = base + e;
-        if (i >= n) break;
-        const float g = L.g[t][i];
-        nf |= !isfinite(g);
-        const float u = g * inv;
-        acc += u * u;
+    for (int e0 = (int)threadIdx.x; e0 < OPT_PER_BLOCK; e0 += 4 * 256) {   // four independent loads in flight
+        float gv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long i = base + e0 + u * 256;
+            gv[u] = (e0 + u * 256 < OPT_PER_BLOCK && i < n) ? L.g[t][i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            nf |= !isfinite(gv[u]);
+            const float x = gv[u] * inv;
+            acc += x * x;
+        }
     }
     if (nf) bad = 1;
     acc = wave_sum(acc);
@@ -735,16 +741,30 @@ __global__ __launch_bounds__(256) void optim_adam(OptList L, const float *__rest
     const float bc1 = 1.f - powf(beta1, s), bc2s = sqrtf(1.f - powf(beta2, s));
     const float step_size = lr / bc1;
     const long base = (long)(b - L.blk0[t]) * OPT_PER_BLOCK, n = L.n[t];
-    for (int e = (int)threadIdx.x; e < OPT_PER_BLOCK; e += 256) {
-        const long i = base + e;
-        if (i >= n) break;
-        const float g = (L.g[t][i] * inv) * coef;
-        L.g[t][i] = g;
-        const float m = beta1 * L.m[t][i] + (1.f - beta1) * g;
-        const float v = beta2 * L.v[t][i] + (1.f - beta2) * g * g;
-        L.m[t][i] = m;
-        L.v[t][i] = v;
-        L.p[t][i] -= step_size * m / (sqrtf(v) / bc2s + eps);
+    for (int e0 = (int)threadIdx.x; e0 < OPT_PER_BLOCK; e0 += 4 * 256) {   // four entries' loads in flight
+        float gv[4], mv[4], vv[4], pv[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long i = base + e0 + u * 256;
+            ok[u] = e0 + u * 256 < OPT_PER_BLOCK && i < n;
+            gv[u] = ok[u] ? L.g[t][i] : 0.f;
+            mv[u] = ok[u] ? L.m[t][i] : 0.f;
+            vv[u] = ok[u] ? L.v[t][i] : 0.f;
+            pv[u] = ok[u] ? L.p[t][i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!ok[u]) continue;
+            const long i = base + e0 + u * 256;
+            const float g = (gv[u] * inv) * coef;
+            const float m = beta1 * mv[u] + (1.f - beta1) * g;
+            const float v = beta2 * vv[u] + (1.f - beta2) * g * g;
+            L.g[t][i] = g;
+            L.m[t][i] = m;
+            L.v[t][i] = v;
+            L.p[t][i] = pv[u] - step_size * m / (sqrtf(v) / bc2s + eps);
+        }
     }
 }
 
